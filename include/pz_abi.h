@@ -1,0 +1,202 @@
+/*
+ * pz_abi.h -- C ABI of the MI355X-native Pi0 hot path (libpizero_hip.so).
+ *
+ * Every entry point takes raw device pointers, int64 sizes/strides and a
+ * hipStream_t passed as `void* stream`; it enqueues work on that stream only
+ * (no device syncs, no hipMalloc/hipFree -> legal inside hipGraph capture) and
+ * returns 0 (PZ_OK) or a PZ_ERR_* code; pz_last_error() then holds a
+ * thread-local message.  All tensors are owned by the caller.  bf16 tensors
+ * are raw 16-bit storage.  Nothing here knows about torch.
+ *
+ * The reference (shroglck/open-pi-zero) has no native code: each entry point
+ * replaces the PyTorch/ATen ops at the cited reference sites (file:line in
+ * the reference tree).
+ */
+#ifndef PZ_ABI_H
+#define PZ_ABI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PZ_ABI_VERSION 1
+
+enum {
+  PZ_OK = 0,
+  PZ_ERR_INVALID_ARG = 1,
+  PZ_ERR_LAUNCH = 2,
+  PZ_ERR_UNSUPPORTED = 3,
+};
+
+/* GEMM epilogues */
+enum {
+  PZ_EPI_NONE = 0,  /* C = alpha*acc (+bias[n]) (+resid[m,n]) (+C if beta_accum)       */
+  PZ_EPI_GELU = 1,  /* pre = alpha*acc + bias; aux = pre; C = gelu_tanh(pre) (+resid)   */
+  PZ_EPI_GEGLU = 2, /* B = [gate; up] (N = 2I); aux = [g | u]; C[m,n] = gelu(g)*u        */
+  PZ_EPI_SILU = 3,  /* pre = alpha*acc + bias; aux = pre; C = silu(pre)                  */
+};
+
+/*
+ * bf16 MFMA GEMM:  C[z](m,n) = epi(alpha * sum_k A[z](m,k) B[z](k,n))
+ *   A(m,k) = A[m*lda + k] if a_kcontig else A[k*lda + m]
+ *   B(k,n) = B[n*ldb + k] if b_kcontig else B[k*ldb + n]   (b_kcontig = nn.Linear weight)
+ *   C(m,n) = C[m*ldc + n]  (bf16, or fp32 if c_fp32)
+ *   batch z in [0,batch): operand offset = (z / batch_inner)*s_outer + (z % batch_inner)*s_inner
+ * Replaces every nn.Linear / torch.matmul on the path: siglip.py:103-106,164,183-192,22-30;
+ * mixture.py:162-218; paligemma/modules.py:86-95; joint_model.py:261,282; vla/modules.py:39-53.
+ */
+typedef struct pz_gemm_args {
+  int64_t M, N, K;
+  const void* A; int64_t lda; int32_t a_kcontig;
+  const void* B; int64_t ldb; int32_t b_kcontig;
+  void* C; int64_t ldc; int32_t c_fp32;
+  int64_t batch, batch_inner;
+  int64_t sA_outer, sA_inner, sB_outer, sB_inner, sC_outer, sC_inner, sR_outer, sR_inner;
+  int32_t epilogue;
+  float alpha;
+  int32_t beta_accum;
+  const void* bias;                   /* bf16 [N] or NULL */
+  const void* resid; int64_t ld_resid; /* bf16, may alias C */
+  void* aux; int64_t ld_aux;           /* bf16 saved pre-activations or NULL */
+  int64_t geglu_inter;                 /* I for PZ_EPI_GEGLU */
+} pz_gemm_args;
+int pz_gemm(const pz_gemm_args* args, void* stream);
+
+/* strided fp32-accumulate GEMM for the K=7 / N=7 linears (pizero.py:94-103, vla/modules.py:44):
+ * C[m*ldc+n] (+)= alpha*sum_k A[m*sAm+k*sAk]*B[k*sBk+n*sBn] (+bias[n]); bf16 in/out */
+typedef struct pz_small_gemm_args {
+  int64_t M, N, K;
+  const void* A; int64_t sAm, sAk;
+  const void* B; int64_t sBk, sBn;
+  void* C; int64_t ldc;
+  const void* bias;
+  float alpha;
+  int32_t beta;
+} pz_small_gemm_args;
+int pz_gemm_small(const pz_small_gemm_args* args, void* stream);
+
+/* Gemma RMSNorm y = x*rsqrt(mean(x^2)+eps)*(1+w), fp32 inside (paligemma/modules.py:7-21).
+ * rstd (fp32 [R]) is saved for backward when non-NULL. */
+int pz_rmsnorm_fwd(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, float* rstd,
+                   int64_t R, int64_t D, float eps, void* stream);
+/* dx = dres + d(rmsnorm)/dx . dy   (dres may alias dx, may be NULL);
+ * dw_part fp32 [ceil(R/rows_per_part), D] partial column sums of dy*xhat (NULL: skip) */
+int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
+                   const float* rstd, const void* dres, void* dx, int64_t lddx, float* dw_part,
+                   int64_t R, int64_t D, void* stream);
+/* LayerNorm with affine (siglip.py:211,217,290 -> nn.LayerNorm, fp32 under autocast) */
+int pz_layernorm_fwd(const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
+                     float* mean, float* rstd, int64_t R, int64_t D, float eps, void* stream);
+int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
+                     const float* mean, const float* rstd, const void* dres, void* dx, int64_t lddx,
+                     float* dw_part, float* db_part, int64_t R, int64_t D, void* stream);
+/* rows_per_part used by the *_bwd partial sums */
+int64_t pz_norm_rows_per_part(void);
+/* out[n] (+)= sum_p part[p*D + n]  -> bf16 (parameter gradient of a norm weight/bias) */
+int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream);
+/* bias gradient: out[n] (+)= sum_m X[m*ld + n] (bf16 X, fp32 workspace ws of >= 64*N floats) */
+int pz_colsum(const void* X, int64_t ld, int64_t M, int64_t N, void* out, int32_t beta, float* ws,
+              void* stream);
+/* sum over a batch of [rows, D] slabs: out (+)= sum_b X[b*stride + r*D + d] (pos-emb grad, siglip.py:76) */
+int pz_batch_sum(const void* X, int64_t B, int64_t stride, int64_t n, void* out, int32_t beta, void* stream);
+
+/* RoPE table: cs[pos*D/2*2 ..] = (cos, sin)(pos * inv_freq[i]) fp32 (paligemma/modules.py:24-67) */
+int pz_rope_table(float* cs, int64_t max_pos, int64_t head_dim, float theta, void* stream);
+/* one mixture's fused QKV projection [B*T, (nh+2*nkv)*hd] -> joint Q [B, Lq, nh*hd] (rows qoff..),
+ * joint K, V [B, Lk, nkv*hd] (rows koff..), RoPE applied to Q and K (utils.py:4-16,
+ * joint_model.py:170-257: the cat over mixtures without repeat_kv).  q_out NULL -> skip Q. */
+int pz_qkv_rope_split(const void* qkv, const int64_t* pos, const float* cs, void* q_out, void* k_out,
+                      void* v_out, int64_t B, int64_t T, int64_t nh, int64_t nkv, int64_t hd,
+                      int64_t Lq, int64_t qoff, int64_t Lk, int64_t koff, void* stream);
+/* backward of the above: writes d(qkv) (un-rotates dQ/dK, copies dV).  dq NULL -> zero dQ part */
+int pz_qkv_rope_split_bwd(const void* dq, const void* dk, const void* dv, const int64_t* pos,
+                          const float* cs, void* dqkv, int64_t B, int64_t T, int64_t nh, int64_t nkv,
+                          int64_t hd, int64_t Lq, int64_t qoff, int64_t Lk, int64_t koff, void* stream);
+
+/* attention softmax over rows of S (fp32) -> P (bf16, zero padded to ldp):
+ * logits = cap>0 ? cap*tanh(scale*s/cap) : scale*s; masked -> excluded (fully masked row ->
+ * uniform, like finfo.min in joint_model.py:271 / pizero.py:291); fp32 softmax (joint_model.py:273).
+ * mask_mode 0: none; 1: Pi0 block mask from per-sample prefix counts cnt[b] (pizero.py:271-306),
+ * query row r -> token qoff + (r % rows_per_batch)/heads, batch r / rows_per_batch;
+ * 2: additive fp32 mask [b][qtok][ldm].  tcap (bf16, NULL ok) saves tanh for backward. */
+typedef struct pz_softmax_args {
+  const float* S; int64_t lds;
+  void* P; int64_t ldp;
+  void* tcap;
+  int64_t R, N;
+  float scale, cap;
+  int32_t mask_mode;
+  int64_t rows_per_batch, heads, qoff;
+  const int32_t* cnt; int64_t prefix, cond;
+  const float* mask; int64_t ldm, mask_bstride;
+} pz_softmax_args;
+int pz_attn_softmax(const pz_softmax_args* a, void* stream);
+/* dS = scale * (1 - t^2) * P * (dP - rowsum(P*dP)), bf16 out zero padded to ldp */
+int pz_attn_softmax_bwd(const void* P, const float* dP, int64_t lddp, const void* tcap, void* dS,
+                        int64_t ldp, int64_t R, int64_t N, float scale, float cap, void* stream);
+
+/* SigLIP patch embed im2col (siglip.py:42-48,69-74): pixels bf16 [B,3,H,W] -> cols bf16
+ * [B*(H/ps)*(W/ps), ldc] with k = c*ps*ps + ky*ps + kx, zero pad k in [3*ps*ps, ldc) */
+int pz_patchify(const void* pix, void* cols, int64_t B, int64_t H, int64_t W, int64_t ps, int64_t ldc,
+                void* stream);
+/* token embed + image merge (pizero.py:376-414) with the joint-model sqrt(hidden) scaling
+ * (joint_model.py:348-355) folded in: out[b,i] = text ? table[id]*emb_scale : image ?
+ * img[b,k]*img_scale : 0 */
+int pz_embed_merge(const int64_t* ids, const void* table, const void* img, void* out, int64_t B,
+                   int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
+                   float emb_scale, float img_scale, void* stream);
+/* dimg[b,k] = dout[b,i]*img_scale for image tokens */
+int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* dimg, int64_t B, int64_t P,
+                       int64_t D, int64_t n_img, int64_t image_token, float img_scale, void* stream);
+
+/* SinusoidalPosEmb (vla/modules.py:9-22) from fp32 t[B] -> bf16 [B, D] */
+int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, void* stream);
+/* out[b*H+h] = [temb[b], e1[b*H+h]] (vla/modules.py:46-51), bf16 */
+int pz_concat_time(const void* temb, const void* e1, void* out, int64_t B, int64_t H, int64_t D,
+                   void* stream);
+/* dtemb not needed (t is data); de1 = dcat[:, D:] */
+int pz_split_time_grad(const void* dcat, void* de1, int64_t rows, int64_t D, void* stream);
+/* psi_t (pizero.py:597-605): psi = (1-(1-s)t) x0 + t x1 -> bf16 */
+int pz_flow_psi(const float* x0, const float* x1, const float* t, void* psi, int64_t B, int64_t HA,
+                float sig_min, void* stream);
+/* flow-matching MSE (pizero.py:660-661): loss = mean((v - (x1-(1-s)x0))^2) -> fp32 loss[0];
+ * dv = grad_scale[0] * 2 (v-d)/numel (bf16). grad_scale is a device fp32 scalar (NULL = 1). */
+int pz_flow_loss(const void* v, int64_t ldv, const float* x0, const float* x1, float* loss, void* dv,
+                 const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream);
+/* Euler step (pizero.py:479-481): a += dt*v ; t += dt */
+int pz_euler_step(float* action, const void* v, int64_t ldv, float* t, int64_t B, int64_t H, int64_t A,
+                  float dt, void* stream);
+int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream);
+
+/* elementwise backward of fused MLP epilogues (recompute activations, no extra saves) */
+int pz_geglu_bwd(const void* dh, int64_t lddh, const void* gu, int64_t ldgu, void* dgu, void* h_out,
+                 int64_t ldh, int64_t M, int64_t I, void* stream);
+int pz_act_bwd(const void* dh, int64_t lddh, const void* pre, int64_t ldpre, void* dpre, void* h_out,
+               int64_t ldh, int64_t M, int64_t N, int32_t act /* PZ_EPI_GELU | PZ_EPI_SILU */,
+               void* stream);
+
+/* flat fused AdamW over bf16 params (train.py:171-198; torch.optim.AdamW semantics),
+ * fp32 moments, gradient pre-scaled by *gscale (device scalar: clip coefficient). */
+int pz_adamw(void* p, const void* g, float* m, float* v, int64_t n, float lr, float beta1,
+             float beta2, float eps, float wd, float bc1, float bc2, const float* gscale, void* stream);
+/* sum of squares of bf16 g[0..n) accumulated (atomic, fp32) into acc[0] */
+int pz_sumsq(const void* g, int64_t n, float* acc, void* stream);
+/* clip_grad_norm_ coefficient (train.py:371-374): coef = min(1, max_norm/(sqrt(acc)+1e-6)) */
+int pz_clip_coef(const float* acc, float* coef, float* norm_out, float max_norm, void* stream);
+
+/* deterministic counter-based fill (oracle/synth.py twin): x[i] = off + scale*u(seed, i) */
+int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float off, float scale,
+                    void* stream);
+/* bf16 <-> fp32 copies / scaled adds */
+int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
+
+const char* pz_last_error(void);
+int pz_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PZ_ABI_H */

@@ -1,0 +1,517 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues (the Pi0 hot-path workhorse).
+//
+//   C[z](m,n) = epilogue( alpha * sum_k A[z](m,k) * B[z](k,n) )
+//
+// Operands are bf16 and each may be "k-contiguous" (A stored [M][K], B stored
+// [N][K]: nn.Linear weights) or "k-strided" (A stored [K][M], B stored [K][N]).
+// That covers forward (NT), dgrad (NN) and wgrad (TN) of every nn.Linear in
+// SigLIP / Gemma / the action expert, and the attention products
+// S = Q K^T, O = P V, dP = dO V^T, dQ = dS K, dK = dS^T Q, dV = P^T dO
+//  without any transpose kernels: k-strided tiles are staged in LDS
+// [k][row] and read with ds_read_b64_tr_b16 (gfx950 hardware transpose read).
+//
+// Tile 128x128x64, 256 threads = 4 waves, mfma_f32_16x16x32_bf16, register
+// staged double-buffered LDS (issue-early / write-late, one barrier per K
+// step), XOR-swizzled LDS images (conflict-free ds_read_b128 and tr reads),
+// XCD-aware tile order.  MFMA operands are swapped (B-frag first) so each lane
+// owns 4 consecutive output columns -> vectorised epilogue stores.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "pz_common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile image in LDS
+
+struct GemmP {
+  const bf16_t* A;
+  const bf16_t* B;
+  void* C;
+  const bf16_t* bias;
+  const bf16_t* resid;
+  bf16_t* aux;
+  int64_t M, N, K, lda, ldb, ldc, ld_resid, ld_aux, geglu_I;
+  int64_t batch_inner, sAo, sAi, sBo, sBi, sCo, sCi, sRo, sRi;
+  int tiles_m, tiles_n, epi, c_fp32, beta;
+  float alpha;
+};
+
+__device__ __forceinline__ int sw_tr(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
+
+// ---- global -> registers (4 x 16 B per thread per operand tile) -------------
+template <bool KC>
+__device__ __forceinline__ void g2r(u32x4 (&r)[4], const bf16_t* __restrict__ base, int64_t ld,
+                                    int64_t row0, int64_t R, int64_t k0, int64_t K,
+                                    bool geglu, int64_t gI) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = t + NT * i;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (KC) {
+      const int rr = c >> 3, kc = c & 7;
+      int64_t grow;
+      bool ok;
+      if (geglu) {
+        const int64_t lr = row0 + (rr & 63);
+        ok = lr < gI;
+        grow = (rr < 64) ? lr : gI + lr;
+      } else {
+        grow = row0 + rr;
+        ok = grow < R;
+      }
+      const int64_t kk = k0 + 8 * kc;
+      if (ok && kk < K) v = *reinterpret_cast<const u32x4*>(base + grow * ld + kk);
+    } else {
+      const int kr = c >> 4, rc = c & 15;
+      const int64_t kk = k0 + kr, rr = row0 + 8 * rc;
+      if (kk < K && rr < R) v = *reinterpret_cast<const u32x4*>(base + kk * ld + rr);
+    }
+    r[i] = v;
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ void r2s(const u32x4 (&r)[4], char* lds) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = t + NT * i;
+    int off;
+    if (KC) {
+      const int rr = c >> 3, kc = c & 7;
+      off = rr * 128 + ((kc ^ ((rr >> 1) & 7)) << 4);
+    } else {
+      const int kr = c >> 4, rc = c & 15;
+      off = kr * 256 + (((2 * rc) ^ sw_tr(kr)) << 3);
+    }
+    *reinterpret_cast<u32x4*>(lds + off) = r[i];
+  }
+}
+
+// fragment for rows rb*16.., k = kk*32 + 8*(lane>>4) + j
+template <bool KC>
+__device__ __forceinline__ bf16x8 frag(const char* lds, int rb, int kk, int lane) {
+  if (KC) {
+    const int r = rb * 16 + (lane & 15);
+    const int ch = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + r * 128 + ((ch ^ ((r >> 1) & 7)) << 4));
+  } else {
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    s16x8 out;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k = kk * 32 + 8 * (lane >> 4) + 4 * t + q;
+      const int off = k * 256 + (((4 * rb + p) ^ sw_tr(k)) << 3);
+      s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(lds + off));
+      out[4 * t + 0] = v[0];
+      out[4 * t + 1] = v[1];
+      out[4 * t + 2] = v[2];
+      out[4 * t + 3] = v[3];
+    }
+    return __builtin_bit_cast(bf16x8, out);
+  }
+}
+
+// bijective XCD-aware remap + grouped (super-row) tile order
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int xcd = bid & 7, local = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int g = wg / per_group;
+  const int first_m = g * GROUP;
+  const int gsize = min(tiles_m - first_m, GROUP);
+  const int in = wg - g * per_group;
+  tm = first_m + in % gsize;
+  tn = in / gsize;
+}
+
+template <bool AKC, bool BKC, int WM>
+__global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
+  constexpr int WN = 4 / WM;
+  constexpr int MI = (BM / WM) / 16;  // m blocks per wave
+  constexpr int NI = (BN / WN) / 16;  // n blocks per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sA = smem;                    // [2][TILE_BYTES]
+  char* sB = smem + 2 * TILE_BYTES;   // [2][TILE_BYTES]
+
+  const bool geglu = p.epi == PZ_EPI_GEGLU;
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int64_t z = blockIdx.y;
+  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bf16_t* A = p.A + zo * p.sAo + zi * p.sAi;
+  const bf16_t* B = p.B + zo * p.sBo + zi * p.sBi;
+  const int64_t m0 = (int64_t)tm * BM;
+  const int64_t n0 = geglu ? (int64_t)tn * (BN / 2) : (int64_t)tn * BN;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)((p.K + BK - 1) / BK);
+  u32x4 ra[4], rb[4];
+  g2r<AKC>(ra, A, p.lda, m0, p.M, 0, p.K, false, 0);
+  g2r<BKC>(rb, B, p.ldb, n0, p.N, 0, p.K, geglu, p.geglu_I);
+  r2s<AKC>(ra, sA);
+  r2s<BKC>(rb, sB);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      g2r<AKC>(ra, A, p.lda, m0, p.M, (int64_t)(kt + 1) * BK, p.K, false, 0);
+      g2r<BKC>(rb, B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BK, p.K, geglu, p.geglu_I);
+    }
+    const char* a_img = sA + cur * TILE_BYTES;
+    const char* b_img = sB + cur * TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = frag<AKC>(a_img, wm * MI + i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = frag<BKC>(b_img, wn * NI + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      r2s<AKC>(ra, sA + (cur ^ 1) * TILE_BYTES);
+      r2s<BKC>(rb, sB + (cur ^ 1) * TILE_BYTES);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  const int64_t cofs = zo * p.sCo + zi * p.sCi;
+  const int64_t rofs = zo * p.sRo + zi * p.sRi;
+  const float alpha = p.alpha;
+  if (geglu) {
+    // wave tile = 32 rows x 128 cols: cols [0,64) gate, [64,128) up
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NI / 2; ++j) {
+        const int64_t n = n0 + j * 16 + 4 * (lane >> 4);
+        if (n >= p.geglu_I) continue;
+        float h[4], g[4], u[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          g[r] = acc[i][j][r] * alpha;
+          u[r] = acc[i][j + NI / 2][r] * alpha;
+          h[r] = gelu_tanh(g[r]) * u[r];
+        }
+        bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+        *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
+        if (p.aux) {
+          bf16_t* X = p.aux + m * p.ld_aux + n;
+          *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(g[0], g[1]), pack2bf(g[2], g[3])};
+          *reinterpret_cast<u32x2*>(X + p.geglu_I) = u32x2{pack2bf(u[0], u[1]), pack2bf(u[2], u[3])};
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+    const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int64_t n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      const bool full = n + 4 <= p.N;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
+      if (p.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (full || n + r < p.N) v[r] += bf2f(p.bias[n + r]);
+      }
+      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+        if (p.aux) {
+          bf16_t* X = p.aux + m * p.ld_aux + n;
+          if (full) {
+            *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+          } else {
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) X[r] = f2bf(v[r]);
+          }
+        }
+        if (p.epi == PZ_EPI_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+        }
+      }
+      if (p.resid) {
+        const bf16_t* R = p.resid + rofs + m * p.ld_resid + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (full || n + r < p.N) v[r] += bf2f(R[r]);
+      }
+      if (p.c_fp32) {
+        float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
+        if (full) {
+          if (p.beta) {
+            f32x4 o = *reinterpret_cast<f32x4*>(Cp);
+            v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+          }
+          *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
+        }
+      } else {
+        bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+        if (full) {
+          if (p.beta) {
+            u32x2 o = *reinterpret_cast<u32x2*>(Cp);
+            v[0] += bf2f(o[0] & 0xffff); v[1] += bf2f(o[0] >> 16);
+            v[2] += bf2f(o[1] & 0xffff); v[3] += bf2f(o[1] >> 16);
+          }
+          *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+        } else {
+          for (int r = 0; r < 4; ++r)
+            if (n + r < p.N) Cp[r] = f2bf(p.beta ? bf2f(Cp[r]) + v[r] : v[r]);
+        }
+      }
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
+// Skinny GEMM for M <= 16 (inference denoise steps, B = 1..4): weights are
+// streamed once straight into VGPRs (no LDS), one wave per 16 output columns,
+// K split across the 4 waves of a block and reduced through LDS.  Operand A
+// must be k-contiguous, B k-contiguous (nn.Linear weight layout).
+// -------------------------------------------------------------------------
+constexpr int SK_WAVES = 4;
+__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmP p) {
+  __shared__ f32x4 red[SK_WAVES][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool geglu = p.epi == PZ_EPI_GEGLU;
+  const int64_t ncols = geglu ? p.geglu_I : p.N;
+  const int64_t n0 = (int64_t)blockIdx.x * 16;
+  const int64_t z = blockIdx.y;
+  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bf16_t* A = p.A + zo * p.sAo + zi * p.sAi;
+  const bf16_t* B = p.B + zo * p.sBo + zi * p.sBi;
+  const int64_t m = lane & 15;
+  const int64_t nr = n0 + (lane & 15);
+  const bool mok = m < p.M, nok = nr < ncols;
+  const int64_t kchunks = p.K / 32;  // K % 32 == 0 required (host checked)
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  const bf16_t* Arow = A + m * p.lda + 8 * (lane >> 4);
+  const bf16_t* Brow = B + nr * p.ldb + 8 * (lane >> 4);
+  const bf16_t* Brow2 = B + (p.geglu_I + nr) * p.ldb + 8 * (lane >> 4);
+  for (int64_t kc = wave; kc < kchunks; kc += SK_WAVES) {
+    bf16x8 a = {}, b = {}, b2 = {};
+    if (mok) a = *reinterpret_cast<const bf16x8*>(Arow + kc * 32);
+    if (nok) b = *reinterpret_cast<const bf16x8*>(Brow + kc * 32);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc, 0, 0, 0);
+    if (geglu) {
+      if (nok) b2 = *reinterpret_cast<const bf16x8*>(Brow2 + kc * 32);
+      acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, a, acc2, 0, 0, 0);
+    }
+  }
+  // D[n_local = 4*(lane>>4)+r][m = lane&15]
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0) {
+    for (int w = 1; w < SK_WAVES; ++w) acc += red[w][lane];
+  }
+  if (geglu) {
+    __syncthreads();
+    red[wave][lane] = acc2;
+    __syncthreads();
+    if (wave == 0)
+      for (int w = 1; w < SK_WAVES; ++w) acc2 += red[w][lane];
+  }
+  if (wave != 0) return;
+  const int64_t mm = lane & 15;
+  if (mm >= p.M) return;
+  const int64_t n = n0 + 4 * (lane >> 4);
+  const int64_t cofs = zo * p.sCo + zi * p.sCi;
+  const int64_t rofs = zo * p.sRo + zi * p.sRi;
+  float v[4];
+  for (int r = 0; r < 4; ++r) {
+    const int64_t nn = n + r;
+    if (nn >= ncols) continue;
+    float x = acc[r] * p.alpha;
+    if (geglu) {
+      const float g = x, u = acc2[r] * p.alpha;
+      if (p.aux) {
+        p.aux[mm * p.ld_aux + nn] = f2bf(g);
+        p.aux[mm * p.ld_aux + p.geglu_I + nn] = f2bf(u);
+      }
+      x = gelu_tanh(g) * u;
+    } else {
+      if (p.bias) x += bf2f(p.bias[nn]);
+      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+        if (p.aux) p.aux[mm * p.ld_aux + nn] = f2bf(x);
+        x = p.epi == PZ_EPI_GELU ? gelu_tanh(x) : silu(x);
+      }
+      if (p.resid) x += bf2f(p.resid[rofs + mm * p.ld_resid + nn]);
+    }
+    v[r] = x;
+    if (p.c_fp32) {
+      float* Cp = reinterpret_cast<float*>(p.C) + cofs + mm * p.ldc + nn;
+      *Cp = p.beta ? *Cp + x : x;
+    } else {
+      bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + mm * p.ldc + nn;
+      *Cp = f2bf(p.beta ? bf2f(*Cp) + x : x);
+    }
+  }
+  (void)v;
+}
+
+// -------------------------------------------------------------------------
+// Small strided fp32-accumulate GEMM for the K=7 / N=7 action/proprio linears
+// (SURVEY 2.2 "proprio enc / action dec": 0.03 GF).  One thread per output.
+// -------------------------------------------------------------------------
+__global__ void gemm_small_kernel(pz_small_gemm_args a) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.M * a.N) return;
+  const int64_t m = idx / a.N, n = idx % a.N;
+  const bf16_t* A = (const bf16_t*)a.A;
+  const bf16_t* B = (const bf16_t*)a.B;
+  float s = 0.f;
+  for (int64_t k = 0; k < a.K; ++k)
+    s += bf2f(A[m * a.sAm + k * a.sAk]) * bf2f(B[k * a.sBk + n * a.sBn]);
+  s *= a.alpha;
+  if (a.bias) s += bf2f(((const bf16_t*)a.bias)[n]);
+  bf16_t* C = (bf16_t*)a.C + m * a.ldc + n;
+  if (a.beta) s += bf2f(*C);
+  *C = f2bf(s);
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- host ----
+
+static thread_local char g_err[512];
+void pz_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char* pz_last_error(void) { return g_err; }
+
+extern "C" int pz_abi_version(void) { return PZ_ABI_VERSION; }
+
+template <bool AKC, bool BKC, int WM>
+static int launch_tile(const GemmP& p, int64_t batch, hipStream_t st) {
+  const int smem = 4 * TILE_BYTES;
+  auto kern = gemm_kernel<AKC, BKC, WM>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  dim3 grid(p.tiles_m * p.tiles_n, (unsigned)batch);
+  hipLaunchKernelGGL(kern, grid, dim3(NT), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
+  PZ_CHECK_ARG(a != nullptr, "pz_gemm: null args");
+  PZ_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0, "pz_gemm: bad dims M=%lld N=%lld K=%lld",
+               (long long)a->M, (long long)a->N, (long long)a->K);
+  PZ_CHECK_ARG(a->A && a->B && a->C, "pz_gemm: null operand");
+  PZ_CHECK_ARG(a->batch >= 1 && a->batch_inner >= 1 && a->batch % a->batch_inner == 0,
+               "pz_gemm: bad batch %lld/%lld", (long long)a->batch, (long long)a->batch_inner);
+  PZ_CHECK_ARG(PZ_ALIGNED(a->A, 16) && PZ_ALIGNED(a->B, 16), "pz_gemm: A/B must be 16-byte aligned");
+  PZ_CHECK_ARG(a->lda % 8 == 0 && a->ldb % 8 == 0, "pz_gemm: lda/ldb must be multiples of 8");
+  PZ_CHECK_ARG(a->ldc % 4 == 0 && PZ_ALIGNED(a->C, 8), "pz_gemm: ldc %% 4 and C 8-byte alignment");
+  PZ_CHECK_ARG(a->sA_outer % 8 == 0 && a->sA_inner % 8 == 0 && a->sB_outer % 8 == 0 &&
+                   a->sB_inner % 8 == 0 && a->sC_outer % 4 == 0 && a->sC_inner % 4 == 0,
+               "pz_gemm: batch strides must keep 16-byte alignment");
+  if (a->a_kcontig) PZ_CHECK_ARG(a->K % 8 == 0, "pz_gemm: k-contiguous A needs K %% 8 == 0");
+  else PZ_CHECK_ARG(a->M % 8 == 0, "pz_gemm: k-strided A needs M %% 8 == 0");
+  if (a->b_kcontig) PZ_CHECK_ARG(a->K % 8 == 0, "pz_gemm: k-contiguous B needs K %% 8 == 0");
+  else PZ_CHECK_ARG(a->N % 8 == 0, "pz_gemm: k-strided B needs N %% 8 == 0");
+  const bool geglu = a->epilogue == PZ_EPI_GEGLU;
+  if (geglu) {
+    PZ_CHECK_ARG(a->b_kcontig && a->geglu_inter > 0 && a->N == 2 * a->geglu_inter && a->batch == 1 &&
+                     !a->beta_accum && !a->resid && !a->bias && !a->c_fp32 && a->geglu_inter % 4 == 0,
+                 "pz_gemm: GEGLU needs k-contiguous B = [gate; up] (N = 2I), no batch/bias/resid");
+  }
+  if (a->epilogue == PZ_EPI_GELU || a->epilogue == PZ_EPI_SILU)
+    PZ_CHECK_ARG(a->batch == 1, "pz_gemm: activation epilogue is unbatched");
+  if (a->aux) PZ_CHECK_ARG(a->ld_aux % 4 == 0 && PZ_ALIGNED(a->aux, 8), "pz_gemm: aux alignment");
+
+  GemmP p;
+  p.A = (const bf16_t*)a->A;
+  p.B = (const bf16_t*)a->B;
+  p.C = a->C;
+  p.bias = (const bf16_t*)a->bias;
+  p.resid = (const bf16_t*)a->resid;
+  p.aux = (bf16_t*)a->aux;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.lda = a->lda; p.ldb = a->ldb; p.ldc = a->ldc;
+  p.ld_resid = a->ld_resid; p.ld_aux = a->ld_aux; p.geglu_I = a->geglu_inter;
+  p.batch_inner = a->batch_inner;
+  p.sAo = a->sA_outer; p.sAi = a->sA_inner;
+  p.sBo = a->sB_outer; p.sBi = a->sB_inner;
+  p.sCo = a->sC_outer; p.sCi = a->sC_inner;
+  p.sRo = a->sR_outer; p.sRi = a->sR_inner;
+  p.epi = a->epilogue;
+  p.c_fp32 = a->c_fp32;
+  p.beta = a->beta_accum;
+  p.alpha = a->alpha;
+  hipStream_t st = (hipStream_t)stream;
+
+  const int64_t ncols = geglu ? a->geglu_inter : a->N;
+  // skinny path: few rows, weights streamed once (inference denoise / proprio rows)
+  if (a->M <= 16 && a->a_kcontig && a->b_kcontig && a->K % 32 == 0 && !a->c_fp32 &&
+      PZ_ALIGNED(a->A, 16) && a->lda % 8 == 0) {
+    dim3 grid((unsigned)((ncols + 15) / 16), (unsigned)a->batch);
+    hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, st, p);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
+  p.tiles_m = (int)((a->M + BM - 1) / BM);
+  p.tiles_n = (int)((ncols + (geglu ? BN / 2 : BN) - 1) / (geglu ? BN / 2 : BN));
+  PZ_CHECK_ARG((int64_t)p.tiles_m * p.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
+  if (geglu) {
+    if (a->a_kcontig) return launch_tile<true, true, 4>(p, a->batch, st);
+    return launch_tile<false, true, 4>(p, a->batch, st);
+  }
+  if (a->a_kcontig && a->b_kcontig) return launch_tile<true, true, 2>(p, a->batch, st);
+  if (a->a_kcontig && !a->b_kcontig) return launch_tile<true, false, 2>(p, a->batch, st);
+  if (!a->a_kcontig && a->b_kcontig) return launch_tile<false, true, 2>(p, a->batch, st);
+  return launch_tile<false, false, 2>(p, a->batch, st);
+}
+
+extern "C" int pz_gemm_small(const pz_small_gemm_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->A && a->B && a->C && a->M > 0 && a->N > 0 && a->K > 0, "pz_gemm_small: bad args");
+  const int64_t total = a->M * a->N;
+  hipLaunchKernelGGL(gemm_small_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, *a);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

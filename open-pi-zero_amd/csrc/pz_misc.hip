@@ -1,0 +1,418 @@
+// Small fused kernels around the Pi0 transformer stacks:
+//   patch im2col (siglip.py:42-76), token embed + image merge (pizero.py:376-414),
+//   sinusoidal time embedding + action-encoder concat (vla/modules.py:9-53),
+//   flow-matching psi / loss / Euler update (pizero.py:479-489,597-661),
+//   activation backward for fused GEMM epilogues, fused flat AdamW +
+//   grad-norm clip (train.py:171-198,371-379), deterministic synthetic fill.
+#include <math.h>
+
+#include "pz_common.h"
+
+namespace {
+
+__global__ void patchify_kernel(const bf16_t* __restrict__ pix, bf16_t* cols, int64_t B, int64_t H, int64_t W,
+                                int ps, int64_t ldc) {
+  const int64_t gw = W / ps, gh = H / ps;
+  const int64_t patch = blockIdx.x;  // over B*gh*gw
+  const int64_t b = patch / (gh * gw), py = (patch / gw) % gh, px = patch % gw;
+  bf16_t* out = cols + patch * ldc;
+  const int kk = 3 * ps * ps;
+  for (int k = threadIdx.x; k < ldc; k += blockDim.x) {
+    bf16_t v = 0;
+    if (k < kk) {
+      const int c = k / (ps * ps), ky = (k / ps) % ps, kx = k % ps;
+      v = pix[((b * 3 + c) * H + py * ps + ky) * W + px * ps + kx];
+    }
+    out[k] = v;
+  }
+}
+
+__global__ void embed_merge_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
+                                   const bf16_t* __restrict__ img, bf16_t* out, int64_t P, int64_t D,
+                                   int64_t n_img, int64_t image_token, int64_t pad_token, float emb_scale,
+                                   float img_scale) {
+  __shared__ int rank_s;
+  const int64_t i = blockIdx.x, b = blockIdx.y;
+  const int64_t id = ids[b * P + i];
+  bf16_t* o = out + (b * P + i) * D;
+  if (id == image_token) {
+    if (threadIdx.x == 0) {
+      int r = 0;
+      for (int64_t j = 0; j < i; ++j) r += ids[b * P + j] == image_token;
+      rank_s = r;
+    }
+    __syncthreads();
+    const int64_t k = rank_s;
+    if (k >= n_img) {
+      for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = 0;
+      return;
+    }
+    const bf16_t* src = img + (b * n_img + k) * D;
+    for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = f2bf(bf2f(src[d]) * img_scale);
+  } else if (id == pad_token) {
+    for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = 0;
+  } else {
+    const bf16_t* src = table + id * D;
+    for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = f2bf(bf2f(src[d]) * emb_scale);
+  }
+}
+
+__global__ void embed_merge_bwd_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ dout,
+                                       bf16_t* dimg, int64_t P, int64_t D, int64_t n_img, int64_t image_token,
+                                       float img_scale) {
+  __shared__ int rank_s;
+  const int64_t i = blockIdx.x, b = blockIdx.y;
+  if (ids[b * P + i] != image_token) return;
+  if (threadIdx.x == 0) {
+    int r = 0;
+    for (int64_t j = 0; j < i; ++j) r += ids[b * P + j] == image_token;
+    rank_s = r;
+  }
+  __syncthreads();
+  const int64_t k = rank_s;
+  if (k >= n_img) return;
+  const bf16_t* src = dout + (b * P + i) * D;
+  bf16_t* dst = dimg + (b * n_img + k) * D;
+  for (int64_t d = threadIdx.x; d < D; d += blockDim.x) dst[d] = f2bf(bf2f(src[d]) * img_scale);
+}
+
+__global__ void time_embed_kernel(const float* __restrict__ t, bf16_t* out, int64_t B, int D, float max_period) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * D) return;
+  const int64_t b = idx / D;
+  const int j = (int)(idx % D), half = D / 2;
+  const int i = j < half ? j : j - half;
+  const float e = logf(max_period) / (float)(half - 1);
+  const float f = expf((float)i * -e);
+  const float a = t[b] * f;
+  out[idx] = f2bf(j < half ? sinf(a) : cosf(a));
+}
+
+__global__ void concat_time_kernel(const bf16_t* __restrict__ temb, const bf16_t* __restrict__ e1, bf16_t* out,
+                                   int64_t rows, int64_t H, int64_t D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * 2 * D) return;
+  const int64_t r = idx / (2 * D), c = idx % (2 * D);
+  out[idx] = c < D ? temb[(r / H) * D + c] : e1[r * D + c - D];
+}
+
+__global__ void split_time_grad_kernel(const bf16_t* __restrict__ dcat, bf16_t* de1, int64_t rows, int64_t D) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * D) return;
+  const int64_t r = idx / D, c = idx % D;
+  de1[idx] = dcat[r * 2 * D + D + c];
+}
+
+__global__ void flow_psi_kernel(const float* x0, const float* x1, const float* t, bf16_t* psi, int64_t B,
+                                int64_t HA, float sig) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= B * HA) return;
+  const float tt = t[idx / HA];
+  psi[idx] = f2bf((1.f - (1.f - sig) * tt) * x0[idx] + tt * x1[idx]);
+}
+
+__global__ void flow_loss_kernel(const bf16_t* __restrict__ v, int64_t ldv, const float* __restrict__ x0,
+                                 const float* __restrict__ x1, float* loss, bf16_t* dv,
+                                 const float* __restrict__ gscale, int64_t rows, int64_t A, float sig) {
+  __shared__ float red[4];
+  const int64_t n = rows * A;
+  float s = 0.f;
+  const float g = gscale ? gscale[0] : 1.f;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t r = i / A, c = i % A;
+    const float d = x1[i] - (1.f - sig) * x0[i];
+    const float e = bf2f(v[r * ldv + c]) - d;
+    s += e * e;
+    if (dv) dv[r * A + c] = f2bf(g * 2.f * e / (float)n);
+  }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) loss[0] = s / (float)n;
+}
+
+__global__ void euler_kernel(float* action, const bf16_t* __restrict__ v, int64_t ldv, float* t, int64_t B,
+                             int64_t H, int64_t A, float dt) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < B * H * A) {
+    const int64_t r = idx / A, c = idx % A;
+    action[idx] += dt * bf2f(v[r * ldv + c]);
+  }
+  if (t && idx < B) t[idx] += dt;
+}
+
+__global__ void clamp_kernel(float* x, int64_t n, float lo, float hi) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < n) x[idx] = fminf(fmaxf(x[idx], lo), hi);
+}
+
+__global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dh, int64_t lddh, const bf16_t* gu, int64_t ldgu,
+                                 bf16_t* dgu, bf16_t* h_out, int64_t ldh, int64_t M, int64_t I) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * I) return;
+  const int64_t m = idx / I, n = idx % I;
+  const float g = bf2f(gu[m * ldgu + n]), u = bf2f(gu[m * ldgu + I + n]);
+  const float d = bf2f(dh[m * lddh + n]);
+  const float ge = gelu_tanh(g);
+  if (h_out) h_out[m * ldh + n] = f2bf(ge * u);
+  dgu[m * ldgu + n] = f2bf(d * u * gelu_tanh_grad(g));
+  dgu[m * ldgu + I + n] = f2bf(d * ge);
+}
+
+__global__ void act_bwd_kernel(const bf16_t* __restrict__ dh, int64_t lddh, const bf16_t* pre, int64_t ldpre,
+                               bf16_t* dpre, bf16_t* h_out, int64_t ldh, int64_t M, int64_t N, int act) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= M * N) return;
+  const int64_t m = idx / N, n = idx % N;
+  const float x = bf2f(pre[m * ldpre + n]);
+  const float d = bf2f(dh[m * lddh + n]);
+  float h, gr;
+  if (act == PZ_EPI_GELU) {
+    h = gelu_tanh(x);
+    gr = gelu_tanh_grad(x);
+  } else {
+    h = silu(x);
+    gr = silu_grad(x);
+  }
+  if (h_out) h_out[m * ldh + n] = f2bf(h);
+  dpre[m * ldpre + n] = f2bf(d * gr);
+}
+
+// AdamW (torch.optim.AdamW, decoupled weight decay), fp32 math, bf16 params
+__global__ void adamw_kernel(bf16_t* __restrict__ p, const bf16_t* __restrict__ g, float* __restrict__ m,
+                             float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
+                             float bc1, float bc2, const float* __restrict__ gscale) {
+  const float gs = gscale ? gscale[0] : 1.f;
+  const float step = lr / bc1;
+  const float bc2s = sqrtf(bc2);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float gr = bf2f(g[i]) * gs;
+    float pv = bf2f(p[i]);
+    pv *= (1.f - lr * wd);
+    const float mi = b1 * m[i] + (1.f - b1) * gr;
+    const float vi = b2 * v[i] + (1.f - b2) * gr * gr;
+    m[i] = mi;
+    v[i] = vi;
+    pv -= step * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] = f2bf(pv);
+  }
+}
+
+__global__ void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n, float* acc) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const int64_t n8 = n / 8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    u32x4 r = reinterpret_cast<const u32x4*>(g)[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float a = __uint_as_float(r[k] << 16), b = __uint_as_float(r[k] & 0xffff0000u);
+      s += a * a + b * b;
+    }
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n8 * 8 + threadIdx.x; i < n; i += blockDim.x) {
+      const float a = bf2f(g[i]);
+      s += a * a;
+    }
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) atomicAdd(acc, s);
+}
+
+__global__ void clip_coef_kernel(const float* acc, float* coef, float* norm_out, float max_norm) {
+  const float nrm = sqrtf(acc[0]);
+  if (norm_out) norm_out[0] = nrm;
+  coef[0] = fminf(1.f, max_norm / (nrm + 1e-6f));
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_uniform_kernel(void* x, int out_fp32, int64_t n, uint64_t seed, float off, float scale) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t z = splitmix64(seed + (uint64_t)i);
+    const float u = (float)(uint32_t)(z >> 40) * 0x1p-23f - 1.0f;
+    // oracle/synth.py computes off + scale*u with two fp32 roundings: reproduce exactly
+    const float w = __fadd_rn(off, __fmul_rn(scale, u));
+    if (out_fp32) ((float*)x)[i] = w;
+    else ((bf16_t*)x)[i] = f2bf(w);
+  }
+}
+
+__global__ void cast_f32_bf16_kernel(const float* x, bf16_t* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = f2bf(x[i]);
+}
+__global__ void cast_bf16_f32_kernel(const bf16_t* x, float* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = bf2f(x[i]);
+}
+
+inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+#define ST ((hipStream_t)stream)
+
+extern "C" int pz_patchify(const void* pix, void* cols, int64_t B, int64_t H, int64_t W, int64_t ps, int64_t ldc,
+                           void* stream) {
+  PZ_CHECK_ARG(pix && cols && B > 0 && H % ps == 0 && W % ps == 0 && ldc >= 3 * ps * ps, "patchify: bad args");
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)(B * (H / ps) * (W / ps))), dim3(256), 0, ST,
+                     (const bf16_t*)pix, (bf16_t*)cols, B, H, W, (int)ps, ldc);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_embed_merge(const int64_t* ids, const void* table, const void* img, void* out, int64_t B,
+                              int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
+                              float emb_scale, float img_scale, void* stream) {
+  PZ_CHECK_ARG(ids && table && img && out && B > 0 && P > 0 && D > 0, "embed_merge: bad args");
+  hipLaunchKernelGGL(embed_merge_kernel, dim3((unsigned)P, (unsigned)B), dim3(256), 0, ST, ids,
+                     (const bf16_t*)table, (const bf16_t*)img, (bf16_t*)out, P, D, n_img, image_token, pad_token,
+                     emb_scale, img_scale);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* dimg, int64_t B, int64_t P,
+                                  int64_t D, int64_t n_img, int64_t image_token, float img_scale, void* stream) {
+  PZ_CHECK_ARG(ids && dout && dimg && B > 0 && P > 0 && D > 0, "embed_merge_bwd: bad args");
+  hipLaunchKernelGGL(embed_merge_bwd_kernel, dim3((unsigned)P, (unsigned)B), dim3(256), 0, ST, ids,
+                     (const bf16_t*)dout, (bf16_t*)dimg, P, D, n_img, image_token, img_scale);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, void* stream) {
+  PZ_CHECK_ARG(t && out && B > 0 && D % 2 == 0 && D >= 4, "time_embed: bad args");
+  hipLaunchKernelGGL(time_embed_kernel, dim3(nblk(B * D)), dim3(256), 0, ST, t, (bf16_t*)out, B, (int)D,
+                     max_period);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_concat_time(const void* temb, const void* e1, void* out, int64_t B, int64_t H, int64_t D,
+                              void* stream) {
+  PZ_CHECK_ARG(temb && e1 && out && B > 0 && H > 0 && D > 0, "concat_time: bad args");
+  hipLaunchKernelGGL(concat_time_kernel, dim3(nblk(B * H * 2 * D)), dim3(256), 0, ST, (const bf16_t*)temb,
+                     (const bf16_t*)e1, (bf16_t*)out, B * H, H, D);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_split_time_grad(const void* dcat, void* de1, int64_t rows, int64_t D, void* stream) {
+  PZ_CHECK_ARG(dcat && de1 && rows > 0 && D > 0, "split_time_grad: bad args");
+  hipLaunchKernelGGL(split_time_grad_kernel, dim3(nblk(rows * D)), dim3(256), 0, ST, (const bf16_t*)dcat,
+                     (bf16_t*)de1, rows, D);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_flow_psi(const float* x0, const float* x1, const float* t, void* psi, int64_t B, int64_t HA,
+                           float sig_min, void* stream) {
+  PZ_CHECK_ARG(x0 && x1 && t && psi && B > 0 && HA > 0, "flow_psi: bad args");
+  hipLaunchKernelGGL(flow_psi_kernel, dim3(nblk(B * HA)), dim3(256), 0, ST, x0, x1, t, (bf16_t*)psi, B, HA,
+                     sig_min);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_flow_loss(const void* v, int64_t ldv, const float* x0, const float* x1, float* loss, void* dv,
+                            const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream) {
+  PZ_CHECK_ARG(v && x0 && x1 && loss && B > 0, "flow_loss: bad args");
+  hipLaunchKernelGGL(flow_loss_kernel, dim3(1), dim3(256), 0, ST, (const bf16_t*)v, ldv, x0, x1, loss,
+                     (bf16_t*)dv, grad_scale, B * H, A, sig_min);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_euler_step(float* action, const void* v, int64_t ldv, float* t, int64_t B, int64_t H, int64_t A,
+                             float dt, void* stream) {
+  PZ_CHECK_ARG(action && v && B > 0, "euler_step: bad args");
+  const int64_t n = B * H * A > B ? B * H * A : B;
+  hipLaunchKernelGGL(euler_kernel, dim3(nblk(n)), dim3(256), 0, ST, action, (const bf16_t*)v, ldv, t, B, H, A, dt);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream) {
+  PZ_CHECK_ARG(x && n > 0, "clamp: bad args");
+  hipLaunchKernelGGL(clamp_kernel, dim3(nblk(n)), dim3(256), 0, ST, x, n, lo, hi);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_geglu_bwd(const void* dh, int64_t lddh, const void* gu, int64_t ldgu, void* dgu, void* h_out,
+                            int64_t ldh, int64_t M, int64_t I, void* stream) {
+  PZ_CHECK_ARG(dh && gu && dgu && M > 0 && I > 0, "geglu_bwd: bad args");
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3(nblk(M * I)), dim3(256), 0, ST, (const bf16_t*)dh, lddh,
+                     (const bf16_t*)gu, ldgu, (bf16_t*)dgu, (bf16_t*)h_out, ldh, M, I);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_act_bwd(const void* dh, int64_t lddh, const void* pre, int64_t ldpre, void* dpre, void* h_out,
+                          int64_t ldh, int64_t M, int64_t N, int32_t act, void* stream) {
+  PZ_CHECK_ARG(dh && pre && dpre && M > 0 && N > 0 && (act == PZ_EPI_GELU || act == PZ_EPI_SILU),
+               "act_bwd: bad args");
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(nblk(M * N)), dim3(256), 0, ST, (const bf16_t*)dh, lddh,
+                     (const bf16_t*)pre, ldpre, (bf16_t*)dpre, (bf16_t*)h_out, ldh, M, N, (int)act);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_adamw(void* p, const void* g, float* m, float* v, int64_t n, float lr, float beta1, float beta2,
+                        float eps, float wd, float bc1, float bc2, const float* gscale, void* stream) {
+  PZ_CHECK_ARG(p && g && m && v && n >= 0, "adamw: bad args");
+  if (n == 0) return PZ_OK;
+  const int64_t blocks = n / 256 + 1 < 8192 ? n / 256 + 1 : 8192;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)blocks), dim3(256), 0, ST, (bf16_t*)p, (const bf16_t*)g, m, v, n,
+                     lr, beta1, beta2, eps, wd, bc1, bc2, gscale);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_sumsq(const void* g, int64_t n, float* acc, void* stream) {
+  PZ_CHECK_ARG(g && acc && n >= 0 && PZ_ALIGNED(g, 16), "sumsq: bad args (16-byte alignment)");
+  if (n == 0) return PZ_OK;
+  const int64_t blocks = n / 2048 + 1 < 4096 ? n / 2048 + 1 : 4096;
+  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, ST, (const bf16_t*)g, n, acc);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_clip_coef(const float* acc, float* coef, float* norm_out, float max_norm, void* stream) {
+  PZ_CHECK_ARG(acc && coef, "clip_coef: bad args");
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, ST, acc, coef, norm_out, max_norm);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float off, float scale,
+                               void* stream) {
+  PZ_CHECK_ARG(x && n >= 0, "fill_uniform: bad args");
+  if (n == 0) return PZ_OK;
+  const int64_t blocks = n / 256 + 1 < 16384 ? n / 256 + 1 : 16384;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3((unsigned)blocks), dim3(256), 0, ST, x, (int)out_fp32, n, seed, off,
+                     scale);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream) {
+  PZ_CHECK_ARG(x && y && n >= 0, "cast: bad args");
+  if (n == 0) return PZ_OK;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(nblk(n)), dim3(256), 0, ST, x, (bf16_t*)y, n);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream) {
+  PZ_CHECK_ARG(x && y && n >= 0, "cast: bad args");
+  if (n == 0) return PZ_OK;
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(nblk(n)), dim3(256), 0, ST, (const bf16_t*)x, y, n);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

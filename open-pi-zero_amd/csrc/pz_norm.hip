@@ -1,0 +1,403 @@
+// Row normalisations for the Pi0 path (memory-bound, one wave per row,
+// 16-byte vector loads, fp32 statistics):
+//   Gemma RMSNorm (paligemma/modules.py:7-21) and SigLIP LayerNorm
+//   (siglip.py:211,217,290), forward + backward, plus the column reductions
+//   used for norm-weight / bias / position-embedding gradients.
+#include "pz_common.h"
+
+namespace {
+
+constexpr int ROWS_PER_PART = 64;  // rows folded into one fp32 partial row of dw/db
+
+__device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
+  u32x4 r = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(r[i] << 16);
+    v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
+  u32x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = pack2bf(v[2 * i], v[2 * i + 1]);
+  *reinterpret_cast<u32x4*>(p) = r;
+}
+
+// --------------------------------------------------------------- RMSNorm ---
+template <int MAXC>
+__global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                          const bf16_t* __restrict__ w, bf16_t* y,
+                                                          int64_t ldy, float* rstd, int64_t R, int D,
+                                                          float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nc = D / 8;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      load8(x + row * ldx + ch * 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = warp_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  if (rstd && lane == 0) rstd[row] = r;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      float wv[8], o[8];
+      load8(w + ch * 8, wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * (1.f + wv[i]);
+      store8(y + row * ldy + ch * 8, o);
+    }
+  }
+}
+
+// one block = ROWS_PER_PART rows (4 waves x 16 rows); dw partial per block
+template <int MAXC>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
+    const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
+    const bf16_t* __restrict__ w, const float* __restrict__ rstd, const bf16_t* dres, bf16_t* dx,
+    int64_t lddx, float* dw_part, int64_t R, int D) {
+  __shared__ float red[4][MAXC * 64 * 8 > 4096 ? 4096 : MAXC * 64 * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nc = D / 8;
+  float dwacc[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwacc[c][i] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
+  for (int rr = wave; rr < ROWS_PER_PART; rr += 4) {
+    const int64_t row = r0 + rr;
+    if (row >= R) break;
+    const float r = rstd[row];
+    float xv[MAXC][8], gv[MAXC][8];
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nc) {
+        float dyv[8], wv[8];
+        load8(x + row * ldx + ch * 8, xv[c]);
+        load8(dy + row * lddy + ch * 8, dyv);
+        load8(w + ch * 8, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          gv[c][i] = dyv[i] * (1.f + wv[i]);
+          dot += gv[c][i] * xv[c][i];
+          dwacc[c][i] += dyv[i] * xv[c][i] * r;
+        }
+      }
+    }
+    dot = warp_sum(dot);
+    const float k = r * r * r * dot / (float)D;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nc) {
+        float o[8];
+        if (dres) load8(dres + row * lddx + ch * 8, o);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += r * gv[c][i] - k * xv[c][i];
+        store8(dx + row * lddx + ch * 8, o);
+      }
+    }
+  }
+  if (!dw_part) return;
+  // reduce dwacc over the 4 waves -> one partial row
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][ch * 8 + i] = dwacc[c][i];
+  }
+  __syncthreads();
+  for (int n = threadIdx.x; n < D; n += 256)
+    dw_part[(int64_t)blockIdx.x * D + n] = red[0][n] + red[1][n] + red[2][n] + red[3][n];
+}
+
+// ------------------------------------------------------------- LayerNorm ---
+template <int MAXC>
+__global__ void __launch_bounds__(256) layernorm_fwd_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                            const bf16_t* __restrict__ w,
+                                                            const bf16_t* __restrict__ b, bf16_t* y,
+                                                            int64_t ldy, float* mean, float* rstd,
+                                                            int64_t R, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nc = D / 8;
+  float v[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      load8(x + row * ldx + ch * 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  const float mu = warp_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        ss += d * d;
+      }
+  }
+  const float r = rsqrtf(warp_sum(ss) / (float)D + eps);
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = r;
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      float wv[8], bv[8], o[8];
+      load8(w + ch * 8, wv);
+      load8(b + ch * 8, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * r * wv[i] + bv[i];
+      store8(y + row * ldy + ch * 8, o);
+    }
+  }
+}
+
+template <int MAXC>
+__global__ void __launch_bounds__(256) layernorm_bwd_kernel(
+    const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
+    const bf16_t* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16_t* dres, bf16_t* dx, int64_t lddx, float* dw_part, float* db_part, int64_t R, int D) {
+  __shared__ float red[4][2048];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nc = D / 8;
+  float dwacc[MAXC][8], dbacc[MAXC][8];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dwacc[c][i] = dbacc[c][i] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
+  for (int rr = wave; rr < ROWS_PER_PART; rr += 4) {
+    const int64_t row = r0 + rr;
+    if (row >= R) break;
+    const float mu = mean[row], r = rstd[row];
+    float xh[MAXC][8], gv[MAXC][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nc) {
+        float dyv[8], wv[8];
+        load8(x + row * ldx + ch * 8, xh[c]);
+        load8(dy + row * lddy + ch * 8, dyv);
+        load8(w + ch * 8, wv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          xh[c][i] = (xh[c][i] - mu) * r;
+          gv[c][i] = dyv[i] * wv[i];
+          sg += gv[c][i];
+          sgx += gv[c][i] * xh[c][i];
+          dwacc[c][i] += dyv[i] * xh[c][i];
+          dbacc[c][i] += dyv[i];
+        }
+      }
+    }
+    sg = warp_sum(sg) / (float)D;
+    sgx = warp_sum(sgx) / (float)D;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nc) {
+        float o[8];
+        if (dres) load8(dres + row * lddx + ch * 8, o);
+        else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] += r * (gv[c][i] - sg - xh[c][i] * sgx);
+        store8(dx + row * lddx + ch * 8, o);
+      }
+    }
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    float* dst = pass == 0 ? dw_part : db_part;
+    if (!dst) continue;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      if (ch < nc)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[wave][ch * 8 + i] = pass == 0 ? dwacc[c][i] : dbacc[c][i];
+    }
+    __syncthreads();
+    for (int n = threadIdx.x; n < D; n += 256)
+      dst[(int64_t)blockIdx.x * D + n] = red[0][n] + red[1][n] + red[2][n] + red[3][n];
+    __syncthreads();
+  }
+}
+
+__global__ void reduce_parts_kernel(const float* __restrict__ part, int64_t P, int64_t D, bf16_t* out,
+                                    int beta) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= D) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < P; ++p) s += part[p * D + n];
+  if (beta) s += bf2f(out[n]);
+  out[n] = f2bf(s);
+}
+
+// column sums of a bf16 matrix: pass 1 -> ws[chunk][n], pass 2 -> out
+__global__ void colsum_pass1(const bf16_t* __restrict__ X, int64_t ld, int64_t M, int64_t N,
+                             int64_t rows_per_chunk, float* ws) {
+  const int64_t n2 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (n2 >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(M, r0 + rows_per_chunk);
+  float s0 = 0.f, s1 = 0.f;
+  const bool two = n2 + 1 < N;
+  for (int64_t r = r0; r < r1; ++r) {
+    s0 += bf2f(X[r * ld + n2]);
+    if (two) s1 += bf2f(X[r * ld + n2 + 1]);
+  }
+  ws[blockIdx.y * N + n2] = s0;
+  if (two) ws[blockIdx.y * N + n2 + 1] = s1;
+}
+
+__global__ void batch_sum_kernel(const bf16_t* __restrict__ X, int64_t B, int64_t stride, int64_t n,
+                                 bf16_t* out, int beta) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < B; ++b) s += bf2f(X[b * stride + i]);
+  if (beta) s += bf2f(out[i]);
+  out[i] = f2bf(s);
+}
+
+}  // namespace
+
+extern "C" int64_t pz_norm_rows_per_part(void) { return ROWS_PER_PART; }
+
+#define NORM_DISPATCH(KERNEL, GRID, ...)                                                   \
+  do {                                                                                    \
+    const int nc = (int)(D / 8);                                                          \
+    if (nc <= 64) hipLaunchKernelGGL(KERNEL<1>, GRID, dim3(256), 0, st, __VA_ARGS__);     \
+    else if (nc <= 128) hipLaunchKernelGGL(KERNEL<2>, GRID, dim3(256), 0, st, __VA_ARGS__); \
+    else if (nc <= 192) hipLaunchKernelGGL(KERNEL<3>, GRID, dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<4>, GRID, dim3(256), 0, st, __VA_ARGS__);              \
+  } while (0)
+
+static int check_norm(const void* x, int64_t ldx, const void* y, int64_t ldy, int64_t D) {
+  PZ_CHECK_ARG(D % 8 == 0 && D <= 2048, "norm: D=%lld must be a multiple of 8 and <= 2048", (long long)D);
+  PZ_CHECK_ARG(ldx % 8 == 0 && ldy % 8 == 0 && PZ_ALIGNED(x, 16) && PZ_ALIGNED(y, 16),
+               "norm: rows must be 16-byte aligned");
+  return PZ_OK;
+}
+
+extern "C" int pz_rmsnorm_fwd(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, float* rstd,
+                              int64_t R, int64_t D, float eps, void* stream) {
+  int e = check_norm(x, ldx, y, ldy, D);
+  if (e) return e;
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + 3) / 4));
+  NORM_DISPATCH(rmsnorm_fwd_kernel, grid, (const bf16_t*)x, ldx, (const bf16_t*)w, (bf16_t*)y, ldy, rstd, R,
+                (int)D, eps);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
+                              const float* rstd, const void* dres, void* dx, int64_t lddx, float* dw_part,
+                              int64_t R, int64_t D, void* stream) {
+  int e = check_norm(x, ldx, dx, lddx, D);
+  if (e) return e;
+  PZ_CHECK_ARG(lddy % 8 == 0, "rmsnorm_bwd: lddy");
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
+  NORM_DISPATCH(rmsnorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
+                rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, R, (int)D);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_layernorm_fwd(const void* x, int64_t ldx, const void* w, const void* b, void* y, int64_t ldy,
+                                float* mean, float* rstd, int64_t R, int64_t D, float eps, void* stream) {
+  int e = check_norm(x, ldx, y, ldy, D);
+  if (e) return e;
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + 3) / 4));
+  NORM_DISPATCH(layernorm_fwd_kernel, grid, (const bf16_t*)x, ldx, (const bf16_t*)w, (const bf16_t*)b,
+                (bf16_t*)y, ldy, mean, rstd, R, (int)D, eps);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
+                                const float* mean, const float* rstd, const void* dres, void* dx, int64_t lddx,
+                                float* dw_part, float* db_part, int64_t R, int64_t D, void* stream) {
+  int e = check_norm(x, ldx, dx, lddx, D);
+  if (e) return e;
+  PZ_CHECK_ARG(lddy % 8 == 0, "layernorm_bwd: lddy");
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
+  NORM_DISPATCH(layernorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
+                mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream) {
+  PZ_CHECK_ARG(part && out && P > 0 && D > 0, "reduce_parts: bad args");
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     part, P, D, (bf16_t*)out, (int)beta);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_colsum(const void* X, int64_t ld, int64_t M, int64_t N, void* out, int32_t beta, float* ws,
+                         void* stream) {
+  PZ_CHECK_ARG(X && out && ws && M > 0 && N > 0, "colsum: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t chunks = M < 64 ? M : 64;
+  const int64_t rpc = (M + chunks - 1) / chunks;
+  dim3 grid((unsigned)((N / 2 + 1 + 255) / 256), (unsigned)chunks);
+  hipLaunchKernelGGL(colsum_pass1, grid, dim3(256), 0, st, (const bf16_t*)X, ld, M, N, rpc, ws);
+  PZ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_parts_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, (const float*)ws,
+                     chunks, N, (bf16_t*)out, (int)beta);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_batch_sum(const void* X, int64_t B, int64_t stride, int64_t n, void* out, int32_t beta,
+                            void* stream) {
+  PZ_CHECK_ARG(X && out && B > 0 && n > 0, "batch_sum: bad args");
+  hipLaunchKernelGGL(batch_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)X, B, stride, n, (bf16_t*)out, (int)beta);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

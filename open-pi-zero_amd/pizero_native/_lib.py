@@ -1,0 +1,124 @@
+"""ctypes binding of libpizero_hip.so (the C ABI declared in include/pz_abi.h).
+
+The library is loaded once, from the package directory only; there is no
+fallback path: if it is missing or fails to load, every op raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
+
+PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
+
+i64, i32, f32, vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
+fp = C.POINTER(C.c_float)
+
+
+class GemmArgs(C.Structure):
+    _fields_ = [
+        ("M", i64), ("N", i64), ("K", i64),
+        ("A", vp), ("lda", i64), ("a_kcontig", i32),
+        ("B", vp), ("ldb", i64), ("b_kcontig", i32),
+        ("C", vp), ("ldc", i64), ("c_fp32", i32),
+        ("batch", i64), ("batch_inner", i64),
+        ("sA_outer", i64), ("sA_inner", i64), ("sB_outer", i64), ("sB_inner", i64),
+        ("sC_outer", i64), ("sC_inner", i64), ("sR_outer", i64), ("sR_inner", i64),
+        ("epilogue", i32), ("alpha", f32), ("beta_accum", i32),
+        ("bias", vp), ("resid", vp), ("ld_resid", i64), ("aux", vp), ("ld_aux", i64),
+        ("geglu_inter", i64),
+    ]
+
+
+class SmallGemmArgs(C.Structure):
+    _fields_ = [
+        ("M", i64), ("N", i64), ("K", i64),
+        ("A", vp), ("sAm", i64), ("sAk", i64),
+        ("B", vp), ("sBk", i64), ("sBn", i64),
+        ("C", vp), ("ldc", i64), ("bias", vp), ("alpha", f32), ("beta", i32),
+    ]
+
+
+class SoftmaxArgs(C.Structure):
+    _fields_ = [
+        ("S", vp), ("lds", i64), ("P", vp), ("ldp", i64), ("tcap", vp),
+        ("R", i64), ("N", i64), ("scale", f32), ("cap", f32), ("mask_mode", i32),
+        ("rows_per_batch", i64), ("heads", i64), ("qoff", i64),
+        ("cnt", vp), ("prefix", i64), ("cond", i64),
+        ("mask", vp), ("ldm", i64), ("mask_bstride", i64),
+    ]
+
+
+# name -> argtypes (restype int unless listed in _RESTYPE)
+SIGNATURES = {
+    "pz_gemm": [C.POINTER(GemmArgs), vp],
+    "pz_gemm_small": [C.POINTER(SmallGemmArgs), vp],
+    "pz_rmsnorm_fwd": [vp, i64, vp, vp, i64, vp, i64, i64, f32, vp],
+    "pz_rmsnorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, i64, vp],
+    "pz_layernorm_fwd": [vp, i64, vp, vp, vp, i64, vp, vp, i64, i64, f32, vp],
+    "pz_layernorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, vp, vp, i64, i64, vp],
+    "pz_norm_rows_per_part": [],
+    "pz_reduce_parts": [vp, i64, i64, vp, i32, vp],
+    "pz_colsum": [vp, i64, i64, i64, vp, i32, vp, vp],
+    "pz_batch_sum": [vp, i64, i64, i64, vp, i32, vp],
+    "pz_rope_table": [vp, i64, i64, f32, vp],
+    "pz_qkv_rope_split": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
+    "pz_qkv_rope_split_bwd": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
+    "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],
+    "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
+    "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],
+    "pz_embed_merge": [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, f32, f32, vp],
+    "pz_embed_merge_bwd": [vp, vp, vp, i64, i64, i64, i64, i64, f32, vp],
+    "pz_time_embed": [vp, vp, i64, i64, f32, vp],
+    "pz_concat_time": [vp, vp, vp, i64, i64, i64, vp],
+    "pz_split_time_grad": [vp, vp, i64, i64, vp],
+    "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
+    "pz_flow_loss": [vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
+    "pz_euler_step": [vp, vp, i64, vp, i64, i64, i64, f32, vp],
+    "pz_clamp": [vp, i64, f32, f32, vp],
+    "pz_geglu_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, vp],
+    "pz_act_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, vp],
+    "pz_adamw": [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, f32, vp, vp],
+    "pz_sumsq": [vp, i64, vp, vp],
+    "pz_clip_coef": [vp, vp, vp, f32, vp],
+    "pz_fill_uniform": [vp, i32, i64, C.c_uint64, f32, f32, vp],
+    "pz_cast_f32_bf16": [vp, vp, i64, vp],
+    "pz_cast_bf16_f32": [vp, vp, i64, vp],
+    "pz_last_error": [],
+    "pz_abi_version": [],
+}
+_RESTYPE = {"pz_last_error": C.c_char_p, "pz_norm_rows_per_part": i64}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libpizero_hip.so (raises if absent: there is no non-native path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"{LIB_PATH} not found: build it with `python open-pi-zero_amd/build_native.py` "
+                "(or __graft_entry__.build()); the Pi0 path has no CPU/eager fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, argt in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = argt
+            fn.restype = _RESTYPE.get(name, C.c_int)
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().pz_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed (rc={rc}): {msg}")
+    return rc

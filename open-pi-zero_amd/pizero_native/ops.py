@@ -1,0 +1,281 @@
+"""Thin torch-tensor front-ends over the C ABI (pointer/size plumbing only).
+
+Every function enqueues HIP kernels on torch's current stream; tensors are
+owned by the caller (PyTorch caching allocator), nothing is allocated on the
+native side, so every sequence of these calls is hipGraph-capturable.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import (
+    PZ_EPI_GEGLU,
+    PZ_EPI_GELU,
+    PZ_EPI_NONE,
+    PZ_EPI_SILU,
+    GemmArgs,
+    SmallGemmArgs,
+    SoftmaxArgs,
+    call,
+)
+
+__all__ = ["PZ_EPI_NONE", "PZ_EPI_GELU", "PZ_EPI_GEGLU", "PZ_EPI_SILU"]
+
+BF16 = torch.bfloat16
+
+
+def _st():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, *, epi=PZ_EPI_NONE, alpha=1.0, beta=False,
+         bias=None, resid=None, ld_resid=0, aux=None, ld_aux=0, geglu_inter=0, batch=1, batch_inner=1,
+         sA=(0, 0), sB=(0, 0), sC=(0, 0), sR=(0, 0)):
+    """Raw GEMM: see pz_gemm_args in include/pz_abi.h.  Element strides."""
+    a = GemmArgs()
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.A, a.lda, a.a_kcontig = _p(A), int(lda), int(bool(a_kc))
+    a.B, a.ldb, a.b_kcontig = _p(B), int(ldb), int(bool(b_kc))
+    a.C, a.ldc, a.c_fp32 = _p(Cm), int(ldc), int(Cm.dtype == torch.float32)
+    a.batch, a.batch_inner = int(batch), int(batch_inner)
+    a.sA_outer, a.sA_inner = int(sA[0]), int(sA[1])
+    a.sB_outer, a.sB_inner = int(sB[0]), int(sB[1])
+    a.sC_outer, a.sC_inner = int(sC[0]), int(sC[1])
+    a.sR_outer, a.sR_inner = int(sR[0]), int(sR[1])
+    a.epilogue, a.alpha, a.beta_accum = int(epi), float(alpha), int(bool(beta))
+    a.bias, a.resid, a.ld_resid = _p(bias), _p(resid), int(ld_resid)
+    a.aux, a.ld_aux, a.geglu_inter = _p(aux), int(ld_aux), int(geglu_inter)
+    call("pz_gemm", C.byref(a), _st())
+
+
+def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha=1.0, beta=False):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T): nn.Linear forward (x, out may be row-strided 2-D views)."""
+    M, K = x.shape
+    N = W.shape[0]
+    if epi == PZ_EPI_GEGLU:
+        I = N // 2
+        gemm(M, N, K, x, x.stride(0), True, W, W.stride(0), True, out, out.stride(0), epi=epi,
+             aux=aux, ld_aux=0 if aux is None else aux.stride(0), geglu_inter=I, alpha=alpha)
+        return out
+    gemm(M, N, K, x, x.stride(0), True, W, W.stride(0), True, out, out.stride(0), epi=epi, alpha=alpha,
+         beta=beta, bias=bias, resid=resid, ld_resid=0 if resid is None else resid.stride(0), aux=aux,
+         ld_aux=0 if aux is None else aux.stride(0))
+    return out
+
+
+def linear_dgrad(dy, W, dx, *, beta=False, resid=None):
+    """dx[M,K] (+)= dy[M,N] @ W[N,K] (+ resid)."""
+    M, N = dy.shape
+    K = W.shape[1]
+    gemm(M, K, N, dy, dy.stride(0), True, W, W.stride(0), False, dx, dx.stride(0), beta=beta,
+         resid=resid, ld_resid=0 if resid is None else resid.stride(0))
+    return dx
+
+
+def linear_wgrad(dy, x, dW, *, beta=False):
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]."""
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, dW, dW.stride(0), beta=beta)
+    return dW
+
+
+def small_linear(x, W, out, *, bias=None, beta=False):
+    """out[M,N] = x[M,K] W[N,K]^T for tiny K or N (7-dim action/proprio)."""
+    M, K = x.shape
+    N = W.shape[0]
+    a = SmallGemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A, a.sAm, a.sAk = _p(x), x.stride(0), x.stride(1)
+    a.B, a.sBk, a.sBn = _p(W), W.stride(1), W.stride(0)
+    a.C, a.ldc, a.bias, a.alpha, a.beta = _p(out), out.stride(0), _p(bias), 1.0, int(beta)
+    call("pz_gemm_small", C.byref(a), _st())
+    return out
+
+
+def small_gemm(M, N, K, A, sAm, sAk, B, sBk, sBn, out, ldc, *, beta=False, bias=None):
+    a = SmallGemmArgs()
+    a.M, a.N, a.K = M, N, K
+    a.A, a.sAm, a.sAk = _p(A), sAm, sAk
+    a.B, a.sBk, a.sBn = _p(B), sBk, sBn
+    a.C, a.ldc, a.bias, a.alpha, a.beta = _p(out), ldc, _p(bias), 1.0, int(beta)
+    call("pz_gemm_small", C.byref(a), _st())
+    return out
+
+
+def rmsnorm(x, w, y, rstd, eps):
+    R, D = x.shape
+    call("pz_rmsnorm_fwd", _p(x), x.stride(0), _p(w), _p(y), y.stride(0), _p(rstd), R, D, float(eps), _st())
+    return y
+
+
+def rmsnorm_bwd(dy, x, w, rstd, dx, dres=None, dw_part=None):
+    R, D = x.shape
+    call("pz_rmsnorm_bwd", _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w), _p(rstd), _p(dres), _p(dx),
+         dx.stride(0), _p(dw_part), R, D, _st())
+    return dx
+
+
+def layernorm(x, w, b, y, mean, rstd, eps):
+    R, D = x.shape
+    call("pz_layernorm_fwd", _p(x), x.stride(0), _p(w), _p(b), _p(y), y.stride(0), _p(mean), _p(rstd), R, D,
+         float(eps), _st())
+    return y
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dx, dres=None, dw_part=None, db_part=None):
+    R, D = x.shape
+    call("pz_layernorm_bwd", _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w), _p(mean), _p(rstd), _p(dres),
+         _p(dx), dx.stride(0), _p(dw_part), _p(db_part), R, D, _st())
+    return dx
+
+
+_RPP = None
+
+
+def rows_per_part():
+    global _RPP
+    if _RPP is None:
+        from ._lib import lib
+
+        _RPP = int(lib().pz_norm_rows_per_part())
+    return _RPP
+
+
+def reduce_parts(part, out, beta=False):
+    P, D = part.shape
+    call("pz_reduce_parts", _p(part), P, D, _p(out), int(beta), _st())
+    return out
+
+
+def colsum(X, out, ws, beta=False):
+    M, N = X.shape
+    call("pz_colsum", _p(X), X.stride(0), M, N, _p(out), int(beta), _p(ws), _st())
+    return out
+
+
+def batch_sum(X, B, stride, n, out, beta=False):
+    call("pz_batch_sum", _p(X), B, stride, n, _p(out), int(beta), _st())
+    return out
+
+
+def rope_table(cs, max_pos, head_dim, theta):
+    call("pz_rope_table", _p(cs), max_pos, head_dim, float(theta), _st())
+    return cs
+
+
+def qkv_rope_split(qkv, pos, cs, q_out, k_out, v_out, B, T, nh, nkv, hd, Lq, qoff, Lk, koff):
+    call("pz_qkv_rope_split", _p(qkv), _p(pos), _p(cs), _p(q_out), _p(k_out), _p(v_out), B, T, nh, nkv, hd,
+         Lq, qoff, Lk, koff, _st())
+
+
+def qkv_rope_split_bwd(dq, dk, dv, pos, cs, dqkv, B, T, nh, nkv, hd, Lq, qoff, Lk, koff):
+    call("pz_qkv_rope_split_bwd", _p(dq), _p(dk), _p(dv), _p(pos), _p(cs), _p(dqkv), B, T, nh, nkv, hd, Lq,
+         qoff, Lk, koff, _st())
+
+
+def attn_softmax(S, lds, P, ldp, R, N, scale, cap=0.0, tcap=None, mask_mode=0, rows_per_batch=1, heads=1,
+                 qoff=0, cnt=None, prefix=0, cond=0, mask=None, ldm=0, mask_bstride=0):
+    a = SoftmaxArgs()
+    a.S, a.lds, a.P, a.ldp, a.tcap = _p(S), lds, _p(P), ldp, _p(tcap)
+    a.R, a.N, a.scale, a.cap, a.mask_mode = R, N, float(scale), float(cap), mask_mode
+    a.rows_per_batch, a.heads, a.qoff = rows_per_batch, heads, qoff
+    a.cnt, a.prefix, a.cond = _p(cnt), prefix, cond
+    a.mask, a.ldm, a.mask_bstride = _p(mask), ldm, mask_bstride
+    call("pz_attn_softmax", C.byref(a), _st())
+
+
+def attn_softmax_bwd(P, dP, lddp, tcap, dS, ldp, R, N, scale, cap):
+    call("pz_attn_softmax_bwd", _p(P), _p(dP), lddp, _p(tcap), _p(dS), ldp, R, N, float(scale), float(cap),
+         _st())
+
+
+def patchify(pix, cols, ps):
+    B, _, H, W = pix.shape
+    call("pz_patchify", _p(pix), _p(cols), B, H, W, ps, cols.stride(0), _st())
+
+
+def embed_merge(ids, table, img, out, n_img, image_token, pad_token, emb_scale, img_scale):
+    B, P = ids.shape
+    D = table.shape[1]
+    call("pz_embed_merge", _p(ids), _p(table), _p(img), _p(out), B, P, D, n_img, image_token, pad_token,
+         float(emb_scale), float(img_scale), _st())
+
+
+def embed_merge_bwd(ids, dout, dimg, n_img, image_token, img_scale):
+    B, P = ids.shape
+    D = dout.shape[-1]
+    call("pz_embed_merge_bwd", _p(ids), _p(dout), _p(dimg), B, P, D, n_img, image_token, float(img_scale),
+         _st())
+
+
+def time_embed(t, out, max_period):
+    B, D = out.shape
+    call("pz_time_embed", _p(t), _p(out), B, D, float(max_period), _st())
+
+
+def concat_time(temb, e1, out, B, H, D):
+    call("pz_concat_time", _p(temb), _p(e1), _p(out), B, H, D, _st())
+
+
+def split_time_grad(dcat, de1, rows, D):
+    call("pz_split_time_grad", _p(dcat), _p(de1), rows, D, _st())
+
+
+def flow_psi(x0, x1, t, psi, sig_min):
+    B = x0.shape[0]
+    call("pz_flow_psi", _p(x0), _p(x1), _p(t), _p(psi), B, x0[0].numel(), float(sig_min), _st())
+
+
+def flow_loss(v, ldv, x0, x1, loss, dv, grad_scale, B, H, A, sig_min):
+    call("pz_flow_loss", _p(v), ldv, _p(x0), _p(x1), _p(loss), _p(dv), _p(grad_scale), B, H, A, float(sig_min),
+         _st())
+
+
+def euler_step(action, v, ldv, t, B, H, A, dt):
+    call("pz_euler_step", _p(action), _p(v), ldv, _p(t), B, H, A, float(dt), _st())
+
+
+def clamp_(x, lo, hi):
+    call("pz_clamp", _p(x), x.numel(), float(lo), float(hi), _st())
+
+
+def geglu_bwd(dh, gu, dgu, h_out, M, I):
+    call("pz_geglu_bwd", _p(dh), dh.stride(0), _p(gu), gu.stride(0), _p(dgu), _p(h_out),
+         0 if h_out is None else h_out.stride(0), M, I, _st())
+
+
+def act_bwd(dh, pre, dpre, h_out, act):
+    M, N = pre.shape
+    call("pz_act_bwd", _p(dh), dh.stride(0), _p(pre), pre.stride(0), _p(dpre), _p(h_out),
+         0 if h_out is None else h_out.stride(0), M, N, int(act), _st())
+
+
+def adamw(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, gscale=None):
+    call("pz_adamw", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(b1), float(b2), float(eps),
+         float(wd), float(bc1), float(bc2), _p(gscale), _st())
+
+
+def sumsq(g, acc):
+    call("pz_sumsq", _p(g), g.numel(), _p(acc), _st())
+
+
+def clip_coef(acc, coef, norm_out, max_norm):
+    call("pz_clip_coef", _p(acc), _p(coef), _p(norm_out), float(max_norm), _st())
+
+
+def fill_uniform(x, seed, off, scale):
+    call("pz_fill_uniform", _p(x), int(x.dtype == torch.float32), x.numel(), C.c_uint64(seed & (2**64 - 1)),
+         float(off), float(scale), _st())
+    return x
+
+
+def cast_to_bf16(x, y):
+    call("pz_cast_f32_bf16", _p(x), _p(y), x.numel(), _st())

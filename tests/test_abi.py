@@ -1,0 +1,42 @@
+"""The C-ABI library loads without a GPU and exports every symbol include/pz_abi.h declares."""
+
+import os
+import re
+
+from tests.conftest import ROOT
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "pz_abi.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(pz_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    syms = declared_symbols()
+    assert "pz_gemm" in syms and "pz_attn_softmax" in syms and "pz_adamw" in syms
+    assert len(syms) >= 30
+
+
+def test_library_exports_all_declared_symbols():
+    import pizero_native
+    from pizero_native._lib import SIGNATURES
+
+    L = pizero_native.lib()
+    for s in declared_symbols():
+        assert hasattr(L, s), s
+        assert s in SIGNATURES, f"{s} has no ctypes signature"
+    assert L.pz_abi_version() == 1
+
+
+def test_error_path_without_gpu():
+    """A host-side argument check fails before any launch and reports a message."""
+    import ctypes
+
+    import pizero_native
+    from pizero_native._lib import GemmArgs
+
+    a = GemmArgs()
+    rc = pizero_native.lib().pz_gemm(ctypes.byref(a), None)
+    assert rc == 1
+    assert b"bad dims" in pizero_native.lib().pz_last_error()

@@ -1,0 +1,285 @@
+"""Per-kernel numerics on the MI355X vs a plain PyTorch fp32 reference of the same op.
+
+Tolerances: bf16 inputs are identical on both sides; the HIP kernels
+accumulate in fp32 and round the output once to bf16, so errors are bounded by
+~1 bf16 ulp of the output (2^-8 relative) plus fp32 summation-order noise.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pizero_native
+
+    pizero_native.lib()
+    torch.manual_seed(0)
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=dev) * scale).to(torch.bfloat16)
+
+
+def close(out, ref, rtol=1.6e-2, atol=1e-2):
+    out, ref = out.float(), ref.float()
+    err = (out - ref).abs()
+    tol = atol + rtol * ref.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{bad} mismatches, max err {err.max().item():.4g}, max ref {ref.abs().max().item():.4g}"
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 136), (4416, 2560, 2048), (7, 33, 72), (1, 2048, 2048),
+                                   (5, 1024, 4096), (276, 2560, 2048)])
+def test_linear_forward(M, N, K):
+    from pizero_native import ops
+
+    x, W = bf(M, K), bf(N, K, scale=K ** -0.5)
+    b = bf(N)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, out, bias=b)
+    close(out, x.float() @ W.float().t() + b.float())
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 192, 128), (4416, 1152, 2048), (281, 256, 2248)])
+def test_dgrad_and_wgrad_layouts(M, N, K):
+    from pizero_native import ops
+
+    dy, W, x = bf(M, N), bf(N, K, scale=N ** -0.5), bf(M, K)
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_dgrad(dy, W, dx)
+    close(dx, dy.float() @ W.float())
+    dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_wgrad(dy, x, dW)
+    close(dW, dy.float().t() @ x.float(), atol=0.05 * math.sqrt(M) / 16)
+    dW2 = dW.clone()
+    ops.linear_wgrad(dy, x, dW2, beta=True)
+    close(dW2, 2 * (dy.float().t() @ x.float()), atol=0.1 * math.sqrt(M) / 16)
+
+
+def test_all_four_layouts_batched_fp32_out():
+    from pizero_native import ops
+
+    Bt, M, N, K = 3, 96, 80, 104
+    A = bf(Bt, M, K)
+    Bm = bf(Bt, N, K)
+    ref = A.float() @ Bm.float().transpose(1, 2)
+    for akc in (True, False):
+        for bkc in (True, False):
+            Aop = A if akc else A.transpose(1, 2).contiguous()
+            Bop = Bm if bkc else Bm.transpose(1, 2).contiguous()
+            C = torch.zeros(Bt, M, N, device=dev, dtype=torch.float32)
+            ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, C, N, batch=Bt,
+                     batch_inner=1, sA=(M * K, 0), sB=(N * K, 0), sC=(M * N, 0))
+            close(C, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_epilogues_gelu_resid_geglu_silu():
+    from pizero_native import ops
+
+    M, K, I = 300, 256, 192
+    x = bf(M, K)
+    W = bf(2 * I, K, scale=K ** -0.5)
+    h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+    gu = torch.empty(M, 2 * I, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+    ref = x.float() @ W.float().t()
+    close(gu, ref)
+    g, u = ref[:, :I], ref[:, I:]
+    close(h, torch.nn.functional.gelu(g, approximate="tanh") * u)
+    # skinny path (M <= 16) for the same op
+    h2 = torch.empty(5, I, device=dev, dtype=torch.bfloat16)
+    ops.linear(x[:5], W, h2, epi=ops.PZ_EPI_GEGLU)
+    close(h2, (torch.nn.functional.gelu(g, approximate="tanh") * u)[:5])
+    # gelu + bias + residual
+    b = bf(I)
+    r = bf(M, I)
+    pre = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+    o = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W[:I], o, bias=b, epi=ops.PZ_EPI_GELU, aux=pre, resid=r)
+    p = x.float() @ W[:I].float().t() + b.float()
+    close(pre, p)
+    close(o, torch.nn.functional.gelu(p, approximate="tanh") + r.float(), atol=2e-2)
+    ops.linear(x, W[:I], o, bias=b, epi=ops.PZ_EPI_SILU, aux=pre)
+    close(o, torch.nn.functional.silu(p))
+
+
+def test_small_gemm():
+    from pizero_native import ops
+
+    x, W, b = bf(20, 7), bf(64, 7), bf(64)
+    out = torch.empty(20, 64, device=dev, dtype=torch.bfloat16)
+    ops.small_linear(x, W, out, bias=b)
+    close(out, x.float() @ W.float().t() + b.float())
+
+
+@pytest.mark.parametrize("D", [1024, 2048, 64])
+def test_rmsnorm_fwd_bwd(D):
+    from pizero_native import ops
+
+    R = 333
+    x = bf(R, D)
+    w = bf(D, scale=0.1)
+    y = torch.empty_like(x)
+    rstd = torch.empty(R, device=dev)
+    ops.rmsnorm(x, w, y, rstd, 1e-6)
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + wr)
+    close(y, yr)
+    dy = bf(R, D)
+    yr.backward(dy.float())
+    dres = bf(R, D)
+    dx = torch.empty_like(x)
+    rpp = ops.rows_per_part()
+    part = torch.empty((R + rpp - 1) // rpp, D, device=dev)
+    ops.rmsnorm_bwd(dy, x, w, rstd, dx, dres=dres, dw_part=part)
+    close(dx, xr.grad + dres.float(), atol=2e-2)
+    dw = torch.empty(D, device=dev, dtype=torch.bfloat16)
+    ops.reduce_parts(part, dw)
+    close(dw, wr.grad, atol=0.1)
+
+
+def test_layernorm_fwd_bwd():
+    from pizero_native import ops
+
+    R, D = 300, 1152
+    x = bf(R, D) * 3 + 1
+    w, b = bf(D) * 0.1 + 1, bf(D) * 0.1
+    y = torch.empty_like(x)
+    mean, rstd = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    ops.layernorm(x, w, b, y, mean, rstd, 1e-6)
+    xr, wr, br = (t.float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-6)
+    close(y, yr)
+    dy = bf(R, D)
+    yr.backward(dy.float())
+    dx = torch.empty_like(x)
+    rpp = ops.rows_per_part()
+    P = (R + rpp - 1) // rpp
+    pw, pb = torch.empty(P, D, device=dev), torch.empty(P, D, device=dev)
+    ops.layernorm_bwd(dy, x, w, mean, rstd, dx, dw_part=pw, db_part=pb)
+    close(dx, xr.grad, atol=2e-2)
+    dw, db = torch.empty(D, device=dev, dtype=torch.bfloat16), torch.empty(D, device=dev, dtype=torch.bfloat16)
+    ops.reduce_parts(pw, dw)
+    ops.reduce_parts(pb, db)
+    close(dw, wr.grad, atol=0.1)
+    close(db, br.grad, atol=0.1)
+    db2 = torch.empty(D, device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(64 * D, device=dev)
+    ops.colsum(dy, db2, ws)
+    close(db2, dy.float().sum(0), atol=0.1)
+
+
+def _block_mask(cnt, P, C, Lq_off, Lq, L):
+    m = torch.zeros(len(cnt), Lq, L, dtype=torch.bool)
+    for b, c in enumerate(cnt):
+        for qi in range(Lq):
+            i = Lq_off + qi
+            for j in range(L):
+                if i < P:
+                    ok = i < c and j < c
+                elif i < P + C:
+                    ok = j < c or (P <= j < P + C)
+                else:
+                    ok = j < c or j >= P
+                m[b, qi, j] = ok
+    return m
+
+
+def test_softmax_block_mask_softcap_fwd_bwd():
+    from pizero_native import ops
+
+    B, P, C, H, nh = 2, 12, 1, 4, 8
+    L = P + C + H
+    Lp = 24
+    cnt = torch.tensor([10, 7], dtype=torch.int32, device=dev)
+    R = B * L * nh
+    S = torch.randn(R, Lp, device=dev) * 40
+    Pm = torch.empty(R, Lp, device=dev, dtype=torch.bfloat16)
+    tc = torch.empty(R, Lp, device=dev, dtype=torch.bfloat16)
+    ops.attn_softmax(S, Lp, Pm, Lp, R, L, 1 / 16, cap=50.0, tcap=tc, mask_mode=1, rows_per_batch=L * nh, heads=nh,
+                     qoff=0, cnt=cnt, prefix=P, cond=C)
+    allowed = _block_mask(cnt.tolist(), P, C, 0, L, L).to(dev)  # [B, L, L]
+    allowed = allowed[:, :, None, :].expand(B, L, nh, L).reshape(R, L)
+    s = (S[:, :L] / 16).requires_grad_()
+    lg = torch.tanh(s / 50) * 50
+    lg = lg + torch.where(allowed, 0.0, torch.finfo(torch.float32).min)
+    ref = torch.softmax(lg, -1)
+    close(Pm[:, :L], ref, atol=2e-3)
+    assert (Pm[:, L:] == 0).all()
+    dP = torch.randn(R, Lp, device=dev)
+    ref.backward(dP[:, :L])
+    dS = torch.empty(R, Lp, device=dev, dtype=torch.bfloat16)
+    ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, R, L, 1 / 16, 50.0)
+    valid = allowed.any(-1)  # fully-masked rows: gradient unused downstream
+    close(dS[valid, :L], s.grad[valid] / 16, atol=3e-3)
+
+
+def test_qkv_rope_split_roundtrip():
+    from pizero_native import ops
+
+    B, T, nh, nkv, hd, theta = 2, 5, 8, 1, 256, 100.0
+    qkv = bf(B * T, (nh + 2 * nkv) * hd)
+    pos = torch.arange(1, T + 1, device=dev).repeat(B, 1)
+    cs = torch.empty(64 * hd, device=dev)
+    ops.rope_table(cs, 63, hd, theta)
+    Lq, Lk, off = 9, 12, 3
+    q = torch.zeros(B, Lq, nh * hd, device=dev, dtype=torch.bfloat16)
+    k = torch.zeros(B, Lk, nkv * hd, device=dev, dtype=torch.bfloat16)
+    v = torch.zeros_like(k)
+    ops.qkv_rope_split(qkv, pos, cs, q, k, v, B, T, nh, nkv, hd, Lq, off, Lk, off)
+    inv = 1.0 / (theta ** (torch.arange(0, hd, 2, device=dev).float() / hd))
+    f = pos[:, :, None].float() * inv
+    emb = torch.cat([f, f], -1)
+    cos, sin = emb.cos(), emb.sin()
+    x = qkv.float().view(B, T, nh + 2 * nkv, hd)
+
+    def rot(t):
+        return t * cos[:, :, None] + torch.cat([-t[..., hd // 2:], t[..., : hd // 2]], -1) * sin[:, :, None]
+
+    close(q[:, off:off + T].view(B, T, nh, hd), rot(x[:, :, :nh]))
+    close(k[:, off:off + T].view(B, T, nkv, hd), rot(x[:, :, nh:nh + nkv]))
+    assert torch.equal(v[:, off:off + T].view(B, T, nkv, hd), x[:, :, nh + nkv:].to(torch.bfloat16))
+    dqkv = torch.empty_like(qkv)
+    ops.qkv_rope_split_bwd(q, k, v, pos, cs, dqkv, B, T, nh, nkv, hd, Lq, off, Lk, off)
+    close(dqkv, qkv, atol=2e-2)  # rotation is orthogonal: bwd(fwd(x)) = x
+
+
+def test_fill_uniform_matches_numpy_generator():
+    from oracle.synth import synth_tensor, tensor_seed
+    from pizero_native import ops
+
+    x = torch.empty(100003, device=dev, dtype=torch.float32)
+    ops.fill_uniform(x, tensor_seed("w.test"), 0.25, 0.5)
+    ref = synth_tensor("w.test", (100003,), 0.25, 0.5)
+    np.testing.assert_array_equal(x.cpu().numpy(), ref)
+
+
+def test_adamw_matches_torch():
+    from pizero_native import ops
+
+    n = 10000
+    p = bf(n)
+    g = bf(n)
+    m = torch.zeros(n, device=dev)
+    v = torch.zeros(n, device=dev)
+    pr = p.float().clone().requires_grad_()
+    opt = torch.optim.AdamW([pr], lr=1e-2, weight_decay=0.01)
+    for step in range(1, 4):
+        pr.grad = g.float()
+        opt.step()
+        ops.adamw(p, g, m, v, 1e-2, 0.9, 0.999, 1e-8, 0.01, 1 - 0.9 ** step, 1 - 0.999 ** step)
+    close(p, pr.detach(), atol=1e-2)
+    acc = torch.zeros(1, device=dev)
+    ops.sumsq(g, acc)
+    assert abs(acc.item() - (g.float() ** 2).sum().item()) < 1e-3 * acc.item()

@@ -1,0 +1,69 @@
+"""Pin the CPU oracle against fixtures produced by the reference itself.
+
+tests/golden/tiny.npz is written by tests/golden/make_golden.py, which imports
+/root/reference (shroglck/open-pi-zero) in the build container and runs
+PiZero.forward/backward/infer_action/infer_action_naive in fp32 on
+generator-defined weights.  The oracle must reproduce it to fp32 rounding.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from tests.oracle_helpers import O, load_golden, oracle_run
+
+REL = 2e-5  # fp32 restatement vs fp32 reference (different op order only)
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    g = load_golden("tiny")
+    out, inp = oracle_run(O.TINY_DIMS, int(g["bsz"]), ragged=True)
+    return g, out, inp
+
+
+def test_inputs_regenerate(tiny):
+    g, _, inp = tiny
+    np.testing.assert_array_equal(g["in/input_ids"], inp["input_ids"])
+    np.testing.assert_array_equal(g["in/attention_mask"], inp["attention_mask"])
+    np.testing.assert_array_equal(g["in/t"], inp["t"])
+    assert inp["attention_mask"].sum(1).tolist() != [inp["attention_mask"].shape[1]] * inp["attention_mask"].shape[0]
+
+
+def test_mask_builder_matches_reference(tiny):
+    g, _, inp = tiny
+    m, *_ = O.build_mask_and_positions(O.TINY_DIMS, torch.from_numpy(inp["attention_mask"]))
+    np.testing.assert_array_equal(m[:, 0].numpy(), g["fp32/mask"])
+
+
+def test_loss(tiny):
+    g, out, _ = tiny
+    ref = float(g["fp32/loss"])
+    assert abs(out["loss"] - ref) <= REL * abs(ref) + 1e-7
+
+
+def test_grads(tiny):
+    g, out, _ = tiny
+    names = [str(n) for n in g["grad_names"]]
+    assert len(names) > 30
+    for n in names:
+        ref_norm = float(g["fp32/gradnorm/" + n])
+        mine = out["grads"].get(n)
+        if ref_norm < 0:
+            assert mine is None, n
+            continue
+        assert mine is not None, n
+        assert abs(mine.double().norm().item() - ref_norm) <= 1e-4 * ref_norm + 1e-9, n
+        head = mine.double().flatten()[:64].numpy()
+        np.testing.assert_allclose(head, g["fp32/gradhead/" + n], rtol=1e-3, atol=1e-6 * max(ref_norm, 1e-3))
+
+
+def test_actions_cached_and_naive(tiny):
+    g, out, _ = tiny
+    np.testing.assert_allclose(out["actions"].numpy(), g["fp32/actions_unclipped"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["actions_naive"].numpy(), g["fp32/actions_naive_unclipped"], rtol=1e-4, atol=1e-5)
+
+
+def test_reference_bf16_deviation_recorded(tiny):
+    g, _, _ = tiny
+    assert abs(float(g["bf16/loss"]) - float(g["fp32/loss"])) < 0.05 * abs(float(g["fp32/loss"]))

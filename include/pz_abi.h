@@ -163,11 +163,11 @@ int pz_flow_psi(const float* x0, const float* x1, const float* t, void* psi, int
                 float sig_min, void* stream);
 /* flow-matching MSE (pizero.py:660-661): loss = mean((v - (x1-(1-s)x0))^2) -> fp32 loss[0];
  * dv = grad_scale[0] * 2 (v-d)/numel (bf16). grad_scale is a device fp32 scalar (NULL = 1). */
-int pz_flow_loss(const void* v, int64_t ldv, const float* x0, const float* x1, float* loss, void* dv,
-                 const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream);
-/* Euler step (pizero.py:479-481): a += dt*v ; t += dt */
-int pz_euler_step(float* action, const void* v, int64_t ldv, float* t, int64_t B, int64_t H, int64_t A,
-                  float dt, void* stream);
+int pz_flow_loss(const void* v, int64_t ldv, int64_t v_bstride, const float* x0, const float* x1, float* loss,
+                 void* dv, const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream);
+/* Euler step (pizero.py:479-481): a += dt*v ; t += dt.  v row (b,h) at v + b*v_bstride + h*ldv */
+int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t v_bstride, float* t, int64_t B, int64_t H,
+                  int64_t A, float dt, void* stream);
 int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream);
 
 /* elementwise backward of fused MLP epilogues (recompute activations, no extra saves) */
@@ -189,6 +189,10 @@ int pz_clip_coef(const float* acc, float* coef, float* norm_out, float max_norm,
 /* deterministic counter-based fill (oracle/synth.py twin): x[i] = off + scale*u(seed, i) */
 int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float off, float scale,
                     void* stream);
+/* strided row copy with scale: dst[b*dbs + r*dld + d] = scale*src[b*sbs + r*sld + d] (+ dst if beta)
+ * (the sqrt(hidden) embedding scaling of joint_model.py:348-355 for proprio/action rows) */
+int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t dld, int64_t dbs, int64_t B,
+                 int64_t rows, int64_t D, float scale, int32_t beta, void* stream);
 /* bf16 <-> fp32 copies / scaled adds */
 int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);

@@ -111,32 +111,46 @@ __global__ void flow_psi_kernel(const float* x0, const float* x1, const float* t
   psi[idx] = f2bf((1.f - (1.f - sig) * tt) * x0[idx] + tt * x1[idx]);
 }
 
-__global__ void flow_loss_kernel(const bf16_t* __restrict__ v, int64_t ldv, const float* __restrict__ x0,
-                                 const float* __restrict__ x1, float* loss, bf16_t* dv,
-                                 const float* __restrict__ gscale, int64_t rows, int64_t A, float sig) {
+__global__ void flow_loss_kernel(const bf16_t* __restrict__ v, int64_t ldv, int64_t vbs,
+                                 const float* __restrict__ x0, const float* __restrict__ x1, float* loss,
+                                 bf16_t* dv, const float* __restrict__ gscale, int64_t H, int64_t rows, int64_t A,
+                                 float sig) {
   __shared__ float red[4];
   const int64_t n = rows * A;
   float s = 0.f;
   const float g = gscale ? gscale[0] : 1.f;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) {
     const int64_t r = i / A, c = i % A;
+    const int64_t vo = (r / H) * vbs + (r % H) * ldv + c;
     const float d = x1[i] - (1.f - sig) * x0[i];
-    const float e = bf2f(v[r * ldv + c]) - d;
+    const float e = bf2f(v[vo]) - d;
     s += e * e;
-    if (dv) dv[r * A + c] = f2bf(g * 2.f * e / (float)n);
+    if (dv) dv[vo] = f2bf(g * 2.f * e / (float)n);
   }
   s = block_sum<4>(s, red);
   if (threadIdx.x == 0) loss[0] = s / (float)n;
 }
 
-__global__ void euler_kernel(float* action, const bf16_t* __restrict__ v, int64_t ldv, float* t, int64_t B,
-                             int64_t H, int64_t A, float dt) {
+__global__ void euler_kernel(float* action, const bf16_t* __restrict__ v, int64_t ldv, int64_t vbs, float* t,
+                             int64_t B, int64_t H, int64_t A, float dt) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx < B * H * A) {
     const int64_t r = idx / A, c = idx % A;
-    action[idx] += dt * bf2f(v[r * ldv + c]);
+    action[idx] += dt * bf2f(v[(r / H) * vbs + (r % H) * ldv + c]);
   }
   if (t && idx < B) t[idx] += dt;
+}
+
+__global__ void copy_rows_kernel(const bf16_t* __restrict__ src, int64_t sld, int64_t sbs, bf16_t* dst, int64_t dld,
+                                 int64_t dbs, int64_t rows, int64_t D, float scale, int beta) {
+  const int64_t b = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < rows * D; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / D, d = i % D;
+    float v = scale * bf2f(src[b * sbs + r * sld + d]);
+    bf16_t* o = dst + b * dbs + r * dld + d;
+    if (beta) v += bf2f(*o);
+    *o = f2bf(v);
+  }
 }
 
 __global__ void clamp_kernel(float* x, int64_t n, float lo, float hi) {
@@ -319,20 +333,33 @@ extern "C" int pz_flow_psi(const float* x0, const float* x1, const float* t, voi
   return PZ_OK;
 }
 
-extern "C" int pz_flow_loss(const void* v, int64_t ldv, const float* x0, const float* x1, float* loss, void* dv,
-                            const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream) {
-  PZ_CHECK_ARG(v && x0 && x1 && loss && B > 0, "flow_loss: bad args");
-  hipLaunchKernelGGL(flow_loss_kernel, dim3(1), dim3(256), 0, ST, (const bf16_t*)v, ldv, x0, x1, loss,
-                     (bf16_t*)dv, grad_scale, B * H, A, sig_min);
+extern "C" int pz_flow_loss(const void* v, int64_t ldv, int64_t v_bstride, const float* x0, const float* x1,
+                            float* loss, void* dv, const float* grad_scale, int64_t B, int64_t H, int64_t A,
+                            float sig_min, void* stream) {
+  PZ_CHECK_ARG(v && x0 && x1 && loss && B > 0 && H > 0 && A > 0, "flow_loss: bad args");
+  hipLaunchKernelGGL(flow_loss_kernel, dim3(1), dim3(256), 0, ST, (const bf16_t*)v, ldv, v_bstride, x0, x1, loss,
+                     (bf16_t*)dv, grad_scale, H, B * H, A, sig_min);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
 
-extern "C" int pz_euler_step(float* action, const void* v, int64_t ldv, float* t, int64_t B, int64_t H, int64_t A,
-                             float dt, void* stream) {
+extern "C" int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t v_bstride, float* t, int64_t B,
+                             int64_t H, int64_t A, float dt, void* stream) {
   PZ_CHECK_ARG(action && v && B > 0, "euler_step: bad args");
   const int64_t n = B * H * A > B ? B * H * A : B;
-  hipLaunchKernelGGL(euler_kernel, dim3(nblk(n)), dim3(256), 0, ST, action, (const bf16_t*)v, ldv, t, B, H, A, dt);
+  hipLaunchKernelGGL(euler_kernel, dim3(nblk(n)), dim3(256), 0, ST, action, (const bf16_t*)v, ldv, v_bstride, t, B,
+                     H, A, dt);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t dld, int64_t dbs, int64_t B,
+                            int64_t rows, int64_t D, float scale, int32_t beta, void* stream) {
+  PZ_CHECK_ARG(src && dst && B > 0 && rows > 0 && D > 0, "copy_rows: bad args");
+  const int64_t n = rows * D;
+  const unsigned gx = (unsigned)(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024);
+  hipLaunchKernelGGL(copy_rows_kernel, dim3(gx, (unsigned)B), dim3(256), 0, ST, (const bf16_t*)src, sld, sbs,
+                     (bf16_t*)dst, dld, dbs, rows, D, scale, (int)beta);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -76,8 +76,9 @@ SIGNATURES = {
     "pz_concat_time": [vp, vp, vp, i64, i64, i64, vp],
     "pz_split_time_grad": [vp, vp, i64, i64, vp],
     "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
-    "pz_flow_loss": [vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
-    "pz_euler_step": [vp, vp, i64, vp, i64, i64, i64, f32, vp],
+    "pz_flow_loss": [vp, i64, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
+    "pz_euler_step": [vp, vp, i64, i64, vp, i64, i64, i64, f32, vp],
+    "pz_copy_rows": [vp, i64, i64, vp, i64, i64, i64, i64, i64, f32, i32, vp],
     "pz_clamp": [vp, i64, f32, f32, vp],
     "pz_geglu_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, vp],
     "pz_act_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, vp],

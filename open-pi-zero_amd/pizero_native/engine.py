@@ -1,0 +1,824 @@
+"""Native layer executor for the Pi0 hot path (SigLIP + joint model, fwd/bwd/infer).
+
+The executor walks the model with HIP kernels from libpizero_hip.so only; it
+never calls torch math on the hot path (torch provides device memory and the
+current stream).  Layout decisions (MI355X-first):
+
+* residual streams are bf16 row-major ``[tokens, hidden]`` per weight group:
+  the VLM group (image+text prefix, Gemma weights) and the action-expert group
+  (proprio + action rows, shared weights after ``tie_action_proprio_weights``);
+  every Linear is one MFMA GEMM on that stream (q|k|v and gate|up fused);
+* the joint attention of the mixture-of-transformers (joint_model.py:130-304)
+  gathers all groups' post-RoPE Q/K/V into joint token buffers
+  ``Q[B, L, nh*hd]``, ``K/V[B, Lp, hd]`` (MQA: one KV head, so the 8 query
+  heads are stacked as rows and no ``repeat_kv`` copy exists), then runs
+  S = Q K^T and O = P V as per-sample batched MFMA GEMMs around a softmax
+  kernel that applies the Gemma soft-cap and generates the block-causal mask
+  arithmetically from per-sample prefix counts;
+* backward reuses the same GEMM kernel in its k-strided layouts (dgrad /
+  wgrad / attention products), writes parameter gradients straight into the
+  flat gradient arena, and reports each finished layer to an optional hook
+  (used by the data-parallel wrapper to start RCCL all-reduces of finished
+  gradient buckets while the backward continues).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+
+from . import ops
+from .ops import PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_SILU
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _cfg(cfg, key, default=None):
+    from src.utils.config import cfg_get
+
+    return cfg_get(cfg, key, default)
+
+
+@dataclass
+class Dims:
+    P: int
+    C: int
+    H: int
+    A: int
+    Pd: int
+    vocab: int
+    image_token: int
+    pad_token: int
+    img: int
+    ps: int
+    n_img: int
+    vH: int
+    vI: int
+    vL: int
+    vheads: int
+    ln_eps: float
+    proj: int
+    nL: int
+    nh: int
+    nkv: int
+    hd: int
+    rms_eps: float
+    gH: int
+    gI: int
+    g_theta: float
+    aH: int
+    aI: int
+    a_theta: float
+    p_theta: float
+    tmax: float
+    sig_min: float
+    steps: int
+    clip: float | None
+
+    @staticmethod
+    def from_cfg(cfg):
+        v = _cfg(cfg, "vision.config")
+        j = _cfg(cfg, "joint.config")
+        mix = _cfg(cfg, "mixture") or _cfg(j, "mixture")
+        img = int(_cfg(v, "image_size"))
+        ps = int(_cfg(v, "patch_size"))
+        clip = _cfg(cfg, "final_action_clip_value", None)
+        return Dims(
+            P=int(_cfg(cfg, "max_image_text_tokens", _cfg(cfg, "max_seq_len"))), C=int(_cfg(cfg, "cond_steps")),
+            H=int(_cfg(cfg, "horizon_steps")), A=int(_cfg(cfg, "action_dim")), Pd=int(_cfg(cfg, "proprio_dim")),
+            vocab=int(_cfg(cfg, "vocab_size")), image_token=int(_cfg(cfg, "image_token_index")),
+            pad_token=int(_cfg(cfg, "pad_token_id")), img=img, ps=ps, n_img=(img // ps) ** 2,
+            vH=int(_cfg(v, "hidden_size")), vI=int(_cfg(v, "intermediate_size")),
+            vL=int(_cfg(v, "num_hidden_layers")), vheads=int(_cfg(v, "num_attention_heads")),
+            ln_eps=float(_cfg(v, "layer_norm_eps", 1e-6)),
+            proj=int(_cfg(cfg, "vision_projector.config.vision_config.projection_dim")),
+            nL=int(_cfg(j, "num_hidden_layers")), nh=int(_cfg(j, "num_attention_heads")),
+            nkv=int(_cfg(j, "num_key_value_heads")), hd=int(_cfg(j, "head_dim")),
+            rms_eps=float(_cfg(j, "rms_norm_eps", 1e-6)),
+            gH=int(_cfg(mix, "vlm.hidden_size")), gI=int(_cfg(mix, "vlm.intermediate_size")),
+            g_theta=float(_cfg(mix, "vlm.rope_theta", 10000.0)),
+            aH=int(_cfg(mix, "action.hidden_size")), aI=int(_cfg(mix, "action.intermediate_size")),
+            a_theta=float(_cfg(mix, "action.rope_theta", 10000.0)),
+            p_theta=float(_cfg(mix, "proprio.rope_theta", _cfg(mix, "action.rope_theta", 10000.0))),
+            tmax=float(_cfg(cfg, "time_max_period", 10000.0)), sig_min=float(_cfg(cfg, "flow_sig_min", 0.001)),
+            steps=int(_cfg(cfg, "num_inference_steps")), clip=None if clip is None else float(clip),
+        )
+
+    @property
+    def L(self):
+        return self.P + self.C + self.H
+
+    @property
+    def Lp(self):
+        return (self.L + 7) // 8 * 8
+
+    @property
+    def kcols(self):
+        return (3 * self.ps * self.ps + 31) // 32 * 32
+
+
+class Group:
+    """Rows of the joint sequence that share one set of mixture weights."""
+
+    def __init__(self, name, prefix, mixtures, T, joint_off, hidden, inter, theta, skip_last, pos_key):
+        self.name, self.prefix, self.mixtures = name, prefix, mixtures
+        self.T, self.off, self.hid, self.inter, self.theta = T, joint_off, hidden, inter, theta
+        self.skip_last = skip_last
+        self.pos_key = pos_key
+
+
+class Engine:
+    def __init__(self, model):
+        self.m = model
+        self.d = Dims.from_cfg(model.cfg)
+        self._tables = {}
+        self._ws = {}
+        if self.d.nkv != 1:
+            raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
+
+    # ------------------------------------------------------------- weights --
+    @property
+    def ar(self):
+        return self.m._arena
+
+    def w(self, name):
+        return self.ar.view(name)
+
+    def gw(self, name):
+        return self.ar.grad_view(name)
+
+    def rg(self, name):
+        return self.m._requires_grad(name)
+
+    def qkv_w(self, p):
+        return self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight")
+
+    def gu_w(self, p):
+        return self.ar.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight")
+
+    def rope(self, theta):
+        dev = self.ar.data.device
+        key = (float(theta), dev)
+        if key not in self._tables:
+            maxpos = self.d.L + 8
+            cs = torch.empty((maxpos + 1) * self.d.hd, device=dev, dtype=F32)
+            ops.rope_table(cs, maxpos, self.d.hd, theta)
+            self._tables[key] = cs
+        return self._tables[key]
+
+    def colsum_ws(self, n):
+        dev = self.ar.data.device
+        t = self._ws.get(("colsum", dev))
+        if t is None or t.numel() < 64 * n:
+            t = torch.empty(64 * max(n, 4608), device=dev, dtype=F32)
+            self._ws[("colsum", dev)] = t
+        return t
+
+    def groups(self, tied, active=("vlm", "proprio", "action")):
+        d = self.d
+        out = []
+        mp = "joint_model.mixtures."
+        if "vlm" in active:
+            out.append(Group("vlm", mp + "vlm.layers.", ["vlm"], d.P, 0, d.gH, d.gI, d.g_theta, True, "vlm"))
+        if tied:
+            mix = [m for m in ("proprio", "action") if m in active]
+            T = (d.C if "proprio" in mix else 0) + (d.H if "action" in mix else 0)
+            if T:
+                off = d.P if "proprio" in mix else d.P + d.C
+                out.append(Group("expert", mp + "action.layers.", mix, T, off, d.aH, d.aI, d.a_theta,
+                                 mix == ["proprio"], "expert"))
+        else:
+            if "proprio" in active:
+                out.append(Group("proprio", mp + "proprio.layers.", ["proprio"], d.C, d.P, d.aH, d.aI, d.p_theta,
+                                 True, "proprio"))
+            if "action" in active:
+                out.append(Group("action", mp + "action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI,
+                                 d.a_theta, False, "action"))
+        return out
+
+    # ================================================================ SigLIP ==
+    def siglip_forward(self, pix, save):
+        """siglip.py:34-300 + projector (siglip.py:9-31). pix bf16 [B,3,H,W] -> img [B*n_img, proj]."""
+        d = self.d
+        B = pix.shape[0]
+        M = B * d.n_img
+        dev = pix.device
+        vt = "vision_tower.vision_model."
+        kc = d.kcols
+        cols = torch.empty(M, kc, device=dev, dtype=BF16)
+        ops.patchify(pix, cols, d.ps)
+        wpad = torch.zeros(d.vH, kc, device=dev, dtype=BF16)
+        wpatch = self.w(vt + "embeddings.patch_embedding.weight").view(d.vH, -1)
+        ops.copy_rows(wpatch, wpatch.shape[1], 0, wpad, kc, 0, 1, d.vH, wpatch.shape[1])
+        x = torch.empty(M, d.vH, device=dev, dtype=BF16)
+        ops.gemm(d.n_img, d.vH, kc, cols, kc, True, wpad, kc, True, x, d.vH, batch=B, sA=(d.n_img * kc, 0),
+                 sC=(d.n_img * d.vH, 0), bias=self.w(vt + "embeddings.patch_embedding.bias"),
+                 resid=self.w(vt + "embeddings.position_embedding.weight"), ld_resid=d.vH, sR=(0, 0))
+        if save is not None:
+            save["cols"] = cols
+        nh, hd = d.vheads, d.vH // d.vheads
+        Np = d.n_img
+        S = torch.empty(B * nh, Np, Np, device=dev, dtype=F32)
+        layers = []
+        for i in range(d.vL):
+            p = f"{vt}encoder.layers.{i}."
+            st = {"x": x}
+            h1 = torch.empty_like(x)
+            mu1 = torch.empty(M, device=dev, dtype=F32)
+            r1 = torch.empty(M, device=dev, dtype=F32)
+            ops.layernorm(x, self.w(p + "layer_norm1.weight"), self.w(p + "layer_norm1.bias"), h1, mu1, r1, d.ln_eps)
+            qkv = torch.empty(M, 3 * d.vH, device=dev, dtype=BF16)
+            ops.linear(h1, self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"), qkv,
+                       bias=self.ar.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias"))
+            W3 = 3 * d.vH
+            # S[b,h] = Q_bh K_bh^T  (heads as the inner batch)
+            ops.gemm(Np, Np, hd, qkv, W3, True, qkv[:, d.vH:], W3, True, S, Np, batch=B * nh, batch_inner=nh,
+                     sA=(Np * W3, hd), sB=(Np * W3, hd), sC=(nh * Np * Np, Np * Np))
+            Pm = torch.empty(B * nh, Np, Np, device=dev, dtype=BF16)
+            ops.attn_softmax(S, Np, Pm, Np, B * nh * Np, Np, hd ** -0.5)
+            O = torch.empty(M, d.vH, device=dev, dtype=BF16)
+            ops.gemm(Np, hd, Np, Pm, Np, True, qkv[:, 2 * d.vH:], W3, False, O, d.vH, batch=B * nh, batch_inner=nh,
+                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * d.vH, hd))
+            xm = torch.empty_like(x)
+            ops.linear(O, self.w(p + "self_attn.out_proj.weight"), xm, bias=self.w(p + "self_attn.out_proj.bias"),
+                       resid=x)
+            h2 = torch.empty_like(x)
+            mu2 = torch.empty(M, device=dev, dtype=F32)
+            r2 = torch.empty(M, device=dev, dtype=F32)
+            ops.layernorm(xm, self.w(p + "layer_norm2.weight"), self.w(p + "layer_norm2.bias"), h2, mu2, r2, d.ln_eps)
+            a1 = torch.empty(M, d.vI, device=dev, dtype=BF16) if save is not None else None
+            g1 = torch.empty(M, d.vI, device=dev, dtype=BF16)
+            ops.linear(h2, self.w(p + "mlp.fc1.weight"), g1, bias=self.w(p + "mlp.fc1.bias"), epi=PZ_EPI_GELU, aux=a1)
+            xn = torch.empty_like(x)
+            ops.linear(g1, self.w(p + "mlp.fc2.weight"), xn, bias=self.w(p + "mlp.fc2.bias"), resid=xm)
+            if save is not None:
+                st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, P=Pm, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1)
+                layers.append(st)
+            x = xn
+        y = torch.empty_like(x)
+        mu = torch.empty(M, device=dev, dtype=F32)
+        r = torch.empty(M, device=dev, dtype=F32)
+        ops.layernorm(x, self.w(vt + "post_layernorm.weight"), self.w(vt + "post_layernorm.bias"), y, mu, r, d.ln_eps)
+        img = torch.empty(M, d.proj, device=dev, dtype=BF16)
+        ops.linear(y, self.w("multi_modal_projector.linear.weight"), img, bias=self.w("multi_modal_projector.linear.bias"))
+        if save is not None:
+            save.update(layers=layers, x_last=x, y=y, mu=mu, r=r, B=B)
+        return img
+
+    def siglip_backward(self, sv, dimg, beta):
+        d = self.d
+        B = sv["B"]
+        M = B * d.n_img
+        dev = dimg.device
+        vt = "vision_tower.vision_model."
+        rpp = ops.rows_per_part()
+        P = (M + rpp - 1) // rpp
+        ws = self.colsum_ws(max(d.vI, 3 * d.vH))
+        pw = torch.empty(P, d.vH, device=dev, dtype=F32)
+        pb = torch.empty(P, d.vH, device=dev, dtype=F32)
+        # projector
+        nm = "multi_modal_projector.linear."
+        if self.rg(nm + "weight"):
+            ops.linear_wgrad(dimg, sv["y"], self.gw(nm + "weight"), beta=beta)
+        if self.rg(nm + "bias"):
+            ops.colsum(dimg, self.gw(nm + "bias"), ws, beta=beta)
+        dy = torch.empty(M, d.vH, device=dev, dtype=BF16)
+        ops.linear_dgrad(dimg, self.w(nm + "weight"), dy)
+        dx = torch.empty_like(dy)
+        ops.layernorm_bwd(dy, sv["x_last"], self.w(vt + "post_layernorm.weight"), sv["mu"], sv["r"], dx,
+                          dw_part=pw, db_part=pb)
+        self._norm_grads(vt + "post_layernorm.", pw, pb, beta)
+        nh, hd = d.vheads, d.vH // d.vheads
+        Np = d.n_img
+        W3 = 3 * d.vH
+        dg = torch.empty(M, d.vI, device=dev, dtype=BF16)
+        g1 = torch.empty(M, d.vI, device=dev, dtype=BF16)
+        dP = torch.empty(B * nh, Np, Np, device=dev, dtype=F32)
+        dS = torch.empty(B * nh, Np, Np, device=dev, dtype=BF16)
+        dqkv = torch.empty(M, W3, device=dev, dtype=BF16)
+        dh = torch.empty(M, d.vH, device=dev, dtype=BF16)
+        dxm = torch.empty(M, d.vH, device=dev, dtype=BF16)
+        dO = torch.empty(M, d.vH, device=dev, dtype=BF16)
+        for i in reversed(range(d.vL)):
+            p = f"{vt}encoder.layers.{i}."
+            st = sv["layers"][i]
+            # MLP: x' = xm + fc2(gelu(fc1(ln2(xm))))
+            ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg)
+            ops.act_bwd(dg, st["a1"], dg, g1, PZ_EPI_GELU)
+            if self.rg(p + "mlp.fc2.weight"):
+                ops.linear_wgrad(dx, g1, self.gw(p + "mlp.fc2.weight"), beta=beta)
+            if self.rg(p + "mlp.fc2.bias"):
+                ops.colsum(dx, self.gw(p + "mlp.fc2.bias"), ws, beta=beta)
+            if self.rg(p + "mlp.fc1.weight"):
+                ops.linear_wgrad(dg, st["h2"], self.gw(p + "mlp.fc1.weight"), beta=beta)
+            if self.rg(p + "mlp.fc1.bias"):
+                ops.colsum(dg, self.gw(p + "mlp.fc1.bias"), ws, beta=beta)
+            ops.linear_dgrad(dg, self.w(p + "mlp.fc1.weight"), dh)
+            ops.layernorm_bwd(dh, st["xm"], self.w(p + "layer_norm2.weight"), st["mu2"], st["r2"], dxm, dres=dx,
+                              dw_part=pw, db_part=pb)
+            self._norm_grads(p + "layer_norm2.", pw, pb, beta)
+            # attention out-proj
+            if self.rg(p + "self_attn.out_proj.weight"):
+                ops.linear_wgrad(dxm, st["O"], self.gw(p + "self_attn.out_proj.weight"), beta=beta)
+            if self.rg(p + "self_attn.out_proj.bias"):
+                ops.colsum(dxm, self.gw(p + "self_attn.out_proj.bias"), ws, beta=beta)
+            ops.linear_dgrad(dxm, self.w(p + "self_attn.out_proj.weight"), dO)
+            qkv, Pm = st["qkv"], st["P"]
+            # dP = dO V^T ; dS ; dQ = dS K ; dK = dS^T Q ; dV = P^T dO
+            ops.gemm(Np, Np, hd, dO, d.vH, True, qkv[:, 2 * d.vH:], W3, True, dP, Np, batch=B * nh, batch_inner=nh,
+                     sA=(Np * d.vH, hd), sB=(Np * W3, hd), sC=(nh * Np * Np, Np * Np))
+            ops.attn_softmax_bwd(Pm, dP, Np, None, dS, Np, B * nh * Np, Np, hd ** -0.5, 0.0)
+            ops.gemm(Np, hd, Np, dS, Np, True, qkv[:, d.vH:], W3, False, dqkv, W3, batch=B * nh, batch_inner=nh,
+                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * W3, hd))
+            ops.gemm(Np, hd, Np, dS, Np, False, qkv, W3, False, dqkv[:, d.vH:], W3, batch=B * nh, batch_inner=nh,
+                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * W3, hd))
+            ops.gemm(Np, hd, Np, Pm, Np, False, dO, d.vH, False, dqkv[:, 2 * d.vH:], W3, batch=B * nh,
+                     batch_inner=nh, sA=(nh * Np * Np, Np * Np), sB=(Np * d.vH, hd), sC=(Np * W3, hd))
+            qn, vn = p + "self_attn.q_proj.", p + "self_attn.v_proj."
+            if all(self.rg(p + f"self_attn.{k}_proj.weight") for k in "qkv"):
+                ops.linear_wgrad(dqkv, st["h1"], self.ar.grad_span(qn + "weight", vn + "weight"), beta=beta)
+            else:
+                for k, c0 in (("q", 0), ("k", d.vH), ("v", 2 * d.vH)):
+                    if self.rg(p + f"self_attn.{k}_proj.weight"):
+                        ops.linear_wgrad(dqkv[:, c0:c0 + d.vH], st["h1"], self.gw(p + f"self_attn.{k}_proj.weight"),
+                                         beta=beta)
+            if all(self.rg(p + f"self_attn.{k}_proj.bias") for k in "qkv"):
+                ops.colsum(dqkv, self.ar.grad_span(qn + "bias", vn + "bias"), ws, beta=beta)
+            ops.linear_dgrad(dqkv, self.qkv_siglip(p), dh)
+            dxn = torch.empty_like(dx)
+            ops.layernorm_bwd(dh, st["x"], self.w(p + "layer_norm1.weight"), st["mu1"], st["r1"], dxn, dres=dxm,
+                              dw_part=pw, db_part=pb)
+            self._norm_grads(p + "layer_norm1.", pw, pb, beta)
+            dx = dxn
+            self._notify("vision", i)
+        # patch embedding + position embedding
+        pe = vt + "embeddings."
+        if self.rg(pe + "position_embedding.weight"):
+            ops.batch_sum(dx, B, d.n_img * d.vH, d.n_img * d.vH, self.gw(pe + "position_embedding.weight"), beta=beta)
+        if self.rg(pe + "patch_embedding.bias"):
+            ops.colsum(dx, self.gw(pe + "patch_embedding.bias"), ws, beta=beta)
+        if self.rg(pe + "patch_embedding.weight"):
+            kc = d.kcols
+            tmp = torch.empty(d.vH, kc, device=dev, dtype=BF16)
+            ops.linear_wgrad(dx, sv["cols"], tmp)
+            g = self.gw(pe + "patch_embedding.weight").view(d.vH, -1)
+            ops.copy_rows(tmp, kc, 0, g, g.shape[1], 0, 1, d.vH, g.shape[1], beta=beta)
+        self._notify("vision", -1)
+
+    def qkv_siglip(self, p):
+        return self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight")
+
+    def _norm_grads(self, prefix, pw, pb, beta):
+        if pw is not None and self.rg(prefix + "weight"):
+            ops.reduce_parts(pw, self.gw(prefix + "weight"), beta=beta)
+        if pb is not None and self.rg(prefix + "bias"):
+            ops.reduce_parts(pb, self.gw(prefix + "bias"), beta=beta)
+
+    # ============================================================ embeddings ==
+    def embed_prefix(self, ids, img):
+        d = self.d
+        B = ids.shape[0]
+        X = torch.empty(B * d.P, d.gH, device=ids.device, dtype=BF16)
+        # pizero.py:395 (/sqrt(hidden)) and joint_model.py:355 (*sqrt(hidden)) cancel for image rows
+        ops.embed_merge(ids, self.w("embed_tokens.weight"), img, X, d.n_img, d.image_token, d.pad_token,
+                        math.sqrt(d.gH), 1.0)
+        return X
+
+    def action_embed(self, psi_bf, t, save):
+        """ActionEncoder (vla/modules.py:39-53) with time embedding (vla/modules.py:15-22)."""
+        d = self.d
+        rows = psi_bf.shape[0]
+        B = t.shape[0]
+        dev = psi_bf.device
+        e1 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+        ops.small_linear(psi_bf, self.w("action_encoder.linear_1.weight"), e1, bias=self.w("action_encoder.linear_1.bias"))
+        temb = torch.empty(B, d.aH, device=dev, dtype=BF16)
+        ops.time_embed(t, temb, d.tmax)
+        cat = torch.empty(rows, 2 * d.aH, device=dev, dtype=BF16)
+        ops.concat_time(temb, e1, cat, B, rows // B, d.aH)
+        pre = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+        e2 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+        ops.linear(cat, self.w("action_encoder.linear_2.weight"), e2, bias=self.w("action_encoder.linear_2.bias"),
+                   epi=PZ_EPI_SILU, aux=pre)
+        e3 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+        ops.linear(e2, self.w("action_encoder.linear_3.weight"), e3, bias=self.w("action_encoder.linear_3.bias"))
+        if save is not None:
+            save.update(ae_psi=psi_bf, ae_cat=cat, ae_pre=pre, ae_e2=e2)
+        return e3
+
+    # ======================================================== joint layers ==
+    def _joint_layers_train(self, groups, X, pos, cnt, B, save):
+        """joint_model.py:24-304 x nL for the training pass (all mixtures active)."""
+        d = self.d
+        dev = X[groups[0].name].device
+        L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
+        S = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+        layers = []
+        for l in range(d.nL):
+            last = l == d.nL - 1
+            Qj = torch.empty(B, L, nh * hd, device=dev, dtype=BF16)
+            Kj = torch.zeros(B, Lp, hd, device=dev, dtype=BF16)
+            Vj = torch.zeros(B, Lp, hd, device=dev, dtype=BF16)
+            st = {"Q": Qj, "K": Kj, "V": Vj, "g": {}}
+            for g in groups:
+                p = f"{g.prefix}{l}."
+                x = X[g.name]
+                M = x.shape[0]
+                h = torch.empty_like(x)
+                r = torch.empty(M, device=dev, dtype=F32)
+                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, r, d.rms_eps)
+                W = (nh + 2) * hd
+                qkv = torch.empty(M, W, device=dev, dtype=BF16)
+                ops.linear(h, self.qkv_w(p), qkv)
+                ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L, g.off,
+                                   Lp, g.off)
+                st["g"][g.name] = {"x": x, "h": h, "r": r}
+            ops.gemm(L * nh, L, hd, Qj, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L * nh * hd, 0),
+                     sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
+            Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+            tc = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+            ops.attn_softmax(S, Lp, Pm, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), cap=50.0, tcap=tc, mask_mode=1,
+                             rows_per_batch=L * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
+            st["P"], st["tc"] = Pm, tc
+            for g in groups:
+                gs = st["g"][g.name]
+                p = f"{g.prefix}{l}."
+                x = X[g.name]
+                M = x.shape[0]
+                if last and g.skip_last:
+                    X[g.name] = None
+                    gs["skip"] = True
+                    continue
+                O = torch.empty(M, nh * hd, device=dev, dtype=BF16)
+                ops.gemm(g.T * nh, hd, Lp, Pm[:, g.off * nh:], Lp, True, Vj, hd, False, O, hd, batch=B,
+                         sA=(L * nh * Lp, 0), sB=(Lp * hd, 0), sC=(g.T * nh * hd, 0))
+                xm = torch.empty_like(x)
+                ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
+                h2 = torch.empty_like(x)
+                r2 = torch.empty(M, device=dev, dtype=F32)
+                ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, r2, d.rms_eps)
+                gu = torch.empty(M, 2 * g.inter, device=dev, dtype=BF16)
+                hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+                ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU, aux=gu)
+                xn = torch.empty_like(x)
+                ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
+                gs.update(O=O, xm=xm, h2=h2, r2=r2, gu=gu, skip=False)
+                X[g.name] = xn
+            layers.append(st)
+        save["joint"] = layers
+        return X
+
+    def _joint_layers_backward(self, groups, dX, pos, cnt, B, sv, beta):
+        d = self.d
+        L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
+        dev = next(v for v in dX.values() if v is not None).device
+        dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+        dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+        rpp = ops.rows_per_part()
+        for l in reversed(range(d.nL)):
+            st = sv["joint"][l]
+            dQ = torch.empty(B, L, nh * hd, device=dev, dtype=BF16)
+            dK = torch.empty(B, Lp, hd, device=dev, dtype=BF16)
+            dV = torch.empty(B, Lp, hd, device=dev, dtype=BF16)
+            dO = {}
+            dXm = {}
+            any_skip = False
+            for g in groups:
+                gs = st["g"][g.name]
+                p = f"{g.prefix}{l}."
+                if gs.get("skip"):
+                    any_skip = True
+                    continue
+                dx = dX[g.name]
+                M = dx.shape[0]
+                part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
+                # MLP
+                dhm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+                ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dhm)
+                hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+                gu = gs["gu"]
+                ops.geglu_bwd(dhm, gu, gu, hm, M, g.inter)  # gu <- d(gate|up), hm <- recomputed
+                if self.rg(p + "mlp.down_proj.weight"):
+                    ops.linear_wgrad(dx, hm, self.gw(p + "mlp.down_proj.weight"), beta=beta)
+                del hm, dhm
+                if self.rg(p + "mlp.gate_proj.weight") and self.rg(p + "mlp.up_proj.weight"):
+                    ops.linear_wgrad(gu, gs["h2"], self.ar.grad_span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"),
+                                     beta=beta)
+                dh2 = torch.empty(M, g.hid, device=dev, dtype=BF16)
+                ops.linear_dgrad(gu, self.gu_w(p), dh2)
+                dxm = torch.empty_like(dx)
+                ops.rmsnorm_bwd(dh2, gs["xm"], self.w(p + "post_attention_layernorm.weight"), gs["r2"], dxm, dres=dx,
+                                dw_part=part)
+                self._norm_grads(p + "post_attention_layernorm.", part, None, beta)
+                # o_proj
+                if self.rg(p + "self_attn.o_proj.weight"):
+                    ops.linear_wgrad(dxm, gs["O"], self.gw(p + "self_attn.o_proj.weight"), beta=beta)
+                o = torch.empty(M, nh * hd, device=dev, dtype=BF16)
+                ops.linear_dgrad(dxm, self.w(p + "self_attn.o_proj.weight"), o)
+                dO[g.name] = o
+                dXm[g.name] = dxm
+            Pm, tc, Qj, Kj, Vj = st["P"], st["tc"], st["Q"], st["K"], st["V"]
+            if any_skip:
+                dP.zero_()
+            for g in groups:
+                if g.name not in dO:
+                    continue
+                ops.gemm(g.T * nh, L, hd, dO[g.name], hd, True, Vj, hd, True, dP[:, g.off * nh:], Lp, batch=B,
+                         sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
+            ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
+            # dQ = dS K ; dK = dS^T Q ; dV = sum_g P_g^T dO_g
+            ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
+                     sB=(Lp * hd, 0), sC=(L * nh * hd, 0))
+            ops.gemm(Lp, hd, L * nh, dS, Lp, False, Qj, hd, False, dK, hd, batch=B, sA=(L * nh * Lp, 0),
+                     sB=(L * nh * hd, 0), sC=(Lp * hd, 0))
+            first = True
+            for g in groups:
+                if g.name not in dO:
+                    continue
+                ops.gemm(Lp, hd, g.T * nh, Pm[:, g.off * nh:], Lp, False, dO[g.name], hd, False, dV, hd, batch=B,
+                         sA=(L * nh * Lp, 0), sB=(g.T * nh * hd, 0), sC=(Lp * hd, 0), beta=not first)
+                first = False
+            if first:
+                dV.zero_()
+            for g in groups:
+                gs = st["g"][g.name]
+                p = f"{g.prefix}{l}."
+                x = gs["x"]
+                M = x.shape[0]
+                W = (nh + 2) * hd
+                dqkv = torch.empty(M, W, device=dev, dtype=BF16)
+                ops.qkv_rope_split_bwd(None if gs.get("skip") else dQ, dK, dV, pos[g.pos_key], self.rope(g.theta), dqkv,
+                                       B, g.T, nh, 1, hd, L, g.off, Lp, g.off)
+                names = [p + f"self_attn.{k}_proj.weight" for k in "qkv"]
+                rgs = [self.rg(n) for n in names]
+                if all(rgs):
+                    ops.linear_wgrad(dqkv, gs["h"], self.ar.grad_span(names[0], names[2]), beta=beta)
+                elif rgs[0] and rgs[1]:  # e.g. last-layer vlm v_proj frozen (pizero.py:231)
+                    ops.linear_wgrad(dqkv[:, : (nh + 1) * hd], gs["h"], self.ar.grad_span(names[0], names[1]), beta=beta)
+                else:
+                    for n, rgk, c0, c1 in zip(names, rgs, (0, nh * hd, (nh + 1) * hd), (nh * hd, (nh + 1) * hd, W)):
+                        if rgk:
+                            ops.linear_wgrad(dqkv[:, c0:c1], gs["h"], self.gw(n), beta=beta)
+                dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
+                ops.linear_dgrad(dqkv, self.qkv_w(p), dh)
+                part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
+                dxn = torch.empty(M, g.hid, device=dev, dtype=BF16)
+                ops.rmsnorm_bwd(dh, x, self.w(p + "input_layernorm.weight"), gs["r"], dxn, dres=dXm.get(g.name),
+                                dw_part=part)
+                self._norm_grads(p + "input_layernorm.", part, None, beta)
+                dX[g.name] = dxn
+            self._notify("joint", l)
+        return dX
+
+    # ============================================================ training ==
+    def train_forward(self, ids, pix, cnt, pos, proprios, actions, t, x0, save):
+        """pizero.py:607-661: returns fp32 loss [1]; ``save`` collects activations."""
+        d = self.d
+        dev = pix.device
+        B = ids.shape[0]
+        tied = self.m._tied
+        sv_v = {}
+        img = self.siglip_forward(pix, sv_v)
+        Xv = self.embed_prefix(ids, img)
+        prop = proprios.reshape(B * d.C, d.Pd).to(BF16)
+        pe = torch.empty(B * d.C, d.aH, device=dev, dtype=BF16)
+        ops.small_linear(prop, self.w("proprio_encoder.weight"), pe, bias=self.w("proprio_encoder.bias"))
+        psi = torch.empty(B * d.H, d.A, device=dev, dtype=BF16)
+        ops.flow_psi(x0, actions, t, psi, d.sig_min)
+        e3 = self.action_embed(psi, t, save)
+        sa = math.sqrt(d.aH)
+        if tied:
+            Xe = torch.empty(B * (d.C + d.H), d.aH, device=dev, dtype=BF16)
+            T = d.C + d.H
+            ops.copy_rows(pe, d.aH, d.C * d.aH, Xe, d.aH, T * d.aH, B, d.C, d.aH, scale=sa)
+            ops.copy_rows(e3, d.aH, d.H * d.aH, Xe[d.C:], d.aH, T * d.aH, B, d.H, d.aH, scale=sa)
+            X = {"vlm": Xv, "expert": Xe}
+        else:
+            Xp = torch.empty(B * d.C, d.aH, device=dev, dtype=BF16)
+            Xa = torch.empty(B * d.H, d.aH, device=dev, dtype=BF16)
+            ops.copy_rows(pe, d.aH, 0, Xp, d.aH, 0, 1, B * d.C, d.aH, scale=sa)
+            ops.copy_rows(e3, d.aH, 0, Xa, d.aH, 0, 1, B * d.H, d.aH, scale=sa)
+            X = {"vlm": Xv, "proprio": Xp, "action": Xa}
+        groups = self.groups(tied)
+        X = self._joint_layers_train(groups, X, pos, cnt, B, save)
+        ag = "expert" if tied else "action"
+        aoff = d.C if tied else 0
+        Tg = d.C + d.H if tied else d.H
+        Xl = X[ag]
+        ya = torch.empty_like(Xl)
+        ra = torch.empty(Xl.shape[0], device=dev, dtype=F32)
+        ops.rmsnorm(Xl, self.w("joint_model.mixtures.action.norm.weight"), ya, ra, d.rms_eps)
+        v = torch.zeros(B * Tg, 8, device=dev, dtype=BF16)
+        ops.small_linear(ya, self.w("action_decoder.weight"), v, bias=self.w("action_decoder.bias"))
+        loss = torch.empty(1, device=dev, dtype=F32)
+        ops.flow_loss(v[aoff:], 8, Tg * 8, x0, actions, loss, None, None, B, d.H, d.A, d.sig_min)
+        save.update(sv_v=sv_v, ids=ids, cnt=cnt, pos=pos, B=B, prop=prop, pe=pe, tied=tied, Xl=Xl, ya=ya, ra=ra,
+                    x0=x0, x1=actions, v=v, ag=ag, aoff=aoff, Tg=Tg, groups=groups)
+        return loss
+
+    def train_backward(self, sv, grad_loss, beta):
+        """Backward of train_forward; grad_loss: device fp32 [1] (d loss)."""
+        d = self.d
+        B = sv["B"]
+        dev = sv["v"].device
+        Tg, aoff = sv["Tg"], sv["aoff"]
+        ws = self.colsum_ws(2 * d.aH)
+        rpp = ops.rows_per_part()
+        # loss + decoder
+        dv = torch.zeros(B * Tg, 8, device=dev, dtype=BF16)
+        tmp = torch.empty(1, device=dev, dtype=F32)
+        ops.flow_loss(sv["v"][aoff:], 8, Tg * 8, sv["x0"], sv["x1"], tmp, dv[aoff:], grad_loss, B, d.H, d.A, d.sig_min)
+        R = B * Tg
+        if self.rg("action_decoder.weight"):
+            ops.small_gemm(d.A, d.aH, R, dv, 1, 8, sv["ya"], d.aH, 1, self.gw("action_decoder.weight"), d.aH, beta=beta)
+        if self.rg("action_decoder.bias"):
+            ops.colsum(dv[:, : d.A], self.gw("action_decoder.bias"), ws, beta=beta)
+        dya = torch.empty(R, d.aH, device=dev, dtype=BF16)
+        ops.small_gemm(R, d.aH, d.A, dv, 8, 1, self.w("action_decoder.weight"), d.aH, 1, dya, d.aH)
+        dXl = torch.empty_like(dya)
+        part = torch.empty((R + rpp - 1) // rpp, d.aH, device=dev, dtype=F32)
+        ops.rmsnorm_bwd(dya, sv["Xl"], self.w("joint_model.mixtures.action.norm.weight"), sv["ra"], dXl, dw_part=part)
+        self._norm_grads("joint_model.mixtures.action.norm.", part, None, beta)
+        groups = sv["groups"]
+        dX = {g.name: None for g in groups}
+        dX[sv["ag"]] = dXl
+        dX = self._joint_layers_backward(groups, dX, sv["pos"], sv["cnt"], B, sv, beta)
+        # expert embeddings (joint_model.py:355 scale) -> encoders
+        sa = math.sqrt(d.aH)
+        dpe = torch.empty(B * d.C, d.aH, device=dev, dtype=BF16)
+        de3 = torch.empty(B * d.H, d.aH, device=dev, dtype=BF16)
+        if sv["tied"]:
+            T = d.C + d.H
+            ops.copy_rows(dX["expert"], d.aH, T * d.aH, dpe, d.aH, d.C * d.aH, B, d.C, d.aH, scale=sa)
+            ops.copy_rows(dX["expert"][d.C:], d.aH, T * d.aH, de3, d.aH, d.H * d.aH, B, d.H, d.aH, scale=sa)
+        else:
+            ops.copy_rows(dX["proprio"], d.aH, 0, dpe, d.aH, 0, 1, B * d.C, d.aH, scale=sa)
+            ops.copy_rows(dX["action"], d.aH, 0, de3, d.aH, 0, 1, B * d.H, d.aH, scale=sa)
+        if self.rg("proprio_encoder.weight"):
+            ops.small_gemm(d.aH, d.Pd, B * d.C, dpe, 1, d.aH, sv["prop"], d.Pd, 1, self.gw("proprio_encoder.weight"),
+                           d.Pd, beta=beta)
+        if self.rg("proprio_encoder.bias"):
+            ops.colsum(dpe, self.gw("proprio_encoder.bias"), ws, beta=beta)
+        ae = "action_encoder."
+        if self.rg(ae + "linear_3.weight"):
+            ops.linear_wgrad(de3, sv["ae_e2"], self.gw(ae + "linear_3.weight"), beta=beta)
+        if self.rg(ae + "linear_3.bias"):
+            ops.colsum(de3, self.gw(ae + "linear_3.bias"), ws, beta=beta)
+        de2 = torch.empty_like(de3)
+        ops.linear_dgrad(de3, self.w(ae + "linear_3.weight"), de2)
+        ops.act_bwd(de2, sv["ae_pre"], de2, None, PZ_EPI_SILU)
+        if self.rg(ae + "linear_2.weight"):
+            ops.linear_wgrad(de2, sv["ae_cat"], self.gw(ae + "linear_2.weight"), beta=beta)
+        if self.rg(ae + "linear_2.bias"):
+            ops.colsum(de2, self.gw(ae + "linear_2.bias"), ws, beta=beta)
+        dcat = torch.empty(B * d.H, 2 * d.aH, device=dev, dtype=BF16)
+        ops.linear_dgrad(de2, self.w(ae + "linear_2.weight"), dcat)
+        de1 = torch.empty_like(de3)
+        ops.split_time_grad(dcat, de1, B * d.H, d.aH)
+        if self.rg(ae + "linear_1.weight"):
+            ops.small_gemm(d.aH, d.A, B * d.H, de1, 1, d.aH, sv["ae_psi"], d.A, 1, self.gw(ae + "linear_1.weight"), d.A,
+                           beta=beta)
+        if self.rg(ae + "linear_1.bias"):
+            ops.colsum(de1, self.gw(ae + "linear_1.bias"), ws, beta=beta)
+        self._notify("encoders", -1)
+        # VLM prefix -> projector -> SigLIP
+        if self.m._vlm_needs_grad():
+            dimg = torch.empty(B * d.n_img, d.gH, device=dev, dtype=BF16)
+            ops.embed_merge_bwd(sv["ids"], dX["vlm"], dimg, d.n_img, d.image_token, 1.0)
+            self.siglip_backward(sv["sv_v"], dimg, beta)
+
+    # ============================================================ inference ==
+    def prefill(self, ids, pix, cnt, vpos, ppos, proprios, kcache, vcache):
+        """pizero.py:430-451: SigLIP + prefix pass over {vlm, proprio}; writes post-RoPE K/V caches."""
+        d = self.d
+        dev = pix.device
+        B = ids.shape[0]
+        nh, hd, Lp = d.nh, d.hd, d.Lp
+        L1 = d.P + d.C
+        img = self.siglip_forward(pix, None)
+        Xv = self.embed_prefix(ids, img)
+        prop = proprios.reshape(B * d.C, d.Pd).to(BF16)
+        pe = torch.empty(B * d.C, d.aH, device=dev, dtype=BF16)
+        ops.small_linear(prop, self.w("proprio_encoder.weight"), pe, bias=self.w("proprio_encoder.bias"))
+        Xp = torch.empty(B * d.C, d.aH, device=dev, dtype=BF16)
+        ops.copy_rows(pe, d.aH, 0, Xp, d.aH, 0, 1, B * d.C, d.aH, scale=math.sqrt(d.aH))
+        tied = self.m._tied
+        pprefix = "joint_model.mixtures." + ("action" if tied else "proprio") + ".layers."
+        groups = [Group("vlm", "joint_model.mixtures.vlm.layers.", ["vlm"], d.P, 0, d.gH, d.gI, d.g_theta, True, "vlm"),
+                  Group("proprio", pprefix, ["proprio"], d.C, d.P, d.aH, d.aI, d.p_theta if not tied else d.a_theta,
+                        True, "proprio")]
+        X = {"vlm": Xv, "proprio": Xp}
+        pos = {"vlm": vpos, "proprio": ppos}
+        Q = torch.empty(B, L1, nh * hd, device=dev, dtype=BF16)
+        S = torch.empty(B, L1 * nh, Lp, device=dev, dtype=F32)
+        Pm = torch.empty(B, L1 * nh, Lp, device=dev, dtype=BF16)
+        for l in range(d.nL):
+            last = l == d.nL - 1
+            Kj, Vj = kcache[l], vcache[l]
+            hs = {}
+            for g in groups:
+                p = f"{g.prefix}{l}."
+                x = X[g.name]
+                M = x.shape[0]
+                h = torch.empty_like(x)
+                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
+                if last:  # only K/V are consumed downstream (pizero.py:451, skipped post-attn)
+                    kv = torch.empty(M, 2 * hd, device=dev, dtype=BF16)
+                    ops.linear(h, self.ar.span(p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"), kv)
+                    qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
+                    ops.copy_rows(kv, 2 * hd, 0, qkv[:, nh * hd:], (nh + 2) * hd, 0, 1, M, 2 * hd)
+                    ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), None, Kj, Vj, B, g.T, nh, 1, hd, L1,
+                                       g.off, Lp, g.off)
+                    continue
+                qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
+                ops.linear(h, self.qkv_w(p), qkv)
+                ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, B, g.T, nh, 1, hd, L1, g.off,
+                                   Lp, g.off)
+                hs[g.name] = h
+            if last:
+                break
+            ops.gemm(L1 * nh, L1, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L1 * nh * hd, 0),
+                     sB=(Lp * hd, 0), sC=(L1 * nh * Lp, 0))
+            ops.attn_softmax(S, Lp, Pm, Lp, B * L1 * nh, L1, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,
+                             rows_per_batch=L1 * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
+            for g in groups:
+                p = f"{g.prefix}{l}."
+                x = X[g.name]
+                X[g.name] = self._post_attn(g, p, x, Pm, Vj, B, L1, Lp)
+        return kcache, vcache
+
+    def _post_attn(self, g, p, x, Pm, Vj, B, Lq, Lp, qrow0=None):
+        d = self.d
+        nh, hd = d.nh, d.hd
+        M = x.shape[0]
+        dev = x.device
+        q0 = g.off if qrow0 is None else qrow0
+        O = torch.empty(M, nh * hd, device=dev, dtype=BF16)
+        ops.gemm(g.T * nh, hd, Lp, Pm[:, q0 * nh:], Lp, True, Vj, hd, False, O, hd, batch=B,
+                 sA=(Lq * nh * Lp, 0), sB=(Lp * hd, 0), sC=(g.T * nh * hd, 0))
+        xm = torch.empty_like(x)
+        ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
+        h2 = torch.empty_like(x)
+        ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)
+        hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+        ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
+        xn = torch.empty_like(x)
+        ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
+        return xn
+
+    def denoise_step(self, action, t, apos, cnt, kcache, vcache, B):
+        """One Euler step of pizero.py:461-481 against the cached vlm+proprio K/V."""
+        d = self.d
+        dev = action.device
+        nh, hd, Lp, L = d.nh, d.hd, d.Lp, d.L
+        psi = torch.empty(B * d.H, d.A, device=dev, dtype=BF16)
+        ops.cast_to_bf16(action, psi)
+        e3 = self.action_embed(psi, t, None)
+        x = torch.empty_like(e3)
+        ops.copy_rows(e3, d.aH, 0, x, d.aH, 0, 1, B * d.H, d.aH, scale=math.sqrt(d.aH))
+        g = Group("action", "joint_model.mixtures.action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI, d.a_theta,
+                  False, "action")
+        Q = torch.empty(B, d.H, nh * hd, device=dev, dtype=BF16)
+        S = torch.empty(B, d.H * nh, Lp, device=dev, dtype=F32)
+        Pm = torch.empty(B, d.H * nh, Lp, device=dev, dtype=BF16)
+        for l in range(d.nL):
+            p = f"{g.prefix}{l}."
+            Kj, Vj = kcache[l], vcache[l]
+            M = x.shape[0]
+            h = torch.empty_like(x)
+            ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
+            qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
+            ops.linear(h, self.qkv_w(p), qkv)
+            ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
+            ops.gemm(d.H * nh, L, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(d.H * nh * hd, 0),
+                     sB=(Lp * hd, 0), sC=(d.H * nh * Lp, 0))
+            ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,
+                             rows_per_batch=d.H * nh, heads=nh, qoff=d.P + d.C, cnt=cnt, prefix=d.P, cond=d.C)
+            x = self._post_attn(g, p, x, Pm, Vj, B, d.H, Lp, qrow0=0)
+        y = torch.empty_like(x)
+        ops.rmsnorm(x, self.w("joint_model.mixtures.action.norm.weight"), y, None, d.rms_eps)
+        v = torch.empty(B * d.H, 8, device=dev, dtype=BF16)
+        ops.small_linear(y, self.w("action_decoder.weight"), v[:, : d.A], bias=self.w("action_decoder.bias"))
+        ops.euler_step(action, v, 8, d.H * 8, t, B, d.H, d.A, 1.0 / d.steps)
+
+    def infer_action(self, ids, pix, cnt, vpos, ppos, apos, proprios, noise, kcache, vcache, clip=True):
+        d = self.d
+        B = ids.shape[0]
+        self.prefill(ids, pix, cnt, vpos, ppos, proprios, kcache, vcache)
+        action = noise.clone()
+        t = torch.zeros(B, device=pix.device, dtype=F32)
+        for _ in range(d.steps):
+            self.denoise_step(action, t, apos, cnt, kcache, vcache, B)
+        if clip and d.clip is not None:
+            ops.clamp_(action, -d.clip, d.clip)
+        return action
+
+    # --------------------------------------------------------------- hooks --
+    hook = None
+
+    def _notify(self, stage, layer):
+        if self.hook is not None:
+            self.hook(stage, layer)

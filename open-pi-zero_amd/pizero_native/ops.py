@@ -234,13 +234,17 @@ def flow_psi(x0, x1, t, psi, sig_min):
     call("pz_flow_psi", _p(x0), _p(x1), _p(t), _p(psi), B, x0[0].numel(), float(sig_min), _st())
 
 
-def flow_loss(v, ldv, x0, x1, loss, dv, grad_scale, B, H, A, sig_min):
-    call("pz_flow_loss", _p(v), ldv, _p(x0), _p(x1), _p(loss), _p(dv), _p(grad_scale), B, H, A, float(sig_min),
-         _st())
+def flow_loss(v, ldv, vbs, x0, x1, loss, dv, grad_scale, B, H, A, sig_min):
+    call("pz_flow_loss", _p(v), ldv, vbs, _p(x0), _p(x1), _p(loss), _p(dv), _p(grad_scale), B, H, A,
+         float(sig_min), _st())
 
 
-def euler_step(action, v, ldv, t, B, H, A, dt):
-    call("pz_euler_step", _p(action), _p(v), ldv, _p(t), B, H, A, float(dt), _st())
+def euler_step(action, v, ldv, vbs, t, B, H, A, dt):
+    call("pz_euler_step", _p(action), _p(v), ldv, vbs, _p(t), B, H, A, float(dt), _st())
+
+
+def copy_rows(src, sld, sbs, dst, dld, dbs, B, rows, D, scale=1.0, beta=False):
+    call("pz_copy_rows", _p(src), sld, sbs, _p(dst), dld, dbs, B, rows, D, float(scale), int(beta), _st())
 
 
 def clamp_(x, lo, hi):

@@ -38,9 +38,9 @@ FULL_DIMS = dict(
 # small structural twin of the bridge config (fast on CPU, same code paths)
 TINY_DIMS = dict(
     vocab_size=1024, image_token_index=1000, pad_token_id=0,
-    max_seq_len=12, num_image_tokens=4, cond_steps=1, horizon_steps=4,
+    max_seq_len=24, num_image_tokens=16, cond_steps=1, horizon_steps=4,
     action_dim=7, proprio_dim=7,
-    image_size=28, patch_size=14, vis_hidden=64, vis_inter=136,
+    image_size=56, patch_size=14, vis_hidden=64, vis_inter=136,
     vis_layers=2, vis_heads=4, ln_eps=1e-6, proj_dim=128,
     n_layers=3, n_heads=8, n_kv=1, head_dim=32, rms_eps=1e-6,
     vlm_hidden=128, vlm_inter=256, vlm_theta=10000.0,

@@ -65,13 +65,13 @@ def test_freezing_matches_reference_rules(tiny_model):
 
 
 def test_mask_builder_matches_reference_semantics(tiny_model):
-    am = torch.tensor([[1] * 10 + [0] * 2, [1] * 7 + [0] * 5], dtype=torch.int64)
+    am = torch.tensor([[1] * 10 + [0] * 14, [1] * 7 + [0] * 17], dtype=torch.int64)
     m1, v1, p1, a1 = tiny_model.build_causal_mask_and_position_ids(am, torch.bfloat16)
     m2, v2, p2, a2 = O.build_mask_and_positions(O.TINY_DIMS, am, torch.bfloat16)
     assert torch.equal(m1, m2) and torch.equal(v1, v2) and torch.equal(p1, p2) and torch.equal(a1, a2)
     assert tiny_model._prefix_counts(m1).tolist() == [10, 7]
     itp, amask = tiny_model.split_full_mask_into_submasks(m1)
-    assert itp.shape[-1] == 12 + 1 and amask.shape[-2] == 4
+    assert itp.shape[-1] == 24 + 1 and amask.shape[-2] == 4
 
 
 def test_dtype_conversion_keeps_arena_binding(tiny_model):

@@ -51,7 +51,8 @@ def _check_grads(g, m):
         rh = g["fp32/gradhead/" + n]
         cos = float(np.dot(head, rh) / (np.linalg.norm(head) * np.linalg.norm(rh) + 1e-30))
         ok_norm = ref == 0 and mine == 0 or abs(mine - ref) <= tol * ref
-        ok_cos = np.linalg.norm(rh) < 1e-12 * ref or cos >= (0.97 if np.linalg.norm(rh) > 1e-3 * ref else 0.9)
+        ok_cos = (ref == 0 and mine == 0) or np.linalg.norm(rh) < 1e-12 * ref or \
+            cos >= (0.97 if np.linalg.norm(rh) > 1e-3 * ref else 0.9)
         if not (ok_norm and ok_cos):
             bad.append((n, mine, ref, refb, cos))
     assert not bad, "\n".join(map(str, bad))

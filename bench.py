@@ -1,0 +1,268 @@
+"""Pi0 training throughput (+ action-chunk inference latency) on MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json metric, configs[1]/[2]): bridge-shaped synthetic batch
+(256 image + 20 text + 1 proprio + 4 action tokens), full Pi0 (SigLIP-So400m +
+Gemma-2B + 0.3B action expert, random-init weights), bf16, flow-matching
+forward + backward + grad-norm clip + AdamW over 2.6B trained parameters.
+One step = one optimizer update at global batch 1024 (= N GPUs x micro-batch x
+accumulation); with N GPUs the grads are all-reduced over RCCL, overlapped
+with the last micro-batch's backward.  ``value`` = samples/s of the whole job.
+Also reported: bf16 action-chunk inference latency (B=1, hipGraph replay),
+the dominant kernel's roofline (live HIP-event timing of the vlm GeGLU GEMM),
+and the CPU restatement (oracle/) timed on this host.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "open-pi-zero_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # dense MFMA bf16 (MI355X_MICROARCH.md)
+TRAIN_FLOP_PER_SAMPLE = 3.812e12  # SURVEY 8(d), FlopCounterMode on the reference
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def synthetic_batch(model, B, device, gen):
+    d = model._engine().d
+    ids = torch.full((B, d.P), 0, dtype=torch.int64)
+    ids[:, : d.n_img] = d.image_token
+    ids[:, d.n_img] = 2
+    ids[:, d.n_img + 1 : d.P - 1] = torch.randint(3, 256000, (B, d.P - d.n_img - 2), generator=gen)
+    ids[:, d.P - 1] = 108
+    am = (ids != 0).long()
+    mask, vpos, ppos, apos = model.build_causal_mask_and_position_ids(am, torch.bfloat16)
+    u = torch.rand(B, generator=gen)
+    t = 0.999 * (1 - u.pow(1 / 1.5))  # Beta(1.5, 1) flipped (train.py:239-247)
+    return dict(
+        input_ids=ids.to(device), pixel_values=(torch.rand(B, 3, d.img, d.img, generator=gen) * 2 - 1).to(device, torch.bfloat16),
+        causal_mask=mask.to(device), vlm_position_ids=vpos.to(device), proprio_position_ids=ppos.to(device),
+        action_position_ids=apos.to(device), proprios=(torch.rand(B, d.C, d.Pd, generator=gen) * 2 - 1).to(device),
+        actions=(torch.rand(B, d.H, d.A, generator=gen) * 2 - 1).to(device), t=t.to(device),
+    )
+
+
+def cpu_baseline(seconds_budget=25.0):
+    """Oracle (CPU fp32 restatement) fwd+bwd of one bridge sample on this host's cores."""
+    from oracle import pizero_oracle as O
+
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    d = O.FULL_DIMS
+    W = {}
+    for k, shp in O.param_shapes(d).items():
+        if ".mixtures.proprio." in k:
+            continue
+        W[k] = torch.empty(shp).uniform_(-0.02, 0.02).requires_grad_(k != "embed_tokens.weight")
+    for k in list(W):
+        if ".mixtures.action." in k:
+            W[k.replace(".mixtures.action.", ".mixtures.proprio.")] = W[k]
+    B = 1
+    ids = torch.full((B, d["max_seq_len"]), d["image_token_index"], dtype=torch.int64)
+    ids[:, 256] = 2
+    ids[:, 257:275] = 1000
+    ids[:, 275] = 108
+    mask, vpos, ppos, apos = O.build_mask_and_positions(d, (ids != 0).long())
+    pix = torch.rand(B, 3, 224, 224) * 2 - 1
+    prop = torch.rand(B, 1, 7)
+    act = torch.rand(B, 4, 7)
+    t = torch.rand(B)
+    x0 = torch.randn(B, 4, 7)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        loss = O.pizero_loss(W, d, ids, pix, mask, vpos, ppos, apos, prop, act, t, x0)
+        loss.backward()
+        for v in W.values():
+            v.grad = None
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds_budget or n >= 3:
+            break
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(line.split(":", 1)[1].strip() for line in f if line.startswith("model name"))
+    except Exception:
+        pass
+    return {"value": n * B / el, "unit": "samples/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x (bridge sample B=1 fwd+bwd, fp32 torch-CPU oracle/pizero_oracle.py), {el:.1f}s on {cpu}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--global-batch", type=int, default=1024)
+    ap.add_argument("--micro-batch", type=int, default=64)
+    ap.add_argument("--infer-iters", type=int, default=20)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-infer", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+
+    from pizero_native import ops
+    from pizero_native.ddp import PiZeroDDP
+    from pizero_native.graph import InferenceGraph
+    from pizero_native.optim import FusedAdamW, clip_grad_norm_
+    from src.model.vla.pizero import PiZero
+    from src.utils.config import load_config
+
+    cfg = load_config(os.path.join(ROOT, "open-pi-zero_amd", "config", "train", "bridge.yaml"))
+    torch.manual_seed(1234 + rank)
+    t0 = time.time()
+    model = PiZero(cfg, use_ddp=world > 1, device=dev, dtype=torch.bfloat16, init="default")
+    model.tie_action_proprio_weights()
+    model.freeze_unused_weights()
+    model.train()
+    meta = PiZeroDDP(model) if world > 1 else model
+    opt_a = FusedAdamW(model.action_expert_parameters, lr=cfg.action_lr, weight_decay=cfg.action_weight_decay)
+    opt_v = FusedAdamW(model.trainable_vlm_parameters, lr=cfg.vlm_lr, weight_decay=cfg.vlm_weight_decay)
+    gb = args.global_batch
+    mb = min(args.micro_batch, gb // world)
+    accum = max(1, gb // (world * mb))
+    gb = mb * accum * world
+    gen = torch.Generator().manual_seed(rank)
+    batches = [synthetic_batch(model, mb, dev, gen) for _ in range(min(accum, 2))]
+    log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world} micro_batch={mb} accum={accum} global={gb}")
+    loss_acc = torch.zeros(1, device=dev)
+
+    def step():
+        for i in range(accum):
+            b = batches[i % len(batches)]
+            last = i == accum - 1
+            ctx = meta.no_sync() if (world > 1 and not last) else torch.enable_grad()
+            with ctx:
+                loss = meta(**b)
+                (loss / accum).backward()
+            loss_acc.add_(loss.detach())
+        clip_grad_norm_([opt_a, opt_v], cfg.max_grad_norm)
+        opt_a.step()
+        opt_v.step()
+        opt_a.zero_grad(set_to_none=True)
+        opt_v.zero_grad(set_to_none=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    # live probe of the dominant kernel: the vlm GeGLU gate|up GEMM (M = mb*276, N = 2*16384, K = 2048)
+    d = model._engine().d
+    Mg, Ng, Kg = mb * d.P, 2 * d.gI, d.gH
+    probe = ops.set_probe(lambda M, N, K, epi, batch: (M, N, K, epi) == (Mg, Ng, Kg, ops.PZ_EPI_GEGLU))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if world > 1:
+        dist.all_reduce(loss_acc)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t1
+    ops.set_probe(None)
+    elt = torch.tensor([el], device=dev)
+    if world > 1:
+        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+    el = float(elt.item())
+    durs = [a.elapsed_time(b) for a, b in probe]
+    kern_ms = sum(durs) / max(1, len(durs))
+    flops_launch = 2.0 * Mg * Ng * Kg
+    achieved = flops_launch / (kern_ms * 1e-3) / 1e12 if durs else None
+    samples_s = gb * args.steps / el
+
+    infer = None
+    if not args.no_infer and rank == 0:
+        model.eval()
+        gi = synthetic_batch(model, 1, dev, torch.Generator().manual_seed(7))
+        itp, amask = model.split_full_mask_into_submasks(gi["causal_mask"])
+        noise = torch.randn(1, d.H, d.A, device=dev)
+        # eager native path
+        for _ in range(2):
+            model.infer_action(gi["input_ids"], gi["pixel_values"], itp, amask, gi["vlm_position_ids"],
+                               gi["proprio_position_ids"], gi["action_position_ids"], gi["proprios"], noise=noise)
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(5):
+            model.infer_action(gi["input_ids"], gi["pixel_values"], itp, amask, gi["vlm_position_ids"],
+                               gi["proprio_position_ids"], gi["action_position_ids"], gi["proprios"], noise=noise)
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - te) / 5 * 1e3
+        g = InferenceGraph(model, 1)
+        g.load(gi["input_ids"], gi["pixel_values"], model._prefix_counts(itp), gi["vlm_position_ids"],
+               gi["proprio_position_ids"], gi["action_position_ids"], gi["proprios"], noise)
+        g.capture()
+        for _ in range(3):
+            g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(args.infer_iters):
+            g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        graph_ms = e0.elapsed_time(e1) / args.infer_iters
+        infer = {"metric": "bf16 action-chunk infer ms (B=1, prefill + 10 Euler steps)", "graph_ms": graph_ms,
+                 "eager_ms": eager_ms, "higher_is_better": False, "baseline_ms": 75.0,
+                 "vs_baseline": 75.0 / graph_ms, "hbm_floor_ms": 1.44}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
+
+    if rank == 0:
+        line = {
+            "metric": "train samples/sec at gbsz 1024 (bf16 fwd+bwd+clip+AdamW)",
+            "value": samples_s, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init weights, random pixels/tokens/proprio/actions)",
+            "config": {"workload": "Pi0 bridge training step: 256 img + 20 text + 1 proprio + 4 action tokens",
+                       "model": "pi0 (SigLIP-So400m/14 + Gemma-2B + 0.3B action expert)", "global_batch": gb,
+                       "micro_batch": mb, "grad_accum": accum, "seq_len": d.L,
+                       "parallelism": f"dp{world}"},
+            "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
+            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<true,true,4> (vlm gate|up GeGLU GEMM)",
+                         "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,
+                         "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS, "traffic": None},
+            "inference": infer,
+            "cpu_baseline": cpu,
+            "loss_mean": float(loss_acc.item()) / (accum * args.steps * max(1, world)),
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

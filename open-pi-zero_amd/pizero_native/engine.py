@@ -689,6 +689,8 @@ class Engine:
             dimg = torch.empty(B * d.n_img, d.gH, device=dev, dtype=BF16)
             ops.embed_merge_bwd(sv["ids"], dX["vlm"], dimg, d.n_img, d.image_token, 1.0)
             self.siglip_backward(sv["sv_v"], dimg, beta)
+        if self.post_backward is not None:
+            self.post_backward()
 
     # ============================================================ inference ==
     def prefill(self, ids, pix, cnt, vpos, ppos, proprios, kcache, vcache):
@@ -817,7 +819,8 @@ class Engine:
         return action
 
     # --------------------------------------------------------------- hooks --
-    hook = None
+    hook = None  # called as hook(stage, layer) when a layer's parameter gradients are final
+    post_backward = None  # called once at the end of train_backward (gradient all-reduce flush)
 
     def _notify(self, stage, layer):
         if self.hook is not None:

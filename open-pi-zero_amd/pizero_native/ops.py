@@ -35,10 +35,35 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+_PROBE = None
+
+
+def set_probe(pred):
+    """Record (start, end) HIP events around every pz_gemm launch for which pred(M, N, K, epi, batch)
+    is true, on the launch stream (bench.py measures the dominant kernel's duration live)."""
+    global _PROBE
+    _PROBE = None if pred is None else (pred, [])
+    return None if _PROBE is None else _PROBE[1]
+
+
 def gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, *, epi=PZ_EPI_NONE, alpha=1.0, beta=False,
          bias=None, resid=None, ld_resid=0, aux=None, ld_aux=0, geglu_inter=0, batch=1, batch_inner=1,
          sA=(0, 0), sB=(0, 0), sC=(0, 0), sR=(0, 0)):
     """Raw GEMM: see pz_gemm_args in include/pz_abi.h.  Element strides."""
+    if _PROBE is not None and _PROBE[0](M, N, K, epi, batch):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+              geglu_inter, batch, batch_inner, sA, sB, sC, sR)
+        e1.record()
+        _PROBE[1].append((e0, e1))
+        return
+    _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR)
+
+
+def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR):
     a = GemmArgs()
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.A, a.lda, a.a_kcontig = _p(A), int(lda), int(bool(a_kc))

@@ -90,6 +90,8 @@ def _resolve_str(s, root, depth=0):
     whole = _REF.fullmatch(s.strip())
     if whole and not whole.group(1).startswith(("oc.env:", "now:", "eval:")):
         v = _lookup(root, whole.group(1).strip())
+        if isinstance(v, (dict, list)):
+            return _resolve(v, root)
         return _resolve_str(v, root, depth + 1) if isinstance(v, str) else v
     out = _REF.sub(rep, s)
     return _resolve_str(out, root, depth + 1) if "${" in out else _coerce(out)

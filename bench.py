@@ -251,7 +251,7 @@ def main():
                        "micro_batch": mb, "grad_accum": accum, "seq_len": d.L,
                        "parallelism": f"dp{world}"},
             "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
-            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<true,true,4> (vlm gate|up GeGLU GEMM)",
+            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<true,true,4,1> (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS, "traffic": None},

@@ -93,7 +93,7 @@ __device__ __forceinline__ void r2s(const u32x4 (&r)[4], char* lds) {
 }
 
 // fragment for rows rb*16.., k = kk*32 + 8*(lane>>4) + j
-template <bool KC>
+template <bool KC, int TRROW = 256>
 __device__ __forceinline__ bf16x8 frag(const char* lds, int rb, int kk, int lane) {
   if (KC) {
     const int r = rb * 16 + (lane & 15);
@@ -105,7 +105,7 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rb, int kk, int lane
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int k = kk * 32 + 8 * (lane >> 4) + 4 * t + q;
-      const int off = k * 256 + (((4 * rb + p) ^ sw_tr(k)) << 3);
+      const int off = k * TRROW + (((4 * rb + p) ^ sw_tr(k)) << 3);
       s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
           (__attribute__((address_space(3))) s16x4*)(lds + off));
       out[4 * t + 0] = v[0];
@@ -130,6 +130,91 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
   const int in = wg - g * per_group;
   tm = first_m + in % gsize;
   tn = in / gsize;
+}
+
+// ---- epilogue: one lane owns C[m][n..n+3] (swapped-operand MFMA layout) -------
+__device__ __forceinline__ void store_out4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                           const f32x4& acc) {
+  if (m >= p.M || n >= p.N) return;
+  const bool full = n + 4 <= p.N;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = acc[r] * p.alpha;
+  if (p.bias) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (full || n + r < p.N) v[r] += bf2f(p.bias[n + r]);
+  }
+  if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+    if (p.aux) {
+      bf16_t* X = p.aux + m * p.ld_aux + n;
+      if (full) {
+        *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      } else {
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) X[r] = f2bf(v[r]);
+      }
+    }
+    if (p.epi == PZ_EPI_GELU) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+    }
+  }
+  if (p.resid) {
+    const bf16_t* R = p.resid + rofs + m * p.ld_resid + n;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (full || n + r < p.N) v[r] += bf2f(R[r]);
+  }
+  if (p.c_fp32) {
+    float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
+    if (full) {
+      if (p.beta) {
+        f32x4 o = *reinterpret_cast<f32x4*>(Cp);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
+    } else {
+      for (int r = 0; r < 4; ++r)
+        if (n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
+    }
+  } else {
+    bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+    if (full) {
+      if (p.beta) {
+        u32x2 o = *reinterpret_cast<u32x2*>(Cp);
+        v[0] += bf2f(o[0] & 0xffff); v[1] += bf2f(o[0] >> 16);
+        v[2] += bf2f(o[1] & 0xffff); v[3] += bf2f(o[1] >> 16);
+      }
+      *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    } else {
+      for (int r = 0; r < 4; ++r)
+        if (n + r < p.N) Cp[r] = f2bf(p.beta ? bf2f(Cp[r]) + v[r] : v[r]);
+    }
+  }
+}
+
+// GeGLU: gate and up accumulators of the same (m, n..n+3) -> h = gelu_tanh(g) * u (+ saved g|u)
+__device__ __forceinline__ void store_geglu4(const GemmP& p, int64_t cofs, int64_t m, int64_t n, const f32x4& ga,
+                                             const f32x4& ua) {
+  if (m >= p.M || n >= p.geglu_I) return;
+  float h[4], g[4], u[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    g[r] = ga[r] * p.alpha;
+    u[r] = ua[r] * p.alpha;
+    h[r] = gelu_tanh(g[r]) * u[r];
+  }
+  bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+  *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
+  if (p.aux) {
+    bf16_t* X = p.aux + m * p.ld_aux + n;
+    *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(g[0], g[1]), pack2bf(g[2], g[3])};
+    *reinterpret_cast<u32x2*>(X + p.geglu_I) = u32x2{pack2bf(u[0], u[1]), pack2bf(u[2], u[3])};
+  }
 }
 
 // TAG only separates kernel symbols (profiling): 1 = the Gemma-2B MLP gate|up GeGLU GEMM (M >= 2048 rows)
@@ -201,105 +286,217 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   // ---------------------------------------------------------------- epilogue
   const int64_t cofs = zo * p.sCo + zi * p.sCi;
   const int64_t rofs = zo * p.sRo + zi * p.sRi;
-  const float alpha = p.alpha;
   if (geglu) {
     // wave tile = 32 rows x 128 cols: cols [0,64) gate, [64,128) up
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-      if (m >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < NI / 2; ++j) {
-        const int64_t n = n0 + j * 16 + 4 * (lane >> 4);
-        if (n >= p.geglu_I) continue;
-        float h[4], g[4], u[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          g[r] = acc[i][j][r] * alpha;
-          u[r] = acc[i][j + NI / 2][r] * alpha;
-          h[r] = gelu_tanh(g[r]) * u[r];
-        }
-        bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-        *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
-        if (p.aux) {
-          bf16_t* X = p.aux + m * p.ld_aux + n;
-          *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(g[0], g[1]), pack2bf(g[2], g[3])};
-          *reinterpret_cast<u32x2*>(X + p.geglu_I) = u32x2{pack2bf(u[0], u[1]), pack2bf(u[2], u[3])};
-        }
-      }
+      for (int j = 0; j < NI / 2; ++j)
+        store_geglu4(p, cofs, m, n0 + j * 16 + 4 * (lane >> 4), acc[i][j], acc[i][j + NI / 2]);
     }
     return;
   }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int64_t n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
-      if (n >= p.N) continue;
-      const bool full = n + 4 <= p.N;
-      float v[4];
+    for (int j = 0; j < NI; ++j)
+      store_out4(p, cofs, rofs, m, n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+// -------------------------------------------------------------------------
+// 256x256 tile, 512 threads = 8 waves (4 along M x 2 along N, 64x128 per wave),
+// operands streamed global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
+// wave-instruction, no VGPR staging).  Two pipelines are built from one body:
+//   BK2 = 64, 2 stages (2 x 64 KiB): the next K-tile's DMA is issued before the
+//     current tile's 64 MFMAs per wave; one vmcnt(0) + barrier per K step;
+//   BK2 = 32, 4-slot ring (4 x 32 KiB): three K-tiles in flight, counted
+//     vmcnt (never 0 in steady state) + raw s_barrier per K step.
+// Measured on MI355X (tools/gemm_bench.py, random bf16): the 64/2-stage form
+// is faster on every Pi0 shape (fewer barriers outweigh the deeper prefetch),
+// so it is the one dispatched; the ring is kept for A/B experiments.
+// LDS images are XOR-swizzled for conflict-free ds_read_b128 (k-contiguous
+// operands) and ds_read_b64_tr_b16 (k-strided operands, [k][row] 512-B rows);
+// the swizzle is applied to each lane's GLOBAL source address because an
+// LDS-DMA write is lane-linear.  Requires K % BK2 == 0; M/N tails clamp the
+// source rows (clamped rows are never stored).  GEGLU: B rows interleave
+// gate/up in 64-row blocks so each wave's 128 virtual columns are 64 gate +
+// the matching 64 up columns.
+// -------------------------------------------------------------------------
+constexpr int BT = 256, NT2 = 512;
+
+__device__ __forceinline__ void glds16(const bf16_t* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// k-contiguous image [256 rows][BKT k]: 16-B chunk ch of row r lives at chunk ch ^ swz(r)
+template <int BKT>
+__device__ __forceinline__ int swz_kc(int r) {
+  return BKT == 64 ? ((r >> 1) & 7) : 3 * ((r >> 3) & 1);
+}
+
+// global source of lane `lane` for DMA instruction j of an operand tile (BKT*256*2/1024 instructions)
+template <bool KC, int BKT>
+__device__ __forceinline__ const bf16_t* dma_src(const bf16_t* base, int64_t ld, int j, int lane, int64_t row0,
+                                                 int64_t R, bool geglu, int64_t gI) {
+  if (KC) {
+    constexpr int CPR = BKT / 8;          // 16-B chunks per row
+    constexpr int RPI = 64 / CPR;         // rows per 1 KiB instruction
+    const int r = RPI * j + lane / CPR;
+    const int kc = (lane % CPR) ^ swz_kc<BKT>(r);
+    int64_t grow;
+    if (geglu) {
+      const int blk = r >> 6;
+      int64_t idx = row0 + (blk >> 1) * 64 + (r & 63);
+      idx = idx < gI ? idx : gI - 1;
+      grow = (blk & 1) ? gI + idx : idx;
+    } else {
+      grow = row0 + r;
+      grow = grow < R ? grow : R - 1;
+    }
+    return base + grow * ld + 8 * kc;
+  } else {
+    const int k = 2 * j + (lane >> 5);
+    const int c = (2 * (lane & 31)) ^ sw_tr(k);
+    int64_t r = row0 + 4 * c;
+    r = r <= R - 8 ? r : R - 8;
+    return base + (int64_t)k * ld + r;
+  }
+}
+
+template <bool KC, int BKT>
+__device__ __forceinline__ bf16x8 frag256(const char* lds, int rb, int kk, int lane) {
+  if (KC) {
+    const int r = rb * 16 + (lane & 15);
+    const int ch = kk * 4 + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(lds + r * (BKT * 2) + ((ch ^ swz_kc<BKT>(r)) << 4));
+  } else {
+    return frag<false, 512>(lds, rb, kk, lane);
+  }
+}
+
+#define PZ_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+#define PZ_BARRIER()                                   \
+  do {                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_s_barrier();                      \
+    asm volatile("" ::: "memory");                     \
+  } while (0)
+
+template <bool AKC, bool BKC, bool GEGLU, int BKT>
+__global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int MI = 4, NI = 8;
+  constexpr int NSTAGE = BKT == 64 ? 2 : 4;
+  constexpr int IMG = 256 * BKT * 2;
+  constexpr int STAGE = 2 * IMG;
+  constexpr int NI_DMA = IMG / 1024 / 8;  // DMA instructions per wave per operand per K-tile
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int64_t m0 = (int64_t)tm * BT;
+  const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int64_t z = blockIdx.y;
+  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bf16_t* Ab = p.A + zo * p.sAo + zi * p.sAi;
+  const bf16_t* Bb = p.B + zo * p.sBo + zi * p.sBi;
+  const int64_t cofs = zo * p.sCo + zi * p.sCi;
+  const int64_t rofs = zo * p.sRo + zi * p.sRi;
+
+  const bf16_t* sa[NI_DMA];
+  const bf16_t* sb[NI_DMA];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] * alpha;
-      if (p.bias) {
+  for (int i = 0; i < NI_DMA; ++i) {
+    sa[i] = dma_src<AKC, BKT>(Ab, p.lda, wave * NI_DMA + i, lane, m0, p.M, false, 0);
+    sb[i] = dma_src<BKC, BKT>(Bb, p.ldb, wave * NI_DMA + i, lane, n0, p.N, GEGLU, p.geglu_I);
+  }
+  const int64_t stepA = AKC ? BKT : BKT * p.lda;
+  const int64_t stepB = BKC ? BKT : BKT * p.ldb;
+
+  f32x4 acc[MI][NI];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) v[r] += bf2f(p.bias[n + r]);
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (int)(p.K / BKT);
+  auto issue = [&](int kt) {
+    char* ia = smem + (kt % NSTAGE) * STAGE;
+    char* ib = ia + IMG;
+#pragma unroll
+    for (int i = 0; i < NI_DMA; ++i) {
+      glds16(sa[i] + kt * stepA, ia + (wave * NI_DMA + i) * 1024);
+      glds16(sb[i] + kt * stepB, ib + (wave * NI_DMA + i) * 1024);
+    }
+  };
+  auto compute = [&](int kt) {
+    const char* a_img = smem + (kt % NSTAGE) * STAGE;
+    const char* b_img = a_img + IMG;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 bfr[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) bfr[j] = frag256<BKC, BKT>(b_img, wn * NI + j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const bf16x8 af = frag256<AKC, BKT>(a_img, wm * MI + i, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af, acc[i][j], 0, 0, 0);
       }
-      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
-        if (p.aux) {
-          bf16_t* X = p.aux + m * p.ld_aux + n;
-          if (full) {
-            *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-          } else {
-            for (int r = 0; r < 4; ++r)
-              if (n + r < p.N) X[r] = f2bf(v[r]);
-          }
-        }
-        if (p.epi == PZ_EPI_GELU) {
+    }
+  };
+  if constexpr (BKT == 64) {
+    issue(0);
+    PZ_WAIT_VM(0);
+    PZ_BARRIER();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) issue(kt + 1);
+      compute(kt);
+      PZ_WAIT_VM(0);
+      PZ_BARRIER();
+    }
+  } else {
+    issue(0);
+    if (nk > 1) issue(1);
+    if (nk > 2) issue(2);
+    if (nk > 2) PZ_WAIT_VM(8);
+    else if (nk > 1) PZ_WAIT_VM(4);
+    else PZ_WAIT_VM(0);
+    PZ_BARRIER();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 3 < nk) issue(kt + 3);
+      compute(kt);
+      if (kt + 3 < nk) PZ_WAIT_VM(8);  // retire tile kt+1, keep kt+2, kt+3 in flight
+      else if (kt + 2 < nk) PZ_WAIT_VM(4);
+      else PZ_WAIT_VM(0);
+      PZ_BARRIER();
+    }
+  }
+  if (GEGLU) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-        } else {
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
-        }
-      }
-      if (p.resid) {
-        const bf16_t* R = p.resid + rofs + m * p.ld_resid + n;
+      for (int j = 0; j < NI / 2; ++j)
+        store_geglu4(p, cofs, m, n0 + wn * 64 + j * 16 + 4 * (lane >> 4), acc[i][j], acc[i][j + NI / 2]);
+    }
+  } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (full || n + r < p.N) v[r] += bf2f(R[r]);
-      }
-      if (p.c_fp32) {
-        float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
-        if (full) {
-          if (p.beta) {
-            f32x4 o = *reinterpret_cast<f32x4*>(Cp);
-            v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-          }
-          *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
-        }
-      } else {
-        bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-        if (full) {
-          if (p.beta) {
-            u32x2 o = *reinterpret_cast<u32x2*>(Cp);
-            v[0] += bf2f(o[0] & 0xffff); v[1] += bf2f(o[0] >> 16);
-            v[2] += bf2f(o[1] & 0xffff); v[3] += bf2f(o[1] >> 16);
-          }
-          *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-        } else {
-          for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) Cp[r] = f2bf(p.beta ? bf2f(Cp[r]) + v[r] : v[r]);
-        }
-      }
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) store_out4(p, cofs, rofs, m, n0 + wn * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
     }
   }
 }
+
+constexpr int BK256 = 64;  // dispatched K-tile of the 256 kernel (see above)
 
 // -------------------------------------------------------------------------
 // Skinny GEMM for M <= 16 (inference denoise steps, B = 1..4): weights are
@@ -438,6 +635,20 @@ static int launch_tile(const GemmP& p, int64_t batch, hipStream_t st) {
   return PZ_OK;
 }
 
+template <bool AKC, bool BKC, bool GEGLU>
+static int launch256(const GemmP& p, int64_t batch, hipStream_t st) {
+  const int smem = 2 * 2 * 256 * 64 * 2;  // 128 KiB for either pipeline
+  auto kern = gemm256_kernel<AKC, BKC, GEGLU, BK256>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n, (unsigned)batch), dim3(NT2), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
 extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   PZ_CHECK_ARG(a != nullptr, "pz_gemm: null args");
   PZ_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0, "pz_gemm: bad dims M=%lld N=%lld K=%lld",
@@ -494,6 +705,19 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
     hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, st, p);
     PZ_CHECK_LAUNCH();
     return PZ_OK;
+  }
+  if (a->K % BK256 == 0 && a->M >= 512 && ncols >= (geglu ? 256 : 512) &&
+      a->batch * ((a->M + BT - 1) / BT) * ((ncols + (geglu ? BT / 2 : BT) - 1) / (geglu ? BT / 2 : BT)) >= 160) {
+    p.tiles_m = (int)((a->M + BT - 1) / BT);
+    p.tiles_n = (int)((ncols + (geglu ? BT / 2 : BT) - 1) / (geglu ? BT / 2 : BT));
+    if (geglu) {
+      if (a->a_kcontig) return launch256<true, true, true>(p, a->batch, st);
+      return launch256<false, true, true>(p, a->batch, st);
+    }
+    if (a->a_kcontig && a->b_kcontig) return launch256<true, true, false>(p, a->batch, st);
+    if (a->a_kcontig && !a->b_kcontig) return launch256<true, false, false>(p, a->batch, st);
+    if (!a->a_kcontig && a->b_kcontig) return launch256<false, true, false>(p, a->batch, st);
+    return launch256<false, false, false>(p, a->batch, st);
   }
   p.tiles_m = (int)((a->M + BM - 1) / BM);
   p.tiles_n = (int)((ncols + (geglu ? BN / 2 : BN) - 1) / (geglu ? BN / 2 : BN));

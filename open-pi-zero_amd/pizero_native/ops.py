@@ -104,11 +104,33 @@ def linear_dgrad(dy, W, dx, *, beta=False, resid=None):
     return dx
 
 
+def _split_k(M, N, K):
+    """Split the token (reduction) dim when the output has too few 256x256 tiles to fill 256 CUs."""
+    tiles = ((N + 255) // 256) * ((K + 255) // 256)
+    if tiles >= 160 or M < 4096 or N < 512 or K < 512:
+        return 1
+    best = 1
+    for s in (2, 4, 8):  # fewest splits that reach ~1 wave of 256-thread... 240+ workgroups
+        if M % (s * 64) == 0:
+            best = s
+            if tiles * s >= 240:
+                break
+    return best
+
+
 def linear_wgrad(dy, x, dW, *, beta=False):
-    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]."""
+    """dW[N,K] (+)= dy[M,N]^T @ x[M,K]   (split-K over tokens into fp32 slabs when the output is small)."""
     M, N = dy.shape
     K = x.shape[1]
-    gemm(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, dW, dW.stride(0), beta=beta)
+    S = _split_k(M, N, K) if dW.is_contiguous() else 1
+    if S == 1:
+        gemm(N, K, M, dy, dy.stride(0), False, x, x.stride(0), False, dW, dW.stride(0), beta=beta)
+        return dW
+    Mc = M // S
+    slabs = torch.empty(S, N, K, device=dW.device, dtype=torch.float32)
+    gemm(N, K, Mc, dy, dy.stride(0), False, x, x.stride(0), False, slabs, K, batch=S,
+         sA=(Mc * dy.stride(0), 0), sB=(Mc * x.stride(0), 0), sC=(N * K, 0))
+    reduce_parts(slabs.view(S, N * K), dW.view(-1), beta=beta)
     return dW
 
 

@@ -83,6 +83,41 @@ def test_all_four_layouts_batched_fp32_out():
             close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm256_layouts_with_tails(akc, bkc):
+    """Large shapes take the 256x256 LDS-DMA kernel; M/N not multiples of the tile."""
+    from pizero_native import ops
+
+    M, N, K = 2600, 4104, 1024
+    A = bf(M, K, scale=0.5)
+    Bm = bf(N, K, scale=0.5)
+    ref = A.float() @ Bm.float().t()
+    Aop = A if akc else A.t().contiguous()
+    Bop = Bm if bkc else Bm.t().contiguous()
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    bias = bf(N)
+    ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, C, N, bias=bias)
+    close(C, ref + bias.float(), atol=3e-2)
+    Cf = torch.zeros(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, Cf, N, beta=True)
+    ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, Cf, N, beta=True)
+    close(Cf, 2 * ref, rtol=1e-3, atol=1e-2)
+
+
+def test_gemm256_geglu_with_tail():
+    from pizero_native import ops
+
+    M, K, I = 2000, 512, 4100
+    x = bf(M, K)
+    W = bf(2 * I, K, scale=K ** -0.5)
+    h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+    gu = torch.empty(M, 2 * I, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+    ref = x.float() @ W.float().t()
+    close(gu, ref)
+    close(h, torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:])
+
+
 def test_epilogues_gelu_resid_geglu_silu():
     from pizero_native import ops
 
@@ -283,3 +318,17 @@ def test_adamw_matches_torch():
     acc = torch.zeros(1, device=dev)
     ops.sumsq(g, acc)
     assert abs(acc.item() - (g.float() ** 2).sum().item()) < 1e-3 * acc.item()
+
+
+def test_wgrad_split_k_matches_single_pass():
+    from pizero_native import ops
+
+    M, N, K = 8192, 1024, 768  # small output, long token reduction -> split-K path
+    assert ops._split_k(M, N, K) > 1
+    dy, x = bf(M, N), bf(M, K)
+    dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_wgrad(dy, x, dW)
+    ref = dy.float().t() @ x.float()
+    close(dW, ref, atol=0.05 * math.sqrt(M) / 16)
+    ops.linear_wgrad(dy, x, dW, beta=True)
+    close(dW, 2 * ref, atol=0.1 * math.sqrt(M) / 16)

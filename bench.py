@@ -122,10 +122,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # PZ_DEVICE / PZ_DIST_BACKEND: single-GPU rehearsal of the N>1 path (gloo, all ranks on one card)
+    dev_idx = int(os.environ.get("PZ_DEVICE", local))
+    backend = os.environ.get("PZ_DIST_BACKEND", "nccl")
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device(f"cuda:{dev_idx}")
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from pizero_native import ops
     from pizero_native.ddp import PiZeroDDP

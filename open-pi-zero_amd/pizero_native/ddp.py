@@ -38,9 +38,10 @@ class GradReducer:
 
     def _launch(self, region, lo, hi):
         g = self.arena.grad[lo:hi]
-        if self.stream is None:
+        if self.stream is None or dist.get_backend(self.group) != "nccl":
+            # gloo (CPU tests / single-GPU rehearsal): synchronous SUM then scale
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
-            g.div_(dist.get_world_size(self.group))
+            g.mul_(1.0 / dist.get_world_size(self.group))
             return
         ev = torch.cuda.Event()
         ev.record()

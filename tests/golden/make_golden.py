@@ -282,3 +282,33 @@ if __name__ == "__main__":
         make("tiny", TINY_DIMS, 3, ragged=True)
     if which in ("full", "all"):
         make("full", FULL_DIMS, 2, ragged=True)
+
+
+def make_lr():
+    """lr trace of the reference CosineAnnealingWarmupRestarts (utils/optim.py:31-159)."""
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from src.utils.optim import CosineAnnealingWarmupRestarts
+
+    out = {}
+    for name, (first, mult, mx, mn, warm, gamma) in {
+        "bridge": (10000000, 1.0, 5e-5, 1e-8, 200, 1.0),
+        "restarts": (50, 1.0, 1e-3, 1e-6, 10, 0.5),
+        "mult": (40, 2.0, 1e-3, 1e-6, 5, 0.8),
+    }.items():
+        p = [torch.nn.Parameter(torch.zeros(1))]
+        opt = torch.optim.SGD(p, lr=1.0)
+        s = CosineAnnealingWarmupRestarts(opt, first_cycle_steps=first, cycle_mult=mult, max_lr=mx, min_lr=mn,
+                                          warmup_steps=warm, gamma=gamma)
+        lrs = [opt.param_groups[0]["lr"]]
+        for _ in range(300):
+            s.step()
+            lrs.append(opt.param_groups[0]["lr"])
+        out[name] = np.array(lrs, dtype=np.float64)
+        out[name + "_args"] = np.array([first, mult, mx, mn, warm, gamma], dtype=np.float64)
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "lr_schedule.npz"), **out)
+    print("wrote lr_schedule.npz")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lr":
+    make_lr()

@@ -144,9 +144,9 @@ int pz_patchify(const void* pix, void* cols, int64_t B, int64_t H, int64_t W, in
 /* token embed + image merge (pizero.py:376-414) with the joint-model sqrt(hidden) scaling
  * (joint_model.py:348-355) folded in: out[b,i] = text ? table[id]*emb_scale : image ?
  * img[b,k]*img_scale : 0 */
-int pz_embed_merge(const int64_t* ids, const void* table, const void* img, void* out, int64_t B,
-                   int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
-                   float emb_scale, float img_scale, void* stream);
+int pz_embed_merge(const int64_t* ids, const void* table, int64_t vocab, const void* img, void* out,
+                   int64_t B, int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
+                   float emb_scale, float img_scale, void* stream);  /* ids outside [0,vocab) -> zero row */
 /* dimg[b,k] = dout[b,i]*img_scale for image tokens */
 int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* dimg, int64_t B, int64_t P,
                        int64_t D, int64_t n_img, int64_t image_token, float img_scale, void* stream);

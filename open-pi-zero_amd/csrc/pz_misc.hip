@@ -27,7 +27,7 @@ __global__ void patchify_kernel(const bf16_t* __restrict__ pix, bf16_t* cols, in
   }
 }
 
-__global__ void embed_merge_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table,
+__global__ void embed_merge_kernel(const int64_t* __restrict__ ids, const bf16_t* __restrict__ table, int64_t vocab,
                                    const bf16_t* __restrict__ img, bf16_t* out, int64_t P, int64_t D,
                                    int64_t n_img, int64_t image_token, int64_t pad_token, float emb_scale,
                                    float img_scale) {
@@ -49,7 +49,7 @@ __global__ void embed_merge_kernel(const int64_t* __restrict__ ids, const bf16_t
     }
     const bf16_t* src = img + (b * n_img + k) * D;
     for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = f2bf(bf2f(src[d]) * img_scale);
-  } else if (id == pad_token) {
+  } else if (id == pad_token || id < 0 || id >= vocab) {  // out-of-vocabulary ids never read the table
     for (int64_t d = threadIdx.x; d < D; d += blockDim.x) o[d] = 0;
   } else {
     const bf16_t* src = table + id * D;
@@ -279,13 +279,13 @@ extern "C" int pz_patchify(const void* pix, void* cols, int64_t B, int64_t H, in
   return PZ_OK;
 }
 
-extern "C" int pz_embed_merge(const int64_t* ids, const void* table, const void* img, void* out, int64_t B,
-                              int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
+extern "C" int pz_embed_merge(const int64_t* ids, const void* table, int64_t vocab, const void* img, void* out,
+                              int64_t B, int64_t P, int64_t D, int64_t n_img, int64_t image_token, int64_t pad_token,
                               float emb_scale, float img_scale, void* stream) {
-  PZ_CHECK_ARG(ids && table && img && out && B > 0 && P > 0 && D > 0, "embed_merge: bad args");
+  PZ_CHECK_ARG(ids && table && img && out && B > 0 && P > 0 && D > 0 && vocab > 0, "embed_merge: bad args");
   hipLaunchKernelGGL(embed_merge_kernel, dim3((unsigned)P, (unsigned)B), dim3(256), 0, ST, ids,
-                     (const bf16_t*)table, (const bf16_t*)img, (bf16_t*)out, P, D, n_img, image_token, pad_token,
-                     emb_scale, img_scale);
+                     (const bf16_t*)table, vocab, (const bf16_t*)img, (bf16_t*)out, P, D, n_img, image_token,
+                     pad_token, emb_scale, img_scale);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -70,7 +70,7 @@ SIGNATURES = {
     "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],
     "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
     "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],
-    "pz_embed_merge": [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, f32, f32, vp],
+    "pz_embed_merge": [vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, f32, vp],
     "pz_embed_merge_bwd": [vp, vp, vp, i64, i64, i64, i64, i64, f32, vp],
     "pz_time_embed": [vp, vp, i64, i64, f32, vp],
     "pz_concat_time": [vp, vp, vp, i64, i64, i64, vp],

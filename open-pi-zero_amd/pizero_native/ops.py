@@ -252,7 +252,8 @@ def patchify(pix, cols, ps):
 def embed_merge(ids, table, img, out, n_img, image_token, pad_token, emb_scale, img_scale):
     B, P = ids.shape
     D = table.shape[1]
-    call("pz_embed_merge", _p(ids), _p(table), _p(img), _p(out), B, P, D, n_img, image_token, pad_token,
+    call("pz_embed_merge", _p(ids), _p(table), table.shape[0], _p(img), _p(out), B, P, D, n_img, image_token,
+         pad_token,
          float(emb_scale), float(img_scale), _st())
 
 

@@ -44,14 +44,16 @@ class SyntheticBridgeDataset(torch.utils.data.IterableDataset):
         n_img = cfg_get(c, "vision.config.num_image_tokens")
         H = cfg_get(c, "horizon_steps")
         img = cfg_get(c, "vision.config.image_size")
+        vmax = min(int(cfg_get(c, "vocab_size")), int(cfg_get(c, "image_token_index")))
+        nl = min(108, vmax - 1)
         while True:
             ids = torch.zeros(self.B, P, dtype=torch.int64)
             ids[:, :n_img] = cfg_get(c, "image_token_index")
             ids[:, n_img] = 2
             for b in range(self.B):
                 n = int(torch.randint(4, P - n_img, (1,), generator=g))
-                ids[b, n_img + 1 : n_img + n - 1] = torch.randint(3, 256000, (n - 2,), generator=g)
-                ids[b, n_img + n - 1] = 108
+                ids[b, n_img + 1 : n_img + n - 1] = torch.randint(3, vmax, (n - 2,), generator=g)
+                ids[b, n_img + n - 1] = nl
             yield {
                 "input_ids": ids,
                 "attention_mask": (ids != 0).long(),

@@ -203,6 +203,7 @@ def main():
     durs = [a.elapsed_time(b) for a, b in probe]
     kern_ms = sum(durs) / max(1, len(durs))
     flops_launch = 2.0 * Mg * Ng * Kg
+    kname = ops.gemm_kernel_name(Mg, Ng, Kg, epi=ops.PZ_EPI_GEGLU, geglu_inter=d.gI)
     achieved = flops_launch / (kern_ms * 1e-3) / 1e12 if durs else None
     samples_s = gb * args.steps / el
 
@@ -257,7 +258,7 @@ def main():
                        "micro_batch": mb, "grad_accum": accum, "seq_len": d.L,
                        "parallelism": f"dp{world}"},
             "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
-            "roofline": {"bound": "mfma", "kernel": "gemm_kernel<true,true,4,1> (vlm gate|up GeGLU GEMM)",
+            "roofline": {"bound": "mfma", "kernel": kname + " (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS, "traffic": None},

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 1
+#define PZ_ABI_VERSION 2
 
 enum {
   PZ_OK = 0,
@@ -61,8 +61,15 @@ typedef struct pz_gemm_args {
   const void* resid; int64_t ld_resid; /* bf16, may alias C */
   void* aux; int64_t ld_aux;           /* bf16 saved pre-activations or NULL */
   int64_t geglu_inter;                 /* I for PZ_EPI_GEGLU */
+  /* optional fp32 scratch (caller-owned, 16-byte aligned): when a batch-1 GEMM has too few
+   * output tiles to fill the chip (prefill at B=1) and ws_bytes allows, K is split over
+   * workgroups into fp32 slabs and a second kernel sums them and applies the epilogue.
+   * NULL / 0 disables the split.  Deterministic (no atomics). */
+  void* workspace; int64_t ws_bytes;
 } pz_gemm_args;
 int pz_gemm(const pz_gemm_args* args, void* stream);
+/* name of the kernel pz_gemm would launch for args (profiling / bench labels); never fails */
+const char* pz_gemm_kernel_name(const pz_gemm_args* args);
 
 /* strided fp32-accumulate GEMM for the K=7 / N=7 linears (pizero.py:94-103, vla/modules.py:44):
  * C[m*ldc+n] (+)= alpha*sum_k A[m*sAm+k*sAk]*B[k*sBk+n*sBn] (+bias[n]); bf16 in/out */

@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "pz_common.h"
 
 namespace {
@@ -37,6 +39,9 @@ struct GemmP {
   int64_t batch_inner, sAo, sAi, sBo, sBi, sCo, sCi, sRo, sRi;
   int tiles_m, tiles_n, epi, c_fp32, beta;
   float alpha;
+  // split-K (batch-1 only): blockIdx.y = split index; raw fp32 partials -> ws[z][M][ldw]
+  float* ws;
+  int64_t ksplit, ldw;
 };
 
 __device__ __forceinline__ int sw_tr(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
@@ -231,11 +236,14 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   int tm, tn;
   tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
   const int64_t z = blockIdx.y;
-  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bool split = p.ksplit > 0;
+  const int64_t zo = split ? 0 : z / p.batch_inner, zi = split ? 0 : z % p.batch_inner;
   const bf16_t* A = p.A + zo * p.sAo + zi * p.sAi;
   const bf16_t* B = p.B + zo * p.sBo + zi * p.sBi;
   const int64_t m0 = (int64_t)tm * BM;
   const int64_t n0 = geglu ? (int64_t)tn * (BN / 2) : (int64_t)tn * BN;
+  const int64_t kbeg = split ? z * p.ksplit : 0;
+  const int64_t kend = split ? min(p.K, kbeg + p.ksplit) : p.K;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -246,10 +254,10 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (int)((p.K + BK - 1) / BK);
+  const int nk = (int)((kend - kbeg + BK - 1) / BK);
   u32x4 ra[4], rb[4];
-  g2r<AKC>(ra, A, p.lda, m0, p.M, 0, p.K, false, 0);
-  g2r<BKC>(rb, B, p.ldb, n0, p.N, 0, p.K, geglu, p.geglu_I);
+  g2r<AKC>(ra, A, p.lda, m0, p.M, kbeg, kend, false, 0);
+  g2r<BKC>(rb, B, p.ldb, n0, p.N, kbeg, kend, geglu, p.geglu_I);
   r2s<AKC>(ra, sA);
   r2s<BKC>(rb, sB);
   __syncthreads();
@@ -258,8 +266,8 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      g2r<AKC>(ra, A, p.lda, m0, p.M, (int64_t)(kt + 1) * BK, p.K, false, 0);
-      g2r<BKC>(rb, B, p.ldb, n0, p.N, (int64_t)(kt + 1) * BK, p.K, geglu, p.geglu_I);
+      g2r<AKC>(ra, A, p.lda, m0, p.M, kbeg + (int64_t)(kt + 1) * BK, kend, false, 0);
+      g2r<BKC>(rb, B, p.ldb, n0, p.N, kbeg + (int64_t)(kt + 1) * BK, kend, geglu, p.geglu_I);
     }
     const char* a_img = sA + cur * TILE_BYTES;
     const char* b_img = sB + cur * TILE_BYTES;
@@ -284,6 +292,29 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
   }
 
   // ---------------------------------------------------------------- epilogue
+  if (split) {
+    // raw partial sums; GEGLU keeps the [gate | up] column layout of B (cols n, I + n)
+    float* W = p.ws + z * p.M * p.ldw;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        int64_t n;
+        if (geglu) {
+          const int64_t nl = n0 + (j % (NI / 2)) * 16 + 4 * (lane >> 4);
+          if (nl >= p.geglu_I) continue;
+          n = j < NI / 2 ? nl : p.geglu_I + nl;
+        } else {
+          n = n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4);
+          if (n >= p.N) continue;
+        }
+        *reinterpret_cast<f32x4*>(W + m * p.ldw + n) = acc[i][j];
+      }
+    }
+    return;
+  }
   const int64_t cofs = zo * p.sCo + zi * p.sCi;
   const int64_t rofs = zo * p.sRo + zi * p.sRi;
   if (geglu) {
@@ -303,6 +334,27 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j)
       store_out4(p, cofs, rofs, m, n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4), acc[i][j]);
+  }
+}
+
+// split-K second pass: C = epilogue(sum_z ws[z]) -- one thread per (row, 4 columns)
+__global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmP p, int S) {
+  const bool geglu = p.epi == PZ_EPI_GEGLU;
+  const int64_t ncols = geglu ? p.geglu_I : p.N;
+  const int64_t groups = (ncols + 3) / 4;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= p.M * groups) return;
+  const int64_t m = idx / groups, n = (idx - m * groups) * 4;
+  const float* W = p.ws + m * p.ldw + n;
+  const int64_t slab = p.M * p.ldw;
+  f32x4 s = *reinterpret_cast<const f32x4*>(W);
+  for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(W + z * slab);
+  if (geglu) {
+    f32x4 u = *reinterpret_cast<const f32x4*>(W + p.geglu_I);
+    for (int z = 1; z < S; ++z) u += *reinterpret_cast<const f32x4*>(W + z * slab + p.geglu_I);
+    store_geglu4(p, 0, m, n, s, u);
+  } else {
+    store_out4(p, 0, 0, m, n, s);
   }
 }
 
@@ -500,12 +552,15 @@ constexpr int BK256 = 64;  // dispatched K-tile of the 256 kernel (see above)
 
 // -------------------------------------------------------------------------
 // Skinny GEMM for M <= 16 (inference denoise steps, B = 1..4): weights are
-// streamed once straight into VGPRs (no LDS), one wave per 16 output columns,
-// K split across the 4 waves of a block and reduced through LDS.  Operand A
-// must be k-contiguous, B k-contiguous (nn.Linear weight layout).
+// streamed once straight into VGPRs (no LDS), a block of W waves per 16 output
+// columns, K split into W contiguous ranges (one per wave, loads issued 8 / 4
+// chunks ahead of their MFMAs so each lane keeps up to 8 x 16 B of weights in
+// flight) and reduced through LDS.  W = 4/8/16 by K so every wave has >= 4
+// chunks of 32.  Operands k-contiguous (nn.Linear weight layout).
 // -------------------------------------------------------------------------
-constexpr int SK_WAVES = 4;
-__global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmP p) {
+template <int W>
+__global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
+  constexpr int SK_WAVES = W;
   __shared__ f32x4 red[SK_WAVES][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool geglu = p.epi == PZ_EPI_GEGLU;
@@ -523,16 +578,29 @@ __global__ void __launch_bounds__(256) gemm_skinny_kernel(GemmP p) {
   const bf16_t* Arow = A + m * p.lda + 8 * (lane >> 4);
   const bf16_t* Brow = B + nr * p.ldb + 8 * (lane >> 4);
   const bf16_t* Brow2 = B + (p.geglu_I + nr) * p.ldb + 8 * (lane >> 4);
-  for (int64_t kc = wave; kc < kchunks; kc += SK_WAVES) {
-    bf16x8 a = {}, b = {}, b2 = {};
-    if (mok) a = *reinterpret_cast<const bf16x8*>(Arow + kc * 32);
-    if (nok) b = *reinterpret_cast<const bf16x8*>(Brow + kc * 32);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc, 0, 0, 0);
-    if (geglu) {
-      if (nok) b2 = *reinterpret_cast<const bf16x8*>(Brow2 + kc * 32);
-      acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2, a, acc2, 0, 0, 0);
+  const int64_t per = (kchunks + SK_WAVES - 1) / SK_WAVES;
+  const int64_t kb = wave * per, ke = min(kchunks, kb + per);
+  int64_t kc = kb;
+  auto run = [&](auto U_) {
+    constexpr int U = decltype(U_)::value;
+    for (; kc + U <= ke; kc += U) {
+      bf16x8 a[U], b[U], b2[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        a[u] = mok ? *reinterpret_cast<const bf16x8*>(Arow + (kc + u) * 32) : bf16x8{};
+        b[u] = nok ? *reinterpret_cast<const bf16x8*>(Brow + (kc + u) * 32) : bf16x8{};
+        if (geglu) b2[u] = nok ? *reinterpret_cast<const bf16x8*>(Brow2 + (kc + u) * 32) : bf16x8{};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u], a[u], acc, 0, 0, 0);
+        if (geglu) acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[u], a[u], acc2, 0, 0, 0);
+      }
     }
-  }
+  };
+  run(std::integral_constant<int, 8>{});
+  run(std::integral_constant<int, 4>{});
+  run(std::integral_constant<int, 1>{});
   // D[n_local = 4*(lane>>4)+r][m = lane&15]
   red[wave][lane] = acc;
   __syncthreads();
@@ -649,6 +717,111 @@ static int launch256(const GemmP& p, int64_t batch, hipStream_t st) {
   return PZ_OK;
 }
 
+namespace {
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT };
+struct Plan {
+  PathKind kind;
+  bool akc, bkc, geglu;
+  int wm, tag, skinny_w, splits;
+  int64_t ksplit, ldw, tiles_m, tiles_n;
+};
+
+// Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
+Plan make_plan(const pz_gemm_args* a) {
+  Plan pl{};
+  pl.akc = a->a_kcontig != 0;
+  pl.bkc = a->b_kcontig != 0;
+  pl.geglu = a->epilogue == PZ_EPI_GEGLU;
+  const int64_t ncols = pl.geglu ? a->geglu_inter : a->N;
+  // skinny path: few rows, weights streamed once (inference denoise / proprio rows)
+  if (a->M <= 16 && pl.akc && pl.bkc && a->K % 32 == 0 && !a->c_fp32) {
+    const int64_t kch = a->K / 32;
+    pl.kind = PATH_SKINNY;
+    pl.skinny_w = kch >= 64 ? 16 : (kch >= 32 ? 8 : 4);
+    pl.tiles_n = (ncols + 15) / 16;
+    return pl;
+  }
+  const int64_t cw = pl.geglu ? BT / 2 : BT;
+  if (a->K % BK256 == 0 && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512) &&
+      a->batch * ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) >= 160) {
+    pl.kind = PATH_256;
+    pl.tiles_m = (a->M + BT - 1) / BT;
+    pl.tiles_n = (ncols + cw - 1) / cw;
+    return pl;
+  }
+  pl.kind = PATH_TILE;
+  pl.tiles_m = (a->M + BM - 1) / BM;
+  pl.tiles_n = (ncols + (pl.geglu ? BN / 2 : BN) - 1) / (pl.geglu ? BN / 2 : BN);
+  pl.wm = pl.geglu ? 4 : 2;
+  pl.tag = (pl.geglu && pl.akc && a->M >= 2048) ? 1 : 0;
+  // split-K when one 128x128 tile per WG leaves most of the 256 CUs idle
+  const int64_t tiles = pl.tiles_m * pl.tiles_n;
+  const int64_t nk = (a->K + BK - 1) / BK;
+  if (a->batch == 1 && a->workspace && tiles < 120 && nk >= 4) {
+    int64_t S = (240 + tiles - 1) / tiles;
+    S = S < 16 ? S : 16;
+    S = S < nk / 2 ? S : nk / 2;
+    if (S >= 2) {
+      const int64_t ks = ((nk + S - 1) / S) * BK;
+      const int64_t Se = (a->K + ks - 1) / ks;
+      const int64_t ldw = pl.geglu ? 2 * a->geglu_inter : (a->N + 3) / 4 * 4;
+      if (Se >= 2 && Se * a->M * ldw * 4 <= a->ws_bytes && PZ_ALIGNED(a->workspace, 16)) {
+        pl.kind = PATH_SPLIT;
+        pl.splits = (int)Se;
+        pl.ksplit = ks;
+        pl.ldw = ldw;
+      }
+    }
+  }
+  return pl;
+}
+
+const char* bstr(bool b) { return b ? "true" : "false"; }
+}  // namespace
+
+extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
+  static thread_local char buf[160];
+  if (!a) return "";
+  const Plan pl = make_plan(a);
+  switch (pl.kind) {
+    case PATH_SKINNY:
+      snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d>", pl.skinny_w);
+      break;
+    case PATH_256:
+      snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
+               BK256);
+      break;
+    case PATH_TILE:
+      snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
+      break;
+    case PATH_SPLIT:
+      snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
+               bstr(pl.bkc), pl.wm, pl.tag, pl.splits);
+      break;
+  }
+  return buf;
+}
+
+template <int W>
+static int launch_skinny(const GemmP& p, int64_t tiles_n, int64_t batch, hipStream_t st) {
+  hipLaunchKernelGGL(gemm_skinny_kernel<W>, dim3((unsigned)tiles_n, (unsigned)batch), dim3(W * 64), 0, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+template <bool AKC, bool BKC, int WM, int TAG>
+static int launch_tile_any(GemmP& p, const Plan& pl, int64_t batch, hipStream_t st) {
+  if (pl.kind != PATH_SPLIT) return launch_tile<AKC, BKC, WM, TAG>(p, batch, st);
+  int rc = launch_tile<AKC, BKC, WM, TAG>(p, pl.splits, st);
+  if (rc != PZ_OK) return rc;
+  const int64_t ncols = pl.geglu ? p.geglu_I : p.N;
+  const int64_t work = p.M * ((ncols + 3) / 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, p,
+                     pl.splits);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
 extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   PZ_CHECK_ARG(a != nullptr, "pz_gemm: null args");
   PZ_CHECK_ARG(a->M > 0 && a->N > 0 && a->K > 0, "pz_gemm: bad dims M=%lld N=%lld K=%lld",
@@ -675,8 +848,10 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   if (a->epilogue == PZ_EPI_GELU || a->epilogue == PZ_EPI_SILU)
     PZ_CHECK_ARG(a->batch == 1, "pz_gemm: activation epilogue is unbatched");
   if (a->aux) PZ_CHECK_ARG(a->ld_aux % 4 == 0 && PZ_ALIGNED(a->aux, 8), "pz_gemm: aux alignment");
+  PZ_CHECK_ARG(a->ws_bytes >= 0, "pz_gemm: negative ws_bytes");
 
   GemmP p;
+  memset(&p, 0, sizeof(p));
   p.A = (const bf16_t*)a->A;
   p.B = (const bf16_t*)a->B;
   p.C = a->C;
@@ -697,19 +872,17 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.alpha = a->alpha;
   hipStream_t st = (hipStream_t)stream;
 
-  const int64_t ncols = geglu ? a->geglu_inter : a->N;
-  // skinny path: few rows, weights streamed once (inference denoise / proprio rows)
-  if (a->M <= 16 && a->a_kcontig && a->b_kcontig && a->K % 32 == 0 && !a->c_fp32 &&
-      PZ_ALIGNED(a->A, 16) && a->lda % 8 == 0) {
-    dim3 grid((unsigned)((ncols + 15) / 16), (unsigned)a->batch);
-    hipLaunchKernelGGL(gemm_skinny_kernel, grid, dim3(256), 0, st, p);
-    PZ_CHECK_LAUNCH();
-    return PZ_OK;
+  const Plan pl = make_plan(a);
+  if (pl.kind == PATH_SKINNY) {
+    PZ_CHECK_ARG(a->batch < 65536, "pz_gemm: batch too large");
+    if (pl.skinny_w == 16) return launch_skinny<16>(p, pl.tiles_n, a->batch, st);
+    if (pl.skinny_w == 8) return launch_skinny<8>(p, pl.tiles_n, a->batch, st);
+    return launch_skinny<4>(p, pl.tiles_n, a->batch, st);
   }
-  if (a->K % BK256 == 0 && a->M >= 512 && ncols >= (geglu ? 256 : 512) &&
-      a->batch * ((a->M + BT - 1) / BT) * ((ncols + (geglu ? BT / 2 : BT) - 1) / (geglu ? BT / 2 : BT)) >= 160) {
-    p.tiles_m = (int)((a->M + BT - 1) / BT);
-    p.tiles_n = (int)((ncols + (geglu ? BT / 2 : BT) - 1) / (geglu ? BT / 2 : BT));
+  p.tiles_m = (int)pl.tiles_m;
+  p.tiles_n = (int)pl.tiles_n;
+  PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
+  if (pl.kind == PATH_256) {
     if (geglu) {
       if (a->a_kcontig) return launch256<true, true, true>(p, a->batch, st);
       return launch256<false, true, true>(p, a->batch, st);
@@ -719,18 +892,20 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
     if (!a->a_kcontig && a->b_kcontig) return launch256<false, true, false>(p, a->batch, st);
     return launch256<false, false, false>(p, a->batch, st);
   }
-  p.tiles_m = (int)((a->M + BM - 1) / BM);
-  p.tiles_n = (int)((ncols + (geglu ? BN / 2 : BN) - 1) / (geglu ? BN / 2 : BN));
-  PZ_CHECK_ARG((int64_t)p.tiles_m * p.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
-  if (geglu) {
-    if (a->a_kcontig && a->M >= 2048) return launch_tile<true, true, 4, 1>(p, a->batch, st);
-    if (a->a_kcontig) return launch_tile<true, true, 4>(p, a->batch, st);
-    return launch_tile<false, true, 4>(p, a->batch, st);
+  if (pl.kind == PATH_SPLIT) {
+    p.ws = (float*)a->workspace;
+    p.ksplit = pl.ksplit;
+    p.ldw = pl.ldw;
   }
-  if (a->a_kcontig && a->b_kcontig) return launch_tile<true, true, 2>(p, a->batch, st);
-  if (a->a_kcontig && !a->b_kcontig) return launch_tile<true, false, 2>(p, a->batch, st);
-  if (!a->a_kcontig && a->b_kcontig) return launch_tile<false, true, 2>(p, a->batch, st);
-  return launch_tile<false, false, 2>(p, a->batch, st);
+  if (geglu) {
+    if (pl.tag) return launch_tile_any<true, true, 4, 1>(p, pl, a->batch, st);
+    if (a->a_kcontig) return launch_tile_any<true, true, 4, 0>(p, pl, a->batch, st);
+    return launch_tile_any<false, true, 4, 0>(p, pl, a->batch, st);
+  }
+  if (a->a_kcontig && a->b_kcontig) return launch_tile_any<true, true, 2, 0>(p, pl, a->batch, st);
+  if (a->a_kcontig && !a->b_kcontig) return launch_tile_any<true, false, 2, 0>(p, pl, a->batch, st);
+  if (!a->a_kcontig && a->b_kcontig) return launch_tile_any<false, true, 2, 0>(p, pl, a->batch, st);
+  return launch_tile_any<false, false, 2, 0>(p, pl, a->batch, st);
 }
 
 extern "C" int pz_gemm_small(const pz_small_gemm_args* a, void* stream) {

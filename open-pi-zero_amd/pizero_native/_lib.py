@@ -12,6 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
+ABI_VERSION = 2  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 
 i64, i32, f32, vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
@@ -30,6 +31,7 @@ class GemmArgs(C.Structure):
         ("epilogue", i32), ("alpha", f32), ("beta_accum", i32),
         ("bias", vp), ("resid", vp), ("ld_resid", i64), ("aux", vp), ("ld_aux", i64),
         ("geglu_inter", i64),
+        ("workspace", vp), ("ws_bytes", i64),
     ]
 
 
@@ -55,6 +57,7 @@ class SoftmaxArgs(C.Structure):
 # name -> argtypes (restype int unless listed in _RESTYPE)
 SIGNATURES = {
     "pz_gemm": [C.POINTER(GemmArgs), vp],
+    "pz_gemm_kernel_name": [C.POINTER(GemmArgs)],
     "pz_gemm_small": [C.POINTER(SmallGemmArgs), vp],
     "pz_rmsnorm_fwd": [vp, i64, vp, vp, i64, vp, i64, i64, f32, vp],
     "pz_rmsnorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, i64, vp],
@@ -91,7 +94,7 @@ SIGNATURES = {
     "pz_last_error": [],
     "pz_abi_version": [],
 }
-_RESTYPE = {"pz_last_error": C.c_char_p, "pz_norm_rows_per_part": i64}
+_RESTYPE = {"pz_last_error": C.c_char_p, "pz_gemm_kernel_name": C.c_char_p, "pz_norm_rows_per_part": i64}
 
 _lib = None
 
@@ -113,6 +116,8 @@ def lib():
             fn = getattr(L, name)
             fn.argtypes = argt
             fn.restype = _RESTYPE.get(name, C.c_int)
+        if L.pz_abi_version() != ABI_VERSION:
+            raise NativeError(f"{LIB_PATH}: ABI version {L.pz_abi_version()} != {ABI_VERSION}; rebuild it")
         _lib = L
     return _lib
 

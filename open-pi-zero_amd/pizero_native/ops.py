@@ -20,6 +20,7 @@ from ._lib import (
     SmallGemmArgs,
     SoftmaxArgs,
     call,
+    lib,
 )
 
 __all__ = ["PZ_EPI_NONE", "PZ_EPI_GELU", "PZ_EPI_GEGLU", "PZ_EPI_SILU"]
@@ -62,8 +63,23 @@ def gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, *, epi=PZ_EPI_NONE, alpha
           geglu_inter, batch, batch_inner, sA, sB, sC, sR)
 
 
-def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-          geglu_inter, batch, batch_inner, sA, sB, sC, sR):
+_WS_BYTES = 64 << 20
+_WS = {}
+
+
+def workspace(device=None):
+    """Per-device fp32 split-K scratch for pz_gemm (allocated once, before any graph capture
+    reuses it; GEMMs are stream-ordered on the main stream, so one buffer is enough)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    ws = _WS.get(dev)
+    if ws is None:
+        ws = torch.empty(_WS_BYTES // 4, dtype=torch.float32, device=dev)
+        _WS[dev] = ws
+    return ws
+
+
+def _args(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws=None):
     a = GemmArgs()
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.A, a.lda, a.a_kcontig = _p(A), int(lda), int(bool(a_kc))
@@ -77,7 +93,28 @@ def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, 
     a.epilogue, a.alpha, a.beta_accum = int(epi), float(alpha), int(bool(beta))
     a.bias, a.resid, a.ld_resid = _p(bias), _p(resid), int(ld_resid)
     a.aux, a.ld_aux, a.geglu_inter = _p(aux), int(ld_aux), int(geglu_inter)
+    if ws is not None:
+        a.workspace, a.ws_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
+    return a
+
+
+def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR):
+    ws = workspace(Cm.device) if batch == 1 else None
+    a = _args(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
+              geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws)
     call("pz_gemm", C.byref(a), _st())
+
+
+def gemm_kernel_name(M, N, K, *, a_kc=True, b_kc=True, epi=PZ_EPI_NONE, geglu_inter=0, batch=1, c_fp32=False,
+                     workspace_bytes=_WS_BYTES):
+    """Name of the kernel pz_gemm dispatches for this problem (bench / profile labels)."""
+    a = GemmArgs()
+    a.M, a.N, a.K = int(M), int(N), int(K)
+    a.a_kcontig, a.b_kcontig, a.c_fp32 = int(a_kc), int(b_kc), int(c_fp32)
+    a.batch, a.batch_inner, a.epilogue, a.geglu_inter = int(batch), 1, int(epi), int(geglu_inter)
+    a.workspace, a.ws_bytes = (256 if workspace_bytes else None), int(workspace_bytes)
+    return lib().pz_gemm_kernel_name(C.byref(a)).decode()
 
 
 def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha=1.0, beta=False):

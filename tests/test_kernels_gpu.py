@@ -148,6 +148,48 @@ def test_epilogues_gelu_resid_geglu_silu():
     close(o, torch.nn.functional.silu(p))
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 1152, 4304), (276, 2048, 16384), (100, 300, 1024), (276, 2560, 2048)])
+def test_split_k_forward_epilogues(M, N, K):
+    """Few-tile batch-1 GEMMs (B=1 prefill) run split-K + epilogue pass; same results as one pass."""
+    from pizero_native import ops
+
+    assert "splitk" in ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GELU)
+    x, W, b, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(N), bf(M, N)
+    ref = x.float() @ W.float().t() + b.float()
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, out, bias=b, resid=r)
+    close(out, ref + r.float(), atol=2e-2)
+    ops.linear(x, W, out, bias=b, epi=ops.PZ_EPI_GELU, aux=pre)
+    close(pre, ref)
+    close(out, torch.nn.functional.gelu(ref, approximate="tanh"))
+    out32 = torch.ones(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(M, N, K, x, K, True, W, K, True, out32, N, beta=True)
+    close(out32, 1.0 + x.float() @ W.float().t(), rtol=1e-3, atol=1e-3)
+    I = N // 2 // 4 * 4
+    if I * 2 == N:
+        h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+        gu = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        assert "splitk" in ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I)
+        ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+        raw = x.float() @ W.float().t()
+        close(gu, raw)
+        close(h, torch.nn.functional.gelu(raw[:, :I], approximate="tanh") * raw[:, I:])
+
+
+@pytest.mark.parametrize("K", [96, 1024, 2048, 4096, 4128])
+def test_skinny_widths(K):
+    """M <= 16 rows: W = 4/8/16 waves per block, 8/4/1-chunk unroll tails."""
+    from pizero_native import ops
+
+    for M in (1, 4, 16):
+        x, W, b = bf(M, K), bf(1040, K, scale=K ** -0.5), bf(1040)
+        out = torch.empty(M, 1040, device=dev, dtype=torch.bfloat16)
+        assert "skinny" in ops.gemm_kernel_name(M, 1040, K)
+        ops.linear(x, W, out, bias=b)
+        close(out, x.float() @ W.float().t() + b.float())
+
+
 def test_small_gemm():
     from pizero_native import ops
 

@@ -265,6 +265,7 @@ def main():
             "inference": infer,
             "cpu_baseline": cpu,
             "loss_mean": float(loss_acc.item()) / (accum * args.steps * max(1, world)),
+            "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else None,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -17,6 +17,7 @@
 // owns 4 consecutive output columns -> vectorised epilogue stores.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <type_traits>
@@ -551,6 +552,282 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmP p) {
 constexpr int BK256 = 64;  // dispatched K-tile of the 256 kernel (see above)
 
 // -------------------------------------------------------------------------
+// 256x256x64 "8-phase" ping-pong GEMM (the dispatched large-GEMM kernel).
+//
+// 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave (acc[8][4], 128 AGPR/VGPR).
+// Each 64-deep K-tile is consumed in 4 phases of 16 MFMAs, one output quadrant
+// (64 rows x 32 cols) per phase, order (0,0) (0,1) (1,1) (1,0) so fragments are
+// read once per K-tile: phase 0 reads A-lo + B-lo, 1 reads B-hi, 2 reads A-hi,
+// 3 reads nothing.  Every phase = [issue one LDS-DMA piece, ds_reads, counted
+// vmcnt, lgkmcnt(0)] barrier [16 MFMA at setprio 1] barrier.  The M-row-1 wave
+// group runs one barrier behind the row-0 group, so on every SIMD (waves w and
+// w+4) one wave's MFMAs overlap the other's LDS reads / DMA issue.
+//
+// LDS: two K-tile buffers of 64 KiB, each = 4 regions of 16 KiB:
+//   A region 0 (rows with (r % 128) < 64), A region 1 (the other 128 rows),
+//   B region 0 (virtual cols 0..127), B region 1 (cols 128..255).
+// A region is free as soon as the phase that last reads it has ended, so the
+// next-but-one K-tile streams in piece by piece: tile kt issues A1(kt+1) in
+// phase 0 and A0/B0/B1(kt+2) in phases 1-3; 4-5 pieces (64-80 KiB) stay in
+// flight and the counted waits (vmcnt 8 / 10) never drain the DMA queue in
+// steady state.  Hazards (one barrier per phase boundary, stagger included):
+// a piece is waited for (vmcnt, issuing waves) in a phase strictly before the
+// phase that reads it; a region is restaged >= 1 phase after its last read,
+// whose lgkmcnt(0) precedes that phase's first barrier.
+// -------------------------------------------------------------------------
+constexpr int P8_BUF = 65536, P8_REG = 16384;
+
+// global row of region-row rr (0..127) of an operand region; B may be the GeGLU [gate; up] stack
+template <bool ISA, bool GEGLU>
+__device__ __forceinline__ int64_t p8_row(int region, int rr, int64_t row0, int64_t R, int64_t gI) {
+  if (ISA) {
+    const int64_t g = row0 + (rr >> 6) * 128 + region * 64 + (rr & 63);
+    return g < R ? g : R - 1;
+  } else if (GEGLU) {
+    const int v = region * 128 + rr;  // virtual column: wave (v >> 6), gate/up (v >> 5 & 1)
+    int64_t g = row0 + (v >> 6) * 32 + (v & 31);
+    g = g < gI ? g : gI - 1;
+    return ((v >> 5) & 1) ? gI + g : g;
+  } else {
+    const int64_t g = row0 + region * 128 + rr;
+    return g < R ? g : R - 1;
+  }
+}
+
+// per-thread global source of DMA instruction i (0/1) of a region image
+template <bool KC, bool ISA, bool GEGLU>
+__device__ __forceinline__ const bf16_t* p8_src(const bf16_t* base, int64_t ld, int region, int i, int t,
+                                                int64_t row0, int64_t R, int64_t gI) {
+  if (KC) {  // image [128 rows][64 k], 128-B rows, chunk ch of row r at ch ^ ((r >> 1) & 7)
+    const int r = i * 64 + (t >> 3);
+    const int ch = (t & 7) ^ ((r >> 1) & 7);
+    return base + p8_row<ISA, GEGLU>(region, r, row0, R, gI) * ld + 8 * ch;
+  } else {  // whole-operand image [64 k][256 rows], 512-B rows; "region" r = k-rows 32r..32r+31;
+            // 16-B chunk c of k-row k at c ^ (sw_tr(k) >> 1) (as the 2-stage kernel's image)
+    const int k = region * 32 + i * 16 + (t >> 5);
+    const int c = (t & 31) ^ (sw_tr(k) >> 1);
+    int64_t g = row0 + 8 * c;  // first of 8 consecutive tile rows
+    g = g <= R - 8 ? g : R - 8;
+    return base + (int64_t)k * ld + g;
+  }
+}
+
+// k-strided fragment through inline-asm ds_read_b64_tr_b16.  With the builtin, hipcc cannot
+// tell the read from the in-flight LDS-DMA writes and drains the DMA queue (s_waitcnt vmcnt(0))
+// before every transposed read, which serialises the 8-phase pipeline.  The asm result is NOT
+// tracked by the compiler's lgkmcnt: callers wait lgkmcnt(0) (PZ_WAIT_LGKM0) before any use,
+// and a sched_barrier keeps the consuming MFMAs behind that wait.
+__device__ __forceinline__ s16x4 ds_tr_asm(const char* p) {
+  s16x4 v;
+  const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
+template <int TRROW>
+__device__ __forceinline__ bf16x8 frag_tr_asm(const char* lds, int rb, int kk, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  s16x8 out;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = kk * 32 + 8 * (lane >> 4) + 4 * t + q;
+    const s16x4 v = ds_tr_asm(lds + k * TRROW + (((4 * rb + p) ^ sw_tr(k)) << 3));
+    out[4 * t + 0] = v[0];
+    out[4 * t + 1] = v[1];
+    out[4 * t + 2] = v[2];
+    out[4 * t + 3] = v[3];
+  }
+  return __builtin_bit_cast(bf16x8, out);
+}
+
+#define PZ_SCHED() __builtin_amdgcn_sched_barrier(0)
+#define PZ_RAW_BARRIER()           \
+  do {                             \
+    PZ_SCHED();                    \
+    __builtin_amdgcn_s_barrier();  \
+    PZ_SCHED();                    \
+  } while (0)
+#define PZ_WAIT_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+
+template <bool AKC, bool BKC, bool GEGLU>
+__global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int64_t m0 = (int64_t)tm * BT;
+  const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t z = blockIdx.y;
+  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bf16_t* Ab = p.A + zo * p.sAo + zi * p.sAi;
+  const bf16_t* Bb = p.B + zo * p.sBo + zi * p.sBi;
+
+  // pieces: 0 = A region 0, 1 = B region 0, 2 = B region 1, 3 = A region 1
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    src[0][i] = p8_src<AKC, true, false>(Ab, p.lda, 0, i, t, m0, p.M, 0);
+    src[3][i] = p8_src<AKC, true, false>(Ab, p.lda, 1, i, t, m0, p.M, 0);
+    src[1][i] = p8_src<BKC, false, GEGLU>(Bb, p.ldb, 0, i, t, n0, p.N, p.geglu_I);
+    src[2][i] = p8_src<BKC, false, GEGLU>(Bb, p.ldb, 1, i, t, n0, p.N, p.geglu_I);
+  }
+  const int64_t stepA = AKC ? 64 : 64 * p.lda;
+  const int64_t stepB = BKC ? 64 : 64 * p.ldb;
+  constexpr int lds_off[4] = {0, 2 * P8_REG, 3 * P8_REG, P8_REG};
+  auto issue = [&](int piece, int kt) {
+    char* dst = smem + (kt & 1) * P8_BUF + lds_off[piece] + wave * 1024;
+    const int64_t step = (piece == 0 || piece == 3) ? stepA : stepB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) glds16(src[piece][i] + kt * step, dst + i * 8192);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bf[2][2][2];  // A quadrant rows (4 x 16) x kk;  B [bh][2 x 16 cols][kk]
+
+  auto read_a = [&](const char* buf, int ah) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        af[i][kk] = AKC ? frag<true>(buf + ah * P8_REG, wr * 4 + i, kk, lane)
+                        : frag_tr_asm<512>(buf, wr * 8 + ah * 4 + i, kk, lane);
+  };
+  auto read_b = [&](const char* buf, int bh) {
+    const char* reg = buf + 2 * P8_REG + (wc >> 1) * P8_REG;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        bf[bh][j][kk] = BKC ? frag<true>(reg, (wc & 1) * 4 + bh * 2 + j, kk, lane)
+                            : frag_tr_asm<512>(buf + 2 * P8_REG, wc * 4 + bh * 2 + j, kk, lane);
+  };
+  auto mfma_quad = [&](int ah, int bh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ah * 4 + i][bh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[bh][j][kk], af[i][kk], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // Per-operand schedule.  k-contiguous operands stream region by region as soon as each is
+  // free (A: A1(kt+1) in phase 0, A0(kt+2) in phase 1; B: B0 in 2, B1 in 3); k-strided ones
+  // load both regions together (B in phase 2, A in phase 3) so every k-row's 512-B span is
+  // fetched by back-to-back instructions.  vmcnt counts (pieces of 2 DMA instructions issued
+  // after the one a wait retires) are the same for all four combinations: 5 / 4 at phase 1
+  // (A split only), 4 at phase 3; tails retire everything.
+  constexpr bool AS = AKC, BS = BKC;
+  const int nk = (int)(p.K / 64);
+  if (AS) {
+    issue(0, 0);
+    issue(1, 0);
+    issue(2, 0);
+    issue(3, 0);
+    if (nk > 1) {
+      issue(0, 1);
+      issue(1, 1);
+      issue(2, 1);
+      PZ_WAIT_VM(8);
+    } else {
+      PZ_WAIT_VM(2);
+    }
+  } else {
+    issue(1, 0);
+    issue(2, 0);
+    issue(0, 0);
+    issue(3, 0);
+    if (nk > 1) {
+      issue(1, 1);
+      issue(2, 1);
+      issue(0, 1);
+      issue(3, 1);
+      PZ_WAIT_VM(8);
+    } else {
+      PZ_WAIT_VM(0);
+    }
+  }
+  PZ_RAW_BARRIER();
+  if (wr == 1) PZ_RAW_BARRIER();  // stagger: row-1 waves run one barrier behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = smem + (kt & 1) * P8_BUF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // phase 0: quadrant (0,0)
+    if (AS && n1) issue(3, kt + 1);
+    read_a(buf, 0);
+    read_b(buf, 0);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mfma_quad(0, 0);
+    PZ_RAW_BARRIER();
+    // phase 1: quadrant (0,1); (A split) retire A region 1 of this tile for phase 2
+    if (AS && n2) issue(0, kt + 2);
+    read_b(buf, 1);
+    if (AS) {
+      if (n2) PZ_WAIT_VM(10);
+      else if (n1) PZ_WAIT_VM(8);
+      else PZ_WAIT_VM(0);
+    }
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mfma_quad(0, 1);
+    PZ_RAW_BARRIER();
+    // phase 2: quadrant (1,1)
+    if (n2) {
+      issue(1, kt + 2);
+      if (!BS) issue(2, kt + 2);
+    }
+    read_a(buf, 1);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mfma_quad(1, 1);
+    PZ_RAW_BARRIER();
+    // phase 3: quadrant (1,0); retire tile kt+1's phase-0 operands (all of A when merged)
+    if (n2) {
+      if (BS) issue(2, kt + 2);
+      if (!AS) {
+        issue(0, kt + 2);
+        issue(3, kt + 2);
+      }
+    }
+    if (n2) PZ_WAIT_VM(8);
+    else if (n1) {
+      if (AS) PZ_WAIT_VM(2);
+      else PZ_WAIT_VM(0);
+    }
+    PZ_RAW_BARRIER();
+    mfma_quad(1, 0);
+    PZ_RAW_BARRIER();
+  }
+  if (wr == 0) PZ_RAW_BARRIER();
+
+  const int64_t cofs = zo * p.sCo + zi * p.sCi;
+  const int64_t rofs = zo * p.sRo + zi * p.sRi;
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb) {
+    const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
+    if (GEGLU) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + 4 * (lane >> 4), acc[rb][j], acc[rb][2 + j]);
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) store_out4(p, cofs, rofs, m, n0 + wc * 64 + cb * 16 + 4 * (lane >> 4), acc[rb][cb]);
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
 // Skinny GEMM for M <= 16 (inference denoise steps, B = 1..4): weights are
 // streamed once straight into VGPRs (no LDS), a block of W waves per 16 output
 // columns, K split into W contiguous ranges (one per wave, loads issued 8 / 4
@@ -672,6 +949,52 @@ __global__ void gemm_small_kernel(pz_small_gemm_args a) {
   *C = f2bf(s);
 }
 
+// Long-K / tiny-N case (action decoder, pizero.py:100-103: [rows, 1024] x [7, 1024]^T): one wave
+// per output row, lanes split K in 16-B chunks (k-contiguous A and B), butterfly reduction.
+constexpr int SMALL_NMAX = 8;
+__global__ void __launch_bounds__(256) gemm_small_rowwave_kernel(pz_small_gemm_args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t m = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const bf16_t* A = (const bf16_t*)a.A + m * a.sAm;
+  const bf16_t* B = (const bf16_t*)a.B;
+  float s[SMALL_NMAX];
+#pragma unroll
+  for (int n = 0; n < SMALL_NMAX; ++n) s[n] = 0.f;
+  for (int64_t k = 8 * lane; k < a.K; k += 512) {
+    const u32x4 xa = *reinterpret_cast<const u32x4*>(A + k);
+    float x[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[2 * e] = bf2f(xa[e] & 0xffff);
+      x[2 * e + 1] = bf2f(xa[e] >> 16);
+    }
+#pragma unroll
+    for (int n = 0; n < SMALL_NMAX; ++n) {
+      if (n >= a.N) break;
+      const u32x4 wb = *reinterpret_cast<const u32x4*>(B + n * a.sBn + k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[n] += x[2 * e] * bf2f(wb[e] & 0xffff) + x[2 * e + 1] * bf2f(wb[e] >> 16);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < SMALL_NMAX; ++n) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s[n] += __shfl_xor(s[n], off);
+  }
+  if (lane < a.N) {
+    float v = 0.f;
+#pragma unroll
+    for (int n = 0; n < SMALL_NMAX; ++n)
+      if (n == lane) v = s[n];
+    v *= a.alpha;
+    if (a.bias) v += bf2f(((const bf16_t*)a.bias)[lane]);
+    bf16_t* C = (bf16_t*)a.C + m * a.ldc + lane;
+    if (a.beta) v += bf2f(*C);
+    *C = f2bf(v);
+  }
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- host ----
@@ -716,6 +1039,8 @@ static int launch256(const GemmP& p, int64_t batch, hipStream_t st) {
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
+
+static bool use_8phase();
 
 namespace {
 enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT };
@@ -788,8 +1113,11 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d>", pl.skinny_w);
       break;
     case PATH_256:
-      snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
-               BK256);
+      if (use_8phase())
+        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu));
+      else
+        snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
+                 BK256);
       break;
     case PATH_TILE:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
@@ -820,6 +1148,26 @@ static int launch_tile_any(GemmP& p, const Plan& pl, int64_t batch, hipStream_t 
                      pl.splits);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
+}
+
+template <bool AKC, bool BKC, bool GEGLU>
+static int launch8p(const GemmP& p, int64_t batch, hipStream_t st) {
+  const int smem = 2 * P8_BUF;  // 128 KiB
+  auto kern = gemm8p_kernel<AKC, BKC, GEGLU>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n, (unsigned)batch), dim3(NT2), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+// large-GEMM kernel: the 8-phase ping-pong (default) or the 2-stage 256 kernel (PZ_GEMM_BIG=2stage, A/B runs)
+static bool use_8phase() {
+  const char* e = getenv("PZ_GEMM_BIG");  // read per call: A/B runs flip it in-process
+  return !(e && strcmp(e, "2stage") == 0);
 }
 
 extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
@@ -882,6 +1230,16 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
+  if (pl.kind == PATH_256 && use_8phase()) {
+    if (geglu) {
+      if (a->a_kcontig) return launch8p<true, true, true>(p, a->batch, st);
+      return launch8p<false, true, true>(p, a->batch, st);
+    }
+    if (a->a_kcontig && a->b_kcontig) return launch8p<true, true, false>(p, a->batch, st);
+    if (a->a_kcontig && !a->b_kcontig) return launch8p<true, false, false>(p, a->batch, st);
+    if (!a->a_kcontig && a->b_kcontig) return launch8p<false, true, false>(p, a->batch, st);
+    return launch8p<false, false, false>(p, a->batch, st);
+  }
   if (pl.kind == PATH_256) {
     if (geglu) {
       if (a->a_kcontig) return launch256<true, true, true>(p, a->batch, st);
@@ -910,6 +1268,13 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
 
 extern "C" int pz_gemm_small(const pz_small_gemm_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->A && a->B && a->C && a->M > 0 && a->N > 0 && a->K > 0, "pz_gemm_small: bad args");
+  if (a->N <= SMALL_NMAX && a->K >= 256 && a->K % 8 == 0 && a->sAk == 1 && a->sBk == 1 && a->sAm % 8 == 0 &&
+      a->sBn % 8 == 0 && PZ_ALIGNED(a->A, 16) && PZ_ALIGNED(a->B, 16)) {
+    hipLaunchKernelGGL(gemm_small_rowwave_kernel, dim3((unsigned)((a->M + 3) / 4)), dim3(256), 0,
+                       (hipStream_t)stream, *a);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   const int64_t total = a->M * a->N;
   hipLaunchKernelGGL(gemm_small_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, *a);

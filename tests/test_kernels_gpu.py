@@ -197,6 +197,15 @@ def test_small_gemm():
     out = torch.empty(20, 64, device=dev, dtype=torch.bfloat16)
     ops.small_linear(x, W, out, bias=b)
     close(out, x.float() @ W.float().t() + b.float())
+    # long-K, N=7 (action decoder): one wave per row; output rows padded to 8 like the engine's
+    for M, K in ((4, 1024), (257, 1024), (3, 264)):
+        x, W, b = bf(M, K), bf(7, K, scale=K ** -0.5), bf(7)
+        out = torch.zeros(M, 8, device=dev, dtype=torch.bfloat16)
+        ops.small_linear(x, W, out[:, :7], bias=b)
+        close(out[:, :7], x.float() @ W.float().t() + b.float())
+        assert out[:, 7].abs().max().item() == 0
+        ops.small_linear(x, W, out[:, :7], bias=b, beta=True)
+        close(out[:, :7], 2 * (x.float() @ W.float().t() + b.float()), atol=2e-2)
 
 
 @pytest.mark.parametrize("D", [1024, 2048, 64])

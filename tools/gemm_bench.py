@@ -46,27 +46,37 @@ def main():
     args = ap.parse_args()
     dev = "cuda"
     rnd = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)  # noqa: E731
-    print(f"{'shape':16s} {'layout':6s} {'M':>6} {'N':>6} {'K':>6} {'pz TF/s':>9} {'torch TF/s':>10}")
+    print(f"{'shape':16s} {'layout':6s} {'M':>6} {'N':>6} {'K':>6} {'8ph TF/s':>9} {'2stg TF/s':>9} {'torch TF/s':>10}")
+
+    def ab(fn):
+        """time fn under the 8-phase kernel and the 2-stage 256 kernel (pz_gemm reads PZ_GEMM_BIG per call)"""
+        os.environ["PZ_GEMM_BIG"] = "8phase"
+        a = timeit(fn, args.iters)
+        os.environ["PZ_GEMM_BIG"] = "2stage"
+        b = timeit(fn, args.iters)
+        os.environ["PZ_GEMM_BIG"] = "8phase"
+        return a, b
+
     for name, M, N, K in SHAPES:
         fl = 2.0 * M * N * K
         x, w = rnd(M, K), rnd(N, K)
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         if "geglu" in name:
-            t = timeit(lambda: ops.linear(x, w, out[:, : N // 2], epi=ops.PZ_EPI_GEGLU), args.iters)
+            t, t2 = ab(lambda: ops.linear(x, w, out[:, : N // 2], epi=ops.PZ_EPI_GEGLU))
         else:
-            t = timeit(lambda: ops.linear(x, w, out), args.iters)
+            t, t2 = ab(lambda: ops.linear(x, w, out))
         tt = timeit(lambda: torch.matmul(x, w.t()), args.iters)
-        print(f"{name:16s} {'NT':6s} {M:6d} {N:6d} {K:6d} {fl / t / 1e9:9.1f} {fl / tt / 1e9:10.1f}")
+        print(f"{name:16s} {'NT':6s} {M:6d} {N:6d} {K:6d} {fl / t / 1e9:9.1f} {fl / t2 / 1e9:9.1f} {fl / tt / 1e9:10.1f}")
         # dgrad: dx[M,K] = dy[M,N] W[N,K]
         dy = rnd(M, N)
         dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
-        t = timeit(lambda: ops.linear_dgrad(dy, w, dx), args.iters)
+        t, t2 = ab(lambda: ops.linear_dgrad(dy, w, dx))
         tt = timeit(lambda: torch.matmul(dy, w), args.iters)
-        print(f"{name:16s} {'NN':6s} {M:6d} {K:6d} {N:6d} {fl / t / 1e9:9.1f} {fl / tt / 1e9:10.1f}")
+        print(f"{name:16s} {'NN':6s} {M:6d} {K:6d} {N:6d} {fl / t / 1e9:9.1f} {fl / t2 / 1e9:9.1f} {fl / tt / 1e9:10.1f}")
         dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
-        t = timeit(lambda: ops.linear_wgrad(dy, x, dW), args.iters)
+        t, t2 = ab(lambda: ops.linear_wgrad(dy, x, dW))
         tt = timeit(lambda: torch.matmul(dy.t(), x), args.iters)
-        print(f"{name:16s} {'TN':6s} {N:6d} {K:6d} {M:6d} {fl / t / 1e9:9.1f} {fl / tt / 1e9:10.1f}")
+        print(f"{name:16s} {'TN':6s} {N:6d} {K:6d} {M:6d} {fl / t / 1e9:9.1f} {fl / t2 / 1e9:9.1f} {fl / tt / 1e9:10.1f}", flush=True)
         del x, w, out, dy, dx, dW
         torch.cuda.empty_cache()
 

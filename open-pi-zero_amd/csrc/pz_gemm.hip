@@ -676,11 +676,31 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   const int64_t stepA = AKC ? 64 : 64 * p.lda;
   const int64_t stepB = BKC ? 64 : 64 * p.ldb;
   constexpr int lds_off[4] = {0, 2 * P8_REG, 3 * P8_REG, P8_REG};
+  // K % 64 != 0: the last K-tile has krem valid k; every lane's source is clamped into the
+  // tensor (finite data) and the A fragments of k >= krem are zeroed before the MFMAs.
+  const int nk = (int)((p.K + 63) / 64);
+  const int krem = (int)(p.K - (int64_t)(nk - 1) * 64);  // 1..64 (K % 8 == 0: multiple of 8)
   auto issue = [&](int piece, int kt) {
     char* dst = smem + (kt & 1) * P8_BUF + lds_off[piece] + wave * 1024;
-    const int64_t step = (piece == 0 || piece == 3) ? stepA : stepB;
+    const bool isA = piece == 0 || piece == 3;
+    const int64_t step = isA ? stepA : stepB;
+    const bool kc = isA ? AKC : BKC;
+    const int region = (piece == 3 || piece == 2) ? 1 : 0;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(src[piece][i] + kt * step, dst + i * 8192);
+    for (int i = 0; i < 2; ++i) {
+      const bf16_t* g = src[piece][i] + kt * step;
+      if (krem < 64 && kt == nk - 1) {
+        if (kc) {  // this lane's 8 k: 8 * chunk within the tile
+          const int r = i * 64 + (t >> 3);
+          const int kl = 8 * ((t & 7) ^ ((r >> 1) & 7));
+          if (kl >= krem) g -= kl - (krem - 8);
+        } else {   // this lane's k-row within the tile
+          const int kl = region * 32 + i * 16 + (t >> 5);
+          if (kl >= krem) g -= (int64_t)(kl - (krem - 1)) * (isA ? p.lda : p.ldb);
+        }
+      }
+      glds16(g, dst + i * 8192);
+    }
   };
 
   f32x4 acc[8][4];
@@ -689,6 +709,15 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bf[2][2][2];  // A quadrant rows (4 x 16) x kk;  B [bh][2 x 16 cols][kk]
+  auto mask_tail_a = [&](int kt) {
+    if (krem < 64 && kt == nk - 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          if (kk * 32 + 8 * (lane >> 4) >= krem) af[i][kk] = bf16x8{};
+    }
+  };
 
   auto read_a = [&](const char* buf, int ah) {
 #pragma unroll
@@ -727,7 +756,6 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   // after the one a wait retires) are the same for all four combinations: 5 / 4 at phase 1
   // (A split only), 4 at phase 3; tails retire everything.
   constexpr bool AS = AKC, BS = BKC;
-  const int nk = (int)(p.K / 64);
   if (AS) {
     issue(0, 0);
     issue(1, 0);
@@ -768,6 +796,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
     read_b(buf, 0);
     PZ_WAIT_LGKM0();
     PZ_RAW_BARRIER();
+    mask_tail_a(kt);
     mfma_quad(0, 0);
     PZ_RAW_BARRIER();
     // phase 1: quadrant (0,1); (A split) retire A region 1 of this tile for phase 2
@@ -790,6 +819,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
     read_a(buf, 1);
     PZ_WAIT_LGKM0();
     PZ_RAW_BARRIER();
+    mask_tail_a(kt);
     mfma_quad(1, 1);
     PZ_RAW_BARRIER();
     // phase 3: quadrant (1,0); retire tile kt+1's phase-0 operands (all of A when merged)
@@ -1067,7 +1097,7 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
-  if (a->K % BK256 == 0 && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512) &&
+  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512) &&
       a->batch * ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) >= 160) {
     pl.kind = PATH_256;
     pl.tiles_m = (a->M + BT - 1) / BT;

@@ -83,12 +83,15 @@ def test_all_four_layouts_batched_fp32_out():
             close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("K", [1024, 4304, 40])
 @pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
-def test_gemm256_layouts_with_tails(akc, bkc):
-    """Large shapes take the 256x256 LDS-DMA kernel; M/N not multiples of the tile."""
+def test_gemm256_layouts_with_tails(akc, bkc, K):
+    """Large shapes take the 256x256 LDS-DMA kernel; M/N not multiples of the tile, K tail
+    (4304 = SigLIP MLP width: 67 full K-tiles + 16; 40: a single partial K-tile)."""
     from pizero_native import ops
 
-    M, N, K = 2600, 4104, 1024
+    M, N = 2600, 4104
+    assert ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc).startswith("gemm8p_kernel")
     A = bf(M, K, scale=0.5)
     Bm = bf(N, K, scale=0.5)
     ref = A.float() @ Bm.float().t()

@@ -649,7 +649,7 @@ __device__ __forceinline__ bf16x8 frag_tr_asm(const char* lds, int rb, int kk, i
   } while (0)
 #define PZ_WAIT_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
-template <bool AKC, bool BKC, bool GEGLU>
+template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int tm, tn;
@@ -679,7 +679,8 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   // K % 64 != 0: the last K-tile has krem valid k; every lane's source is clamped into the
   // tensor (finite data) and the A fragments of k >= krem are zeroed before the MFMAs.
   const int nk = (int)((p.K + 63) / 64);
-  const int krem = (int)(p.K - (int64_t)(nk - 1) * 64);  // 1..64 (K % 8 == 0: multiple of 8)
+  // (KTAIL = false instantiations assume K % 64 == 0 and carry none of this code)
+  const int krem = KTAIL ? (int)(p.K - (int64_t)(nk - 1) * 64) : 64;  // 1..64 (K % 8 == 0)
   auto issue = [&](int piece, int kt) {
     char* dst = smem + (kt & 1) * P8_BUF + lds_off[piece] + wave * 1024;
     const bool isA = piece == 0 || piece == 3;
@@ -689,7 +690,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const bf16_t* g = src[piece][i] + kt * step;
-      if (krem < 64 && kt == nk - 1) {
+      if (KTAIL && krem < 64 && kt == nk - 1) {
         if (kc) {  // this lane's 8 k: 8 * chunk within the tile
           const int r = i * 64 + (t >> 3);
           const int kl = 8 * ((t & 7) ^ ((r >> 1) & 7));
@@ -710,7 +711,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 af[4][2], bf[2][2][2];  // A quadrant rows (4 x 16) x kk;  B [bh][2 x 16 cols][kk]
   auto mask_tail_a = [&](int kt) {
-    if (krem < 64 && kt == nk - 1) {
+    if (KTAIL && krem < 64 && kt == nk - 1) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1144,7 +1145,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
     case PATH_256:
       if (use_8phase())
-        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu));
+        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s, %s>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
+                 bstr(a->K % 64 != 0));
       else
         snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
                  BK256);
@@ -1180,10 +1182,10 @@ static int launch_tile_any(GemmP& p, const Plan& pl, int64_t batch, hipStream_t 
   return PZ_OK;
 }
 
-template <bool AKC, bool BKC, bool GEGLU>
-static int launch8p(const GemmP& p, int64_t batch, hipStream_t st) {
+template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
+static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
-  auto kern = gemm8p_kernel<AKC, BKC, GEGLU>;
+  auto kern = gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -1192,6 +1194,12 @@ static int launch8p(const GemmP& p, int64_t batch, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n, (unsigned)batch), dim3(NT2), smem, st, p);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
+}
+
+template <bool AKC, bool BKC, bool GEGLU>
+static int launch8p(const GemmP& p, int64_t batch, hipStream_t st) {
+  if (p.K % 64 != 0) return launch8p_k<AKC, BKC, GEGLU, true>(p, batch, st);
+  return launch8p_k<AKC, BKC, GEGLU, false>(p, batch, st);
 }
 
 // large-GEMM kernel: the 8-phase ping-pong (default) or the 2-stage 256 kernel (PZ_GEMM_BIG=2stage, A/B runs)

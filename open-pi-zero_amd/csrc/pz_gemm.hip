@@ -43,6 +43,10 @@ struct GemmP {
   // split-K (batch-1 only): blockIdx.y = split index; raw fp32 partials -> ws[z][M][ldw]
   float* ws;
   int64_t ksplit, ldw;
+  // 8-phase split tail (batch-1 only, tail_s > 0): work units [0, dp_tiles) are whole tiles; unit
+  // dp_tiles + u is K-piece (u % tail_s) (tail_kt K-tiles) of tile dp_tiles + u / tail_s, whose raw
+  // accumulators go to ws[u] (256 KiB, thread-major) for gemm8p_tail_epilogue.
+  int dp_tiles, tail_s, tail_kt;
 };
 
 __device__ __forceinline__ int sw_tr(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
@@ -649,11 +653,40 @@ __device__ __forceinline__ bf16x8 frag_tr_asm(const char* lds, int rb, int kk, i
   } while (0)
 #define PZ_WAIT_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 
+// 8-phase epilogue: wave (wr, wc) owns rows wr*128 + 16*rb + (lane & 15) and columns
+// wc*64 + 16*cb + 4*(lane >> 4) .. +3 (GeGLU: gate cb = 0,1 with up cb + 2 of the same column)
+template <bool GEGLU>
+__device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
+                                           int wr, int wc, int lane, const f32x4 (&acc)[8][4]) {
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb) {
+    const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
+    if (GEGLU) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + 4 * (lane >> 4), acc[rb][j], acc[rb][2 + j]);
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+        store_out4(p, cofs, rofs, m, n0 + wc * 64 + cb * 16 + 4 * (lane >> 4), acc[rb][cb]);
+    }
+  }
+}
+
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nk_all = (int)((p.K + 63) / 64);
+  int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
+  if (p.tail_s && lid >= p.dp_tiles) {  // split tail: one K-piece of a leftover tile
+    const int u = lid - p.dp_tiles;
+    piece = u;
+    lid = p.dp_tiles + u / p.tail_s;
+    kt0 = (u % p.tail_s) * p.tail_kt;
+    nk = min(nk_all - kt0, p.tail_kt);
+  }
   int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
   const int64_t m0 = (int64_t)tm * BT;
   const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
   const int t = threadIdx.x, lane = t & 63;
@@ -675,12 +708,21 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   }
   const int64_t stepA = AKC ? 64 : 64 * p.lda;
   const int64_t stepB = BKC ? 64 : 64 * p.ldb;
+  if (kt0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      src[0][i] += kt0 * stepA;
+      src[3][i] += kt0 * stepA;
+      src[1][i] += kt0 * stepB;
+      src[2][i] += kt0 * stepB;
+    }
+  }
   constexpr int lds_off[4] = {0, 2 * P8_REG, 3 * P8_REG, P8_REG};
   // K % 64 != 0: the last K-tile has krem valid k; every lane's source is clamped into the
   // tensor (finite data) and the A fragments of k >= krem are zeroed before the MFMAs.
-  const int nk = (int)((p.K + 63) / 64);
-  // (KTAIL = false instantiations assume K % 64 == 0 and carry none of this code)
-  const int krem = KTAIL ? (int)(p.K - (int64_t)(nk - 1) * 64) : 64;  // 1..64 (K % 8 == 0)
+  // (KTAIL = false instantiations assume K % 64 == 0 and carry none of this code; a K-piece
+  // that does not end the reduction has no tail)
+  const int krem = (KTAIL && kt0 + nk == nk_all) ? (int)(p.K - (int64_t)(nk_all - 1) * 64) : 64;  // 1..64
   auto issue = [&](int piece, int kt) {
     char* dst = smem + (kt & 1) * P8_BUF + lds_off[piece] + wave * 1024;
     const bool isA = piece == 0 || piece == 3;
@@ -842,19 +884,41 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   }
   if (wr == 0) PZ_RAW_BARRIER();
 
-  const int64_t cofs = zo * p.sCo + zi * p.sCi;
-  const int64_t rofs = zo * p.sRo + zi * p.sRi;
+  if (piece >= 0) {  // split tail: raw partial sums, summed + epilogued by gemm8p_tail_epilogue
+    f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)piece * (32 * NT2);
 #pragma unroll
-  for (int rb = 0; rb < 8; ++rb) {
-    const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
-    if (GEGLU) {
+    for (int rb = 0; rb < 8; ++rb)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + 4 * (lane >> 4), acc[rb][j], acc[rb][2 + j]);
-    } else {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) store_out4(p, cofs, rofs, m, n0 + wc * 64 + cb * 16 + 4 * (lane >> 4), acc[rb][cb]);
-    }
+      for (int cb = 0; cb < 4; ++cb) W[(rb * 4 + cb) * NT2 + t] = acc[rb][cb];
+    return;
+  }
+  epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc);
+}
+
+// Split tail, second pass: 16 blocks of 512 threads per leftover tile (one accumulator row-block rb and
+// one column half each, so the partial sums stream through many CUs); thread t sums the tail_s
+// partial accumulators it owned in gemm8p_kernel (fixed order) and applies the same epilogue.
+template <bool GEGLU>
+__global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
+  const int tile = blockIdx.x >> 4, rb = (blockIdx.x >> 1) & 7, h = blockIdx.x & 1;
+  int tm, tn;
+  tile_coords(p.dp_tiles + tile, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 2, wc = wave & 3;
+  const f32x4* W = reinterpret_cast<const f32x4*>(p.ws) + (int64_t)tile * p.tail_s * (32 * NT2);
+  // GeGLU pairs gate cb = h with up cb = h + 2; plain outputs take cb = 2h, 2h + 1
+  const int c0 = GEGLU ? h : 2 * h, c1 = GEGLU ? h + 2 : 2 * h + 1;
+  f32x4 a0 = W[(rb * 4 + c0) * NT2 + t], a1 = W[(rb * 4 + c1) * NT2 + t];
+  for (int z = 1; z < p.tail_s; ++z) {
+    a0 += W[(int64_t)z * (32 * NT2) + (rb * 4 + c0) * NT2 + t];
+    a1 += W[(int64_t)z * (32 * NT2) + (rb * 4 + c1) * NT2 + t];
+  }
+  const int64_t m = (int64_t)tm * BT + wr * 128 + rb * 16 + (lane & 15);
+  if (GEGLU) {
+    store_geglu4(p, 0, m, (int64_t)tn * (BT / 2) + wc * 32 + h * 16 + 4 * (lane >> 4), a0, a1);
+  } else {
+    const int64_t n = (int64_t)tn * BT + wc * 64 + 4 * (lane >> 4);
+    store_out4(p, 0, 0, m, n + c0 * 16, a0);
+    store_out4(p, 0, 0, m, n + c1 * 16, a1);
   }
 }
 
@@ -1080,7 +1144,47 @@ struct Plan {
   bool akc, bkc, geglu;
   int wm, tag, skinny_w, splits;
   int64_t ksplit, ldw, tiles_m, tiles_n;
+  int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
 };
+
+// compute units of the current device (the "wave" of resident 8-phase workgroups: 1 per CU)
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// Wave quantisation of the 8-phase kernel (one 256x256 tile per CU at a time): T = q*G + r tiles
+// leave the last round r/G full.  Split each of the r leftover tiles into s K-pieces (s*r <= G)
+// so the last round takes ~1/s of a tile time; partial sums go through the fp32 workspace.
+// q == 0 (fewer tiles than CUs, e.g. weight gradients of small layers) is the same split.
+void plan_tail(Plan& pl, const pz_gemm_args* a) {
+  if (a->batch != 1 || !a->workspace || !PZ_ALIGNED(a->workspace, 16)) return;
+  const char* e = getenv("PZ_GEMM_TAIL");  // "0": whole tiles only (A/B runs; read per call)
+  if (e && e[0] == '0') return;
+  const int64_t G = device_cus();
+  const int64_t T = pl.tiles_m * pl.tiles_n;
+  const int64_t q = T / G, r = T % G;
+  const int64_t nk = (a->K + 63) / 64;
+  // a leftover round at least half full runs about as fast as its K-pieces would (less contention)
+  if (r == 0 || (q > 0 && 2 * r >= G)) return;
+  int64_t s = G / r;
+  s = s < 16 ? s : 16;
+  s = s < nk / 2 ? s : nk / 2;
+  if (s < 2) return;
+  const int64_t kt = (nk + s - 1) / s;
+  s = (nk + kt - 1) / kt;
+  if (s < 2 || r * s * (int64_t)(32 * NT2 * 16) > a->ws_bytes) return;
+  pl.dp_tiles = (int)(q * G);
+  pl.tail_s = (int)s;
+  pl.tail_kt = (int)kt;
+}
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
 Plan make_plan(const pz_gemm_args* a) {
@@ -1098,12 +1202,16 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
-  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512) &&
-      a->batch * ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) >= 160) {
-    pl.kind = PATH_256;
-    pl.tiles_m = (a->M + BT - 1) / BT;
-    pl.tiles_n = (ncols + cw - 1) / cw;
-    return pl;
+  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512)) {
+    const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;
+    Plan cand = pl;
+    cand.kind = PATH_256;
+    cand.tiles_m = tm;
+    cand.tiles_n = tn;
+    if (use_8phase()) plan_tail(cand, a);
+    // enough workgroups to fill the chip: whole tiles, or tiles split into K-pieces
+    const int64_t units = cand.tail_s ? cand.dp_tiles + (tm * tn - cand.dp_tiles) * cand.tail_s : a->batch * tm * tn;
+    if (units >= 160) return cand;
   }
   pl.kind = PATH_TILE;
   pl.tiles_m = (a->M + BM - 1) / BM;
@@ -1144,7 +1252,11 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d>", pl.skinny_w);
       break;
     case PATH_256:
-      if (use_8phase())
+      if (use_8phase() && pl.tail_s)
+        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s, %s>+gemm8p_tail_epilogue(tail %lld x %d)",
+                 bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0),
+                 (long long)(pl.tiles_m * pl.tiles_n - pl.dp_tiles), pl.tail_s);
+      else if (use_8phase())
         snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s, %s>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
                  bstr(a->K % 64 != 0));
       else
@@ -1191,8 +1303,14 @@ static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(p.tiles_m * p.tiles_n, (unsigned)batch), dim3(NT2), smem, st, p);
+  const int T = p.tiles_m * p.tiles_n;
+  const int units = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
+  hipLaunchKernelGGL(kern, dim3(units, (unsigned)batch), dim3(NT2), smem, st, p);
   PZ_CHECK_LAUNCH();
+  if (p.tail_s) {
+    hipLaunchKernelGGL(gemm8p_tail_epilogue<GEGLU>, dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+    PZ_CHECK_LAUNCH();
+  }
   return PZ_OK;
 }
 
@@ -1269,6 +1387,12 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
   if (pl.kind == PATH_256 && use_8phase()) {
+    if (pl.tail_s) {
+      p.ws = (float*)a->workspace;
+      p.dp_tiles = pl.dp_tiles;
+      p.tail_s = pl.tail_s;
+      p.tail_kt = pl.tail_kt;
+    }
     if (geglu) {
       if (a->a_kcontig) return launch8p<true, true, true>(p, a->batch, st);
       return launch8p<false, true, true>(p, a->batch, st);

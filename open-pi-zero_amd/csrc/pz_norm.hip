@@ -267,6 +267,48 @@ __global__ void reduce_parts_kernel(const float* __restrict__ part, int64_t P, i
   out[n] = f2bf(s);
 }
 
+// Vectorised fixed-order reduction of P fp32 partial rows (D % 4 == 0): a 256-thread block owns
+// 4*CT columns; CT column-threads read float4s, 256/CT part-lanes stride over P (4 loads in flight),
+// then the part-lanes are folded through LDS in a fixed order (deterministic, run to run).
+template <int CT>
+__global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restrict__ part, int64_t P,
+                                                            int64_t D, bf16_t* out, int beta) {
+  constexpr int PL = 256 / CT;
+  __shared__ f32x4 red[PL][CT];
+  const int ct = threadIdx.x % CT, pl = threadIdx.x / CT;
+  const int64_t c = ((int64_t)blockIdx.x * CT + ct) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (c < D) {
+    const float* src = part + c;
+    int64_t p = pl;
+    for (; p + 3 * PL < P; p += 4 * PL) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(src + p * D);
+      const f32x4 b = *reinterpret_cast<const f32x4*>(src + (p + PL) * D);
+      const f32x4 e = *reinterpret_cast<const f32x4*>(src + (p + 2 * PL) * D);
+      const f32x4 f = *reinterpret_cast<const f32x4*>(src + (p + 3 * PL) * D);
+      s += (a + b) + (e + f);
+    }
+    for (; p < P; p += PL) s += *reinterpret_cast<const f32x4*>(src + p * D);
+  }
+  red[pl][ct] = s;
+  __syncthreads();
+  if (pl == 0 && c < D) {
+#pragma unroll 8
+    for (int i = 1; i < PL; ++i) s += red[i][ct];
+    u32x2 o;
+    if (beta) {
+      const u32x2 prev = *reinterpret_cast<const u32x2*>(out + c);
+      s[0] += __uint_as_float(prev[0] << 16);
+      s[1] += __uint_as_float(prev[0] & 0xffff0000u);
+      s[2] += __uint_as_float(prev[1] << 16);
+      s[3] += __uint_as_float(prev[1] & 0xffff0000u);
+    }
+    o[0] = pack2bf(s[0], s[1]);
+    o[1] = pack2bf(s[2], s[3]);
+    *reinterpret_cast<u32x2*>(out + c) = o;
+  }
+}
+
 // column sums of a bf16 matrix: pass 1 -> ws[chunk][n], pass 2 -> out
 __global__ void colsum_pass1(const bf16_t* __restrict__ X, int64_t ld, int64_t M, int64_t N,
                              int64_t rows_per_chunk, float* ws) {
@@ -282,6 +324,37 @@ __global__ void colsum_pass1(const bf16_t* __restrict__ X, int64_t ld, int64_t M
   }
   ws[blockIdx.y * N + n2] = s0;
   if (two) ws[blockIdx.y * N + n2 + 1] = s1;
+}
+
+// colsum pass 1 for N % 8 == 0, ld % 8 == 0: 32 column-threads x 8 row-lanes per block, 16-B
+// loads (8 columns), one block row per `rpc` rows -> ws[chunk][N] (fp32, fixed order).
+__global__ void __launch_bounds__(256) colsum8_pass1(const bf16_t* __restrict__ X, int64_t ld, int64_t M,
+                                                     int64_t N, int64_t rpc, float* ws) {
+  __shared__ float red[8][32 * 8 + 4];
+  const int ct = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int64_t c = ((int64_t)blockIdx.x * 32 + ct) * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * rpc;
+  const int64_t r1 = min(M, r0 + rpc);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    for (int64_t r = r0 + rl; r < r1; r += 8) {
+      float v[8];
+      load8(X + r * ld + c, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[rl][ct * 8 + i] = s[i];
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * 256;
+  const int j = threadIdx.x;  // one output column per thread
+  if (c0 + j < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][j];
+    ws[blockIdx.y * N + c0 + j] = t;
+  }
 }
 
 __global__ void batch_sum_kernel(const bf16_t* __restrict__ X, int64_t B, int64_t stride, int64_t n,
@@ -370,10 +443,27 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   return PZ_OK;
 }
 
+static void launch_reduce_parts(const float* part, int64_t P, int64_t D, bf16_t* out, int beta, hipStream_t st) {
+  if (D % 4 == 0 && PZ_ALIGNED(part, 16) && PZ_ALIGNED(out, 8)) {
+    // column-threads per block: enough blocks to cover the chip when D is small, wide rows when D is large
+    if (D >= 256 * 256)
+      hipLaunchKernelGGL(reduce_parts4_kernel<64>, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, st, part, P, D,
+                         out, beta);
+    else if (D >= 256 * 64)
+      hipLaunchKernelGGL(reduce_parts4_kernel<16>, dim3((unsigned)((D + 63) / 64)), dim3(256), 0, st, part, P, D,
+                         out, beta);
+    else
+      hipLaunchKernelGGL(reduce_parts4_kernel<4>, dim3((unsigned)((D + 15) / 16)), dim3(256), 0, st, part, P, D,
+                         out, beta);
+  } else {
+    hipLaunchKernelGGL(reduce_parts_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, st, part, P, D, out,
+                       beta);
+  }
+}
+
 extern "C" int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream) {
   PZ_CHECK_ARG(part && out && P > 0 && D > 0, "reduce_parts: bad args");
-  hipLaunchKernelGGL(reduce_parts_kernel, dim3((unsigned)((D + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     part, P, D, (bf16_t*)out, (int)beta);
+  launch_reduce_parts(part, P, D, (bf16_t*)out, (int)beta, (hipStream_t)stream);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
@@ -382,13 +472,19 @@ extern "C" int pz_colsum(const void* X, int64_t ld, int64_t M, int64_t N, void* 
                          void* stream) {
   PZ_CHECK_ARG(X && out && ws && M > 0 && N > 0, "colsum: bad args");
   hipStream_t st = (hipStream_t)stream;
-  const int64_t chunks = M < 64 ? M : 64;
-  const int64_t rpc = (M + chunks - 1) / chunks;
-  dim3 grid((unsigned)((N / 2 + 1 + 255) / 256), (unsigned)chunks);
-  hipLaunchKernelGGL(colsum_pass1, grid, dim3(256), 0, st, (const bf16_t*)X, ld, M, N, rpc, ws);
+  int64_t chunks = M < 64 ? M : 64;  // ws holds 64 partial rows (pz_abi.h)
+  if (N % 8 == 0 && ld % 8 == 0 && PZ_ALIGNED(X, 16)) {
+    const int64_t rpc = (M + chunks - 1) / chunks;
+    chunks = (M + rpc - 1) / rpc;
+    dim3 grid((unsigned)((N + 255) / 256), (unsigned)chunks);
+    hipLaunchKernelGGL(colsum8_pass1, grid, dim3(256), 0, st, (const bf16_t*)X, ld, M, N, rpc, ws);
+  } else {
+    const int64_t rpc = (M + chunks - 1) / chunks;
+    dim3 grid((unsigned)((N / 2 + 1 + 255) / 256), (unsigned)chunks);
+    hipLaunchKernelGGL(colsum_pass1, grid, dim3(256), 0, st, (const bf16_t*)X, ld, M, N, rpc, ws);
+  }
   PZ_CHECK_LAUNCH();
-  hipLaunchKernelGGL(reduce_parts_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, st, (const float*)ws,
-                     chunks, N, (bf16_t*)out, (int)beta);
+  launch_reduce_parts(ws, chunks, N, (bf16_t*)out, (int)beta, st);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -144,8 +144,8 @@ def linear_dgrad(dy, W, dx, *, beta=False, resid=None):
 def _split_k(M, N, K):
     """Split the token (reduction) dim when the output has too few 256x256 tiles to fill 256 CUs."""
     tiles = ((N + 255) // 256) * ((K + 255) // 256)
-    if tiles >= 160 or M < 4096 or N < 512 or K < 512:
-        return 1
+    if tiles >= 160 or M < 4096 or N < 512 or K < 512 or M % 8 == 0:
+        return 1  # (M % 8 == 0: the 8-phase kernel splits K itself -- pz_gemm "split tail")
     best = 1
     for s in (2, 4, 8):  # fewest splits that reach ~1 wave of 256-thread... 240+ workgroups
         if M % (s * 64) == 0:

@@ -121,6 +121,55 @@ def test_gemm256_geglu_with_tail():
     close(h, torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:])
 
 
+@pytest.mark.parametrize("M,N,K", [(1280, 1280, 2056), (4352, 4096, 1024)])
+@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
+def test_gemm8p_split_tail(akc, bkc, M, N, K):
+    """Wave-quantisation split: leftover tiles (all 25 of a 5x5 grid; 16 after one full round of 256)
+    run as K-pieces into the fp32 workspace, summed + epilogued by gemm8p_tail_epilogue.
+    Covers bias, residual, beta accumulation and a K tail (2056 = 32 K-tiles + 8) in the last piece."""
+    import os
+
+    from pizero_native import ops
+
+    name = ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc)
+    assert name.startswith("gemm8p_kernel") and "tail" in name, name
+    A = bf(M, K, scale=0.5)
+    Bm = bf(N, K, scale=0.5)
+    ref = A.float() @ Bm.float().t()
+    Aop = A if akc else A.t().contiguous()
+    Bop = Bm if bkc else Bm.t().contiguous()
+    lda, ldb = (K if akc else M), (K if bkc else N)
+    bias, R = bf(N), bf(M, N)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, Aop, lda, akc, Bop, ldb, bkc, C, N, bias=bias, resid=R, ld_resid=N)
+    close(C, ref + bias.float() + R.float(), atol=3e-2)
+    C0 = torch.empty_like(C)
+    os.environ["PZ_GEMM_TAIL"] = "0"
+    try:
+        ops.gemm(M, N, K, Aop, lda, akc, Bop, ldb, bkc, C0, N, bias=bias, resid=R, ld_resid=N)
+    finally:
+        os.environ.pop("PZ_GEMM_TAIL")
+    close(C, C0, atol=3e-2)
+    Cb = R.clone()
+    ops.gemm(M, N, K, Aop, lda, akc, Bop, ldb, bkc, Cb, N, beta=True)
+    close(Cb, ref + R.float(), atol=3e-2)
+    C2 = torch.empty_like(C)
+    ops.gemm(M, N, K, Aop, lda, akc, Bop, ldb, bkc, C2, N, bias=bias, resid=R, ld_resid=N)
+    assert torch.equal(C, C2)  # fixed-order partial sums: deterministic
+
+
+def test_wgrad_small_output_uses_split_tail():
+    """weight gradient of a 1152x1152 layer over 16384 tokens: 25 output tiles split into K-pieces"""
+    from pizero_native import ops
+
+    M, N, K = 16384, 1152, 1152
+    dy, x = bf(M, N, scale=0.3), bf(M, K, scale=0.3)
+    assert "tail" in ops.gemm_kernel_name(N, K, M, a_kc=False, b_kc=False)
+    dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    ops.linear_wgrad(dy, x, dW)
+    close(dW, dy.float().t() @ x.float(), atol=5e-2)
+
+
 def test_epilogues_gelu_resid_geglu_silu():
     from pizero_native import ops
 
@@ -269,6 +318,32 @@ def test_layernorm_fwd_bwd():
     close(db2, dy.float().sum(0), atol=0.1)
 
 
+@pytest.mark.parametrize("M,N", [(16384, 1152), (17664, 2048), (300, 4304), (5, 7), (1000, 40), (64, 3456), (257, 1024)])
+def test_colsum_and_reduce_parts_shapes(M, N):
+    """bias / norm-weight gradient reductions (vectorised and scalar dispatch paths), with and without beta"""
+    from pizero_native import ops
+
+    X = bf(M, N)
+    ref = X.float().sum(0)
+    out = torch.empty(N, device=dev, dtype=torch.bfloat16)
+    ws = torch.empty(64 * N, device=dev)
+    ops.colsum(X, out, ws)
+    close(out, ref, atol=0.05 + 2e-3 * math.sqrt(M))
+    prev = bf(N)
+    out2 = prev.clone()
+    ops.colsum(X, out2, ws, beta=True)
+    close(out2, ref + prev.float(), atol=0.05 + 2e-3 * math.sqrt(M))
+    # fixed-order reduction: bitwise identical on a second launch
+    out3 = torch.empty_like(out)
+    ops.colsum(X, out3, ws)
+    assert torch.equal(out, out3)
+    P = (M + 63) // 64
+    part = torch.randn(P, N, device=dev)
+    r = torch.empty(N, device=dev, dtype=torch.bfloat16)
+    ops.reduce_parts(part, r)
+    close(r, part.sum(0), atol=1e-2 * math.sqrt(P))
+
+
 def _block_mask(cnt, P, C, Lq_off, Lq, L):
     m = torch.zeros(len(cnt), Lq, L, dtype=torch.bool)
     for b, c in enumerate(cnt):
@@ -377,8 +452,8 @@ def test_adamw_matches_torch():
 def test_wgrad_split_k_matches_single_pass():
     from pizero_native import ops
 
-    M, N, K = 8192, 1024, 768  # small output, long token reduction -> split-K path
-    assert ops._split_k(M, N, K) > 1
+    M, N, K = 8192, 1024, 768  # small output, long token reduction -> K split inside pz_gemm (split tail)
+    assert "tail" in ops.gemm_kernel_name(N, K, M, a_kc=False, b_kc=False)
     dy, x = bf(M, N), bf(M, K)
     dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
     ops.linear_wgrad(dy, x, dW)

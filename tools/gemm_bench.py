@@ -1,4 +1,4 @@
-"""Microbenchmark: pz_gemm (all layouts) vs torch.matmul (hipBLASLt) on the Pi0 training shapes.
+"""Microbenchmark: pz_gemm (all layouts; split tail on/off) vs torch.matmul (hipBLASLt) on the Pi0 training shapes.
 
     python tools/gemm_bench.py [--iters 20]
 Random bf16 operands (uniform [-1,1)), interleaved A/B timing in one process.
@@ -46,15 +46,14 @@ def main():
     args = ap.parse_args()
     dev = "cuda"
     rnd = lambda *s: (torch.rand(*s, device=dev) * 2 - 1).to(torch.bfloat16)  # noqa: E731
-    print(f"{'shape':16s} {'layout':6s} {'M':>6} {'N':>6} {'K':>6} {'8ph TF/s':>9} {'2stg TF/s':>9} {'torch TF/s':>10}")
+    print(f"{'shape':16s} {'layout':6s} {'M':>6} {'N':>6} {'K':>6} {'8ph TF/s':>9} {'notail':>9} {'torch TF/s':>10}")
 
     def ab(fn):
-        """time fn under the 8-phase kernel and the 2-stage 256 kernel (pz_gemm reads PZ_GEMM_BIG per call)"""
-        os.environ["PZ_GEMM_BIG"] = "8phase"
+        """time fn with and without the 8-phase split tail (pz_gemm reads PZ_GEMM_TAIL per call)"""
         a = timeit(fn, args.iters)
-        os.environ["PZ_GEMM_BIG"] = "2stage"
+        os.environ["PZ_GEMM_TAIL"] = "0"
         b = timeit(fn, args.iters)
-        os.environ["PZ_GEMM_BIG"] = "8phase"
+        os.environ.pop("PZ_GEMM_TAIL")
         return a, b
 
     for name, M, N, K in SHAPES:

@@ -1,7 +1,8 @@
 """Run one pz_gemm shape/layout a few times (for rocprofv3 counter passes).
 
     python tools/gemm_one.py --layout TN --M 17664 --N 2048 --K 2048 [--variant 8phase|2stage] [--iters 5]
-M, N, K = the forward nn.Linear shape; layouts NT (fwd), NN (dgrad), TN (wgrad) as in tools/gemm_bench.py.
+M, N, K = the forward nn.Linear shape; layouts NT (fwd), NN (dgrad), TN (wgrad) as in tools/gemm_bench.py;
+GEGLU = the vlm gate|up GEMM with the GeGLU epilogue and saved g|u (N = 2 * intermediate).
 """
 
 import argparse
@@ -23,8 +24,11 @@ def main():
     ap.add_argument("--K", type=int, default=2048)
     ap.add_argument("--variant", default="8phase")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--notail", action="store_true", help="PZ_GEMM_TAIL=0: whole tiles only")
     a = ap.parse_args()
     os.environ["PZ_GEMM_BIG"] = a.variant
+    if a.notail:
+        os.environ["PZ_GEMM_TAIL"] = "0"
     from pizero_native import ops
 
     dev = "cuda"
@@ -34,8 +38,12 @@ def main():
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
     dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
-    fn = {"NT": lambda: ops.linear(x, w, y), "NN": lambda: ops.linear_dgrad(dy, w, dx),
-          "TN": lambda: ops.linear_wgrad(dy, x, dW)}[a.layout]
+    if a.layout == "GEGLU":  # the bench's dominant launch: gate|up GEMM + GeGLU, saved g|u (engine.py)
+        hm = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+        fn = lambda: ops.linear(x, w, hm, epi=ops.PZ_EPI_GEGLU, aux=y)  # noqa: E731
+    else:
+        fn = {"NT": lambda: ops.linear(x, w, y), "NN": lambda: ops.linear_dgrad(dy, w, dx),
+              "TN": lambda: ops.linear_wgrad(dy, x, dW)}[a.layout]
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(2):
         fn()

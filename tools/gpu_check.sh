@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, default bench line, rocprofv3 kernel stats of the bench.
+# usage (gpurun, from the repo root): bash tools/gpu_check.sh TAG [tests|bench|prof ...]
+# Every GPU step has its own time limit; the first failing step ends the script.
+set -e
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests bench prof}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread \
+        > "$OUT/tests.log" 2>&1 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > "$OUT/bench.log" 2>&1 ;;
+    prof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/prof.log" 2>&1 ;;
+    infprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/infprof" -o infer \
+        -- python3 tools/infer_bench.py --iters 20 > "$OUT/infprof.log" 2>&1 ;;
+    gemmbench)
+      timeout -k 10 400 python -u tools/gemm_bench.py --iters 10 > "$OUT/gemm_bench.log" 2>&1 ;;
+    pmc)
+      bash tools/pmc_dominant.sh "$OUT/pmc" ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  echo "step $s ok"
+done

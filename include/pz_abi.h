@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 2
+#define PZ_ABI_VERSION 3
 
 enum {
   PZ_OK = 0,
@@ -36,6 +36,11 @@ enum {
   PZ_EPI_GELU = 1,  /* pre = alpha*acc + bias; aux = pre; C = gelu_tanh(pre) (+resid)   */
   PZ_EPI_GEGLU = 2, /* B = [gate; up] (N = 2I); aux = [g | u]; C[m,n] = gelu(g)*u        */
   PZ_EPI_SILU = 3,  /* pre = alpha*acc + bias; aux = pre; C = silu(pre)                  */
+  /* backward epilogues (dgrad GEMM of the layer after the activation; aux is READ):            */
+  PZ_EPI_DGELU = 4,  /* C = alpha*acc * gelu_tanh'(aux[m,n])   (aux = saved pre-activation)  */
+  PZ_EPI_DSILU = 5,  /* C = alpha*acc * silu'(aux[m,n])                                       */
+  PZ_EPI_DGEGLU = 6, /* N = I, aux = saved [g | u] ([M, 2I]); d = alpha*acc:                    */
+                     /*   C[m,n] = d*u*gelu'(g), C[m,I+n] = d*gelu(g)  (C may alias aux)       */
 };
 
 /*
@@ -60,7 +65,7 @@ typedef struct pz_gemm_args {
   const void* bias;                   /* bf16 [N] or NULL */
   const void* resid; int64_t ld_resid; /* bf16, may alias C */
   void* aux; int64_t ld_aux;           /* bf16 saved pre-activations or NULL */
-  int64_t geglu_inter;                 /* I for PZ_EPI_GEGLU */
+  int64_t geglu_inter;                 /* I for PZ_EPI_GEGLU / PZ_EPI_DGEGLU */
   /* optional fp32 scratch (caller-owned, 16-byte aligned): when a batch-1 GEMM has too few
    * output tiles to fill the chip (prefill at B=1) and ws_bytes allows, K is split over
    * workgroups into fp32 slabs and a second kernel sums them and applies the epilogue.

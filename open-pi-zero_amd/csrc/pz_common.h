@@ -50,17 +50,24 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
+// tanh through one v_exp_f32 + one reciprocal (|err| ~1e-7 absolute; saturates cleanly to +-1):
+// libm tanhf expands to ~40 instructions, which bloats every fused epilogue that applies it per element
+__device__ __forceinline__ float tanh_fast(float u) {
+  const float e = __expf(2.f * u);
+  return 1.f - __fdividef(2.f, e + 1.f);
+}
+
 // gelu(x, approximate="tanh") and its derivative (fp32)
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanhf(u));
+  return 0.5f * x * (1.f + tanh_fast(u));
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;
   float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
+  float t = tanh_fast(u);
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 

@@ -143,67 +143,248 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
 }
 
 // ---- epilogue: one lane owns C[m][n..n+3] (swapped-operand MFMA layout) -------
-__device__ __forceinline__ void store_out4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                           const f32x4& acc) {
+// Side inputs of the epilogue (residual, saved activations, old C for beta accumulation, bias) are
+// loaded by epi_load4 into raw registers and consumed by epi_store4.  Kernels that own many output
+// groups per lane issue the loads of the next groups before the stores of the current ones: the
+// pointers may alias C (resid == C, DGEGLU in place), so the compiler cannot hoist a load above an
+// earlier store by itself and would otherwise pay one memory round trip per 4-column group.
+struct Side {
+  u32x4 w;  // .xy: aux (DGELU/DSILU pre-activation, DGEGLU g) or old bf16 C (beta); .zw: resid or DGEGLU u
+            // (fp32 C with beta: all four lanes hold the old fp32 values)
+};
+
+__device__ __forceinline__ u32x2 ld4bf(const bf16_t* X, bool full, int64_t n, int64_t N) {
+  if (full) return *reinterpret_cast<const u32x2*>(X);
+  unsigned h[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) h[r] = n + r < N ? (unsigned)X[r] : 0u;
+  return u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+}
+__device__ __forceinline__ void unpack4(u32x2 w, float (&o)[4]) {
+  o[0] = __uint_as_float(w[0] << 16); o[1] = __uint_as_float(w[0] & 0xffff0000u);
+  o[2] = __uint_as_float(w[1] << 16); o[3] = __uint_as_float(w[1] & 0xffff0000u);
+}
+__device__ __forceinline__ void store4(bf16_t* X, bool full, int64_t n, int64_t N, const float (&v)[4]) {
+  if (full) {
+    *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < N) X[r] = f2bf(v[r]);
+  }
+}
+
+__device__ __forceinline__ u32x2 epi_load_bias(const GemmP& p, int64_t n) {
+  if (!p.bias || n >= p.N) return u32x2{0u, 0u};
+  return ld4bf(p.bias + n, n + 4 <= p.N, n, p.N);
+}
+
+// epilogue classes (compile-time, so each fully unrolled 8-phase epilogue carries one class's code)
+enum EpiMode { EM_BF16 = 0, EM_F32 = 1, EM_DACT = 2, EM_DGEGLU = 3 };
+
+template <int EM>
+__device__ __forceinline__ void epi_load4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                          Side& s) {
+  s.w = u32x4{0u, 0u, 0u, 0u};
+  if (m >= p.M || n >= p.N) return;
+  const bool full = n + 4 <= p.N;
+  if constexpr (EM == EM_DGEGLU) {
+    const bf16_t* X = p.aux + m * p.ld_aux + n;
+    const u32x2 g = ld4bf(X, full, n, p.N), u = ld4bf(X + p.geglu_I, full, n, p.N);
+    s.w = u32x4{g[0], g[1], u[0], u[1]};
+  } else if constexpr (EM == EM_DACT) {
+    const u32x2 x = ld4bf(p.aux + m * p.ld_aux + n, full, n, p.N);
+    s.w = u32x4{x[0], x[1], 0u, 0u};
+  } else if constexpr (EM == EM_F32) {
+    if (p.beta) {
+      const float* Cp = reinterpret_cast<const float*>(p.C) + cofs + m * p.ldc + n;
+      if (full) {
+        s.w = *reinterpret_cast<const u32x4*>(Cp);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s.w[r] = n + r < p.N ? __float_as_uint(Cp[r]) : 0u;
+      }
+    } else if (p.resid) {
+      const u32x2 x = ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N);
+      s.w = u32x4{0u, 0u, x[0], x[1]};
+    }
+  } else {
+    u32x2 x0{0u, 0u}, x1{0u, 0u};
+    if (p.resid) x1 = ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N);
+    if (p.beta) x0 = ld4bf(reinterpret_cast<const bf16_t*>(p.C) + cofs + m * p.ldc + n, full, n, p.N);
+    s.w = u32x4{x0[0], x0[1], x1[0], x1[1]};
+  }
+}
+
+template <int EM>
+__device__ __forceinline__ void epi_store4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                           const f32x4& acc, const Side& s, u32x2 bias) {
   if (m >= p.M || n >= p.N) return;
   const bool full = n + 4 <= p.N;
   float v[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] = acc[r] * p.alpha;
-  if (p.bias) {
+  float x0[4], x1[4];
+  unpack4(u32x2{s.w[0], s.w[1]}, x0);
+  unpack4(u32x2{s.w[2], s.w[3]}, x1);
+  bf16_t* Cb = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+  if constexpr (EM == EM_DGEGLU) {  // GeGLU backward from saved [g | u]: two outputs, nothing else applies
+    float dg[4], du[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (full || n + r < p.N) v[r] += bf2f(p.bias[n + r]);
-  }
-  if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
-    if (p.aux) {
-      bf16_t* X = p.aux + m * p.ld_aux + n;
-      if (full) {
-        *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    for (int r = 0; r < 4; ++r) {
+      dg[r] = v[r] * x1[r] * gelu_tanh_grad(x0[r]);
+      du[r] = v[r] * gelu_tanh(x0[r]);
+    }
+    store4(Cb, full, n, p.N, dg);
+    store4(Cb + p.geglu_I, full, n, p.N, du);
+  } else if constexpr (EM == EM_DACT) {  // activation backward from the saved pre-activation
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= p.epi == PZ_EPI_DGELU ? gelu_tanh_grad(x0[r]) : silu_grad(x0[r]);
+    store4(Cb, full, n, p.N, v);
+  } else {
+    if (p.bias) {
+      float b[4];
+      unpack4(bias, b);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += b[r];
+    }
+    if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+      if (p.aux) store4(p.aux + m * p.ld_aux + n, full, n, p.N, v);
+      if (p.epi == PZ_EPI_GELU) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
       } else {
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) X[r] = f2bf(v[r]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
       }
     }
-    if (p.epi == PZ_EPI_GELU) {
+    if constexpr (EM == EM_F32) {
+      if (p.beta) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
+        for (int r = 0; r < 4; ++r) v[r] += __uint_as_float(s.w[r]);
+      } else if (p.resid) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += x1[r];
+      }
+      float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
+      if (full) {
+        *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < p.N) Cp[r] = v[r];
+      }
     } else {
+      if (p.resid) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
+        for (int r = 0; r < 4; ++r) v[r] += x1[r];
+      }
+      if (p.beta) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += x0[r];
+      }
+      store4(Cb, full, n, p.N, v);
     }
   }
-  if (p.resid) {
-    const bf16_t* R = p.resid + rofs + m * p.ld_resid + n;
+}
+
+__device__ __forceinline__ int epi_mode(const GemmP& p) {
+  if (p.epi == PZ_EPI_DGEGLU) return EM_DGEGLU;
+  if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) return EM_DACT;
+  return p.c_fp32 ? EM_F32 : EM_BF16;
+}
+
+template <int EM>
+__device__ __forceinline__ void store_out4_m(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                             const f32x4& acc) {
+  Side s;
+  epi_load4<EM>(p, cofs, rofs, m, n, s);
+  epi_store4<EM>(p, cofs, rofs, m, n, acc, s, epi_load_bias(p, n));
+}
+
+// one group, runtime-general (edge tiles of the 8-phase kernel: one compact copy per group)
+__device__ __forceinline__ void store_out4_rt(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                              const f32x4& acc) {
+  if (m >= p.M || n >= p.N) return;
+  const bool full = n + 4 <= p.N;
+  float v[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (full || n + r < p.N) v[r] += bf2f(R[r]);
+  for (int r = 0; r < 4; ++r) v[r] = acc[r] * p.alpha;
+  if (p.epi == PZ_EPI_DGEGLU) {
+    float g[4], u[4], dg[4], du[4];
+    const bf16_t* X = p.aux + m * p.ld_aux + n;
+    unpack4(ld4bf(X, full, n, p.N), g);
+    unpack4(ld4bf(X + p.geglu_I, full, n, p.N), u);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      dg[r] = v[r] * u[r] * gelu_tanh_grad(g[r]);
+      du[r] = v[r] * gelu_tanh(g[r]);
+    }
+    bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
+    store4(Cp, full, n, p.N, dg);
+    store4(Cp + p.geglu_I, full, n, p.N, du);
+    return;
+  }
+  if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) {
+    float x[4];
+    unpack4(ld4bf(p.aux + m * p.ld_aux + n, full, n, p.N), x);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= p.epi == PZ_EPI_DGELU ? gelu_tanh_grad(x[r]) : silu_grad(x[r]);
+  }
+  if (p.bias) {
+    float b[4];
+    unpack4(ld4bf(p.bias + n, full, n, p.N), b);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += b[r];
+  }
+  if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+    if (p.aux) store4(p.aux + m * p.ld_aux + n, full, n, p.N, v);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = p.epi == PZ_EPI_GELU ? gelu_tanh(v[r]) : silu(v[r]);
+  }
+  if (p.resid) {
+    float x[4];
+    unpack4(ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N), x);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += x[r];
   }
   if (p.c_fp32) {
     float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
-    if (full) {
-      if (p.beta) {
-        f32x4 o = *reinterpret_cast<f32x4*>(Cp);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-      }
-      *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
-    } else {
-      for (int r = 0; r < 4; ++r)
-        if (n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
-    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (full || n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
   } else {
     bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-    if (full) {
-      if (p.beta) {
-        u32x2 o = *reinterpret_cast<u32x2*>(Cp);
-        v[0] += bf2f(o[0] & 0xffff); v[1] += bf2f(o[0] >> 16);
-        v[2] += bf2f(o[1] & 0xffff); v[3] += bf2f(o[1] >> 16);
-      }
-      *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-    } else {
-      for (int r = 0; r < 4; ++r)
-        if (n + r < p.N) Cp[r] = f2bf(p.beta ? bf2f(Cp[r]) + v[r] : v[r]);
+    if (p.beta) {
+      float o[4];
+      unpack4(ld4bf(Cp, full, n, p.N), o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += o[r];
     }
+    store4(Cp, full, n, p.N, v);
+  }
+}
+
+// run f(std::integral_constant<int, EM>) for the epilogue class of p (one branch per launch, outside
+// the unrolled per-group loops)
+template <class F>
+__device__ __forceinline__ void epi_dispatch(const GemmP& p, F&& f) {
+  switch (epi_mode(p)) {
+    case EM_DGEGLU: f(std::integral_constant<int, EM_DGEGLU>{}); break;
+    case EM_DACT: f(std::integral_constant<int, EM_DACT>{}); break;
+    case EM_F32: f(std::integral_constant<int, EM_F32>{}); break;
+    default: f(std::integral_constant<int, EM_BF16>{}); break;
+  }
+}
+
+// one group, loads then stores (kernels with few groups per lane)
+__device__ __forceinline__ void store_out4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
+                                           const f32x4& acc) {
+  switch (epi_mode(p)) {
+    case EM_DGEGLU: store_out4_m<EM_DGEGLU>(p, cofs, rofs, m, n, acc); break;
+    case EM_DACT: store_out4_m<EM_DACT>(p, cofs, rofs, m, n, acc); break;
+    case EM_F32: store_out4_m<EM_F32>(p, cofs, rofs, m, n, acc); break;
+    default: store_out4_m<EM_BF16>(p, cofs, rofs, m, n, acc); break;
   }
 }
 
@@ -333,13 +514,16 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
     }
     return;
   }
+  epi_dispatch(p, [&](auto em) {
+    constexpr int EM = decltype(em)::value;
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
+    for (int i = 0; i < MI; ++i) {
+      const int64_t m = m0 + wm * (BM / WM) + i * 16 + (lane & 15);
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      store_out4(p, cofs, rofs, m, n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4), acc[i][j]);
-  }
+      for (int j = 0; j < NI; ++j)
+        store_out4_m<EM>(p, cofs, rofs, m, n0 + wn * (BN / WN) + j * 16 + 4 * (lane >> 4), acc[i][j]);
+    }
+  });
 }
 
 // split-K second pass: C = epilogue(sum_z ws[z]) -- one thread per (row, 4 columns)
@@ -544,12 +728,16 @@ __global__ void __launch_bounds__(NT2, 1) gemm256_kernel(GemmP p) {
         store_geglu4(p, cofs, m, n0 + wn * 64 + j * 16 + 4 * (lane >> 4), acc[i][j], acc[i][j + NI / 2]);
     }
   } else {
+    epi_dispatch(p, [&](auto em) {
+      constexpr int EM = decltype(em)::value;
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
+      for (int i = 0; i < MI; ++i) {
+        const int64_t m = m0 + wm * 64 + i * 16 + (lane & 15);
 #pragma unroll
-      for (int j = 0; j < NI; ++j) store_out4(p, cofs, rofs, m, n0 + wn * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
-    }
+        for (int j = 0; j < NI; ++j)
+          store_out4_m<EM>(p, cofs, rofs, m, n0 + wn * 128 + j * 16 + 4 * (lane >> 4), acc[i][j]);
+      }
+    });
   }
 }
 
@@ -655,21 +843,186 @@ __device__ __forceinline__ bf16x8 frag_tr_asm(const char* lds, int rb, int kk, i
 
 // 8-phase epilogue: wave (wr, wc) owns rows wr*128 + 16*rb + (lane & 15) and columns
 // wc*64 + 16*cb + 4*(lane >> 4) .. +3 (GeGLU: gate cb = 0,1 with up cb + 2 of the same column)
+// ---- 8-phase epilogue -------------------------------------------------------
+// Wave (wr, wc) owns rows wr*128 + 16*rb + (lane & 15) and columns wc*64 + 16*cb + 4*(lane >> 4) .. +3
+// (GeGLU: gate cb = 0,1 with up cb + 2 of the same column).  Interior tiles (the vast majority)
+// take a lean path per epilogue class: no bounds checks, row pointers stepped by 16 rows, and the
+// side inputs (residual / old C / saved activations) of row block rb + 1 loaded before the stores
+// of row block rb, so their latency overlaps the stores (vmcnt retires the older loads first).
+// Edge tiles use the general per-group store_out4_rt.
+enum FastMode { FM_STORE = 0, FM_BF16 = 1, FM_F32 = 2, FM_DACT = 3, FM_DGEGLU = 4 };
+
+__device__ __forceinline__ int fast_mode(const GemmP& p) {
+  if (p.epi == PZ_EPI_DGEGLU) return FM_DGEGLU;
+  if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) return FM_DACT;
+  if (p.c_fp32) return FM_F32;
+  if (!p.resid && !p.beta && p.epi == PZ_EPI_NONE) return FM_STORE;
+  return FM_BF16;
+}
+
+__device__ __forceinline__ u32x2 pk4(const float (&v)[4]) {
+  return u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+}
+
+template <int FM>
+__device__ __forceinline__ void epi8p_fast(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t nb,
+                                           const f32x4 (&acc)[8][4]) {
+  const float alpha = p.alpha;
+  const int64_t crow = 16 * p.ldc;
+  float bias[4][4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    if (FM <= FM_F32 && p.bias) {
+      unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias[cb]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias[cb][r] = 0.f;
+    }
+  }
+  if constexpr (FM == FM_STORE) {
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + nb;
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * alpha + bias[cb][r];
+        *reinterpret_cast<u32x2*>(C + rb * crow + cb * 16) = pk4(v);
+      }
+    }
+  } else if constexpr (FM == FM_F32) {
+    float* C = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + nb;
+    const bf16_t* R = p.resid ? p.resid + rofs + m * p.ld_resid + nb : nullptr;
+    const int64_t rrow = 16 * p.ld_resid;
+    const bool ld = p.beta || R;
+    f32x4 side[2][4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      side[0][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      side[1][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    auto load = [&](int rb, f32x4 (&d)[4]) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        if (p.beta) {
+          d[cb] = *reinterpret_cast<const f32x4*>(C + rb * crow + cb * 16);
+        } else {
+          float x[4];
+          unpack4(*reinterpret_cast<const u32x2*>(R + rb * rrow + cb * 16), x);
+          d[cb] = f32x4{x[0], x[1], x[2], x[3]};
+        }
+      }
+    };
+    if (ld) load(0, side[0]);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      if (ld && rb + 1 < 8) load(rb + 1, side[(rb + 1) & 1]);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        f32x4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * alpha + bias[cb][r] + side[rb & 1][cb][r];
+        *reinterpret_cast<f32x4*>(C + rb * crow + cb * 16) = v;
+      }
+    }
+  } else {
+    // bf16 output with side inputs: FM_BF16 (resid and/or old C, optional GELU/SILU with saved
+    // pre-activation), FM_DACT (aux = pre-activation), FM_DGEGLU (aux = [g | u], two outputs)
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + nb;
+    const bool aux_in = FM == FM_DACT || FM == FM_DGEGLU;
+    const bf16_t* X0 = aux_in ? p.aux + m * p.ld_aux + nb : (p.beta ? C : nullptr);
+    const int64_t x0row = aux_in ? 16 * p.ld_aux : crow;
+    const bf16_t* X1 = FM == FM_DGEGLU ? X0 + p.geglu_I : (FM == FM_BF16 && p.resid ? p.resid + rofs + m * p.ld_resid + nb : nullptr);
+    const int64_t x1row = FM == FM_DGEGLU ? x0row : 16 * p.ld_resid;
+    u32x2 s0[2][4], s1[2][4];
+    auto load = [&](int rb, u32x2 (&d0)[4], u32x2 (&d1)[4]) {
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        d0[cb] = X0 ? *reinterpret_cast<const u32x2*>(X0 + rb * x0row + cb * 16) : u32x2{0u, 0u};
+        d1[cb] = X1 ? *reinterpret_cast<const u32x2*>(X1 + rb * x1row + cb * 16) : u32x2{0u, 0u};
+      }
+    };
+    load(0, s0[0], s1[0]);
+    const bool act = FM == FM_BF16 && (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU);
+    const bool gelu = p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_DGELU;
+    bf16_t* Aux = act && p.aux ? p.aux + m * p.ld_aux + nb : nullptr;
+    const int64_t arow = 16 * p.ld_aux;
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      if (rb + 1 < 8) load(rb + 1, s0[(rb + 1) & 1], s1[(rb + 1) & 1]);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        float v[4], x0[4], x1[4];
+        unpack4(s0[rb & 1][cb], x0);
+        unpack4(s1[rb & 1][cb], x1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * alpha;
+        bf16_t* Cp = C + rb * crow + cb * 16;
+        if constexpr (FM == FM_DGEGLU) {
+          float dg[4], du[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dg[r] = v[r] * x1[r] * gelu_tanh_grad(x0[r]);
+            du[r] = v[r] * gelu_tanh(x0[r]);
+          }
+          *reinterpret_cast<u32x2*>(Cp) = pk4(dg);
+          *reinterpret_cast<u32x2*>(Cp + p.geglu_I) = pk4(du);
+        } else if constexpr (FM == FM_DACT) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] *= gelu ? gelu_tanh_grad(x0[r]) : silu_grad(x0[r]);
+          *reinterpret_cast<u32x2*>(Cp) = pk4(v);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += bias[cb][r];
+          if (act) {
+            if (Aux) *reinterpret_cast<u32x2*>(Aux + rb * arow + cb * 16) = pk4(v);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = gelu ? gelu_tanh(v[r]) : silu(v[r]);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += x1[r] + x0[r];  // resid, old C (zeros when absent)
+          *reinterpret_cast<u32x2*>(Cp) = pk4(v);
+        }
+      }
+    }
+  }
+}
+
 template <bool GEGLU>
 __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
-                                           int wr, int wc, int lane, const f32x4 (&acc)[8][4]) {
+                                           int wr, int wc, int lane, const f32x4 (&acc)[8][4], char* smem) {
+  if (GEGLU) {  // stores only
 #pragma unroll
-  for (int rb = 0; rb < 8; ++rb) {
-    const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
-    if (GEGLU) {
+    for (int rb = 0; rb < 8; ++rb) {
+      const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + 4 * (lane >> 4), acc[rb][j], acc[rb][2 + j]);
-    } else {
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-        store_out4(p, cofs, rofs, m, n0 + wc * 64 + cb * 16 + 4 * (lane >> 4), acc[rb][cb]);
     }
+    return;
+  }
+  const int64_t m = m0 + wr * 128 + (lane & 15), nb = n0 + wc * 64 + 4 * (lane >> 4);
+  if (m0 + BT <= p.M && n0 + BT <= p.N) {
+    switch (fast_mode(p)) {
+      case FM_STORE: epi8p_fast<FM_STORE>(p, cofs, rofs, m, nb, acc); break;
+      case FM_F32: epi8p_fast<FM_F32>(p, cofs, rofs, m, nb, acc); break;
+      case FM_DACT: epi8p_fast<FM_DACT>(p, cofs, rofs, m, nb, acc); break;
+      case FM_DGEGLU: epi8p_fast<FM_DGEGLU>(p, cofs, rofs, m, nb, acc); break;
+      default: epi8p_fast<FM_BF16>(p, cofs, rofs, m, nb, acc); break;
+    }
+    return;
+  }
+  // edge tile: park each half of the wave's accumulators in its own 16 KiB of the (now idle) LDS
+  // and run ONE runtime-general group store in a rolled loop (lane-private slots: no barrier)
+  f32x4* park = reinterpret_cast<f32x4*>(smem) + (wr * 4 + wc) * 1024 + lane;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) park[g * 64] = acc[half * 4 + (g >> 2)][g & 3];
+#pragma unroll 1
+    for (int g = 0; g < 16; ++g)
+      store_out4_rt(p, cofs, rofs, m + (half * 4 + (g >> 2)) * 16, nb + (g & 3) * 16, park[g * 64]);
   }
 }
 
@@ -892,7 +1245,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
       for (int cb = 0; cb < 4; ++cb) W[(rb * 4 + cb) * NT2 + t] = acc[rb][cb];
     return;
   }
-  epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc);
+  epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc, smem);
 }
 
 // Split tail, second pass: 16 blocks of 512 threads per leftover tile (one accumulator row-block rb and
@@ -1194,7 +1547,7 @@ Plan make_plan(const pz_gemm_args* a) {
   pl.geglu = a->epilogue == PZ_EPI_GEGLU;
   const int64_t ncols = pl.geglu ? a->geglu_inter : a->N;
   // skinny path: few rows, weights streamed once (inference denoise / proprio rows)
-  if (a->M <= 16 && pl.akc && pl.bkc && a->K % 32 == 0 && !a->c_fp32) {
+  if (a->M <= 16 && pl.akc && pl.bkc && a->K % 32 == 0 && !a->c_fp32 && a->epilogue < PZ_EPI_DGELU) {
     const int64_t kch = a->K / 32;
     pl.kind = PATH_SKINNY;
     pl.skinny_w = kch >= 64 ? 16 : (kch >= 32 ? 8 : 4);
@@ -1351,6 +1704,16 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   }
   if (a->epilogue == PZ_EPI_GELU || a->epilogue == PZ_EPI_SILU)
     PZ_CHECK_ARG(a->batch == 1, "pz_gemm: activation epilogue is unbatched");
+  PZ_CHECK_ARG(a->epilogue >= PZ_EPI_NONE && a->epilogue <= PZ_EPI_DGEGLU, "pz_gemm: unknown epilogue %d",
+               (int)a->epilogue);
+  PZ_CHECK_ARG(!(a->c_fp32 && a->beta_accum && a->resid), "pz_gemm: fp32 beta accumulation takes no resid");
+  if (a->epilogue >= PZ_EPI_DGELU) {
+    PZ_CHECK_ARG(a->batch == 1 && a->aux && !a->bias && !a->resid && !a->beta_accum && !a->c_fp32,
+                 "pz_gemm: backward epilogues read aux, write bf16 C, unbatched, no bias/resid/beta");
+    if (a->epilogue == PZ_EPI_DGEGLU)
+      PZ_CHECK_ARG(a->geglu_inter == a->N && a->ldc >= 2 * a->N && a->ld_aux >= 2 * a->N,
+                   "pz_gemm: DGEGLU needs N == geglu_inter and [*, 2I] aux / C rows");
+  }
   if (a->aux) PZ_CHECK_ARG(a->ld_aux % 4 == 0 && PZ_ALIGNED(a->aux, 8), "pz_gemm: aux alignment");
   PZ_CHECK_ARG(a->ws_bytes >= 0, "pz_gemm: negative ws_bytes");
 

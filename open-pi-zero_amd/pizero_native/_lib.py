@@ -12,8 +12,9 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 2  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 3  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
+PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 
 i64, i32, f32, vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
 fp = C.POINTER(C.c_float)

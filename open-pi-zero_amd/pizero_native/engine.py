@@ -30,7 +30,7 @@ from dataclasses import dataclass
 import torch
 
 from . import ops
-from .ops import PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_SILU
+from .ops import PZ_EPI_DGEGLU, PZ_EPI_DGELU, PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_SILU
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -255,7 +255,7 @@ class Engine:
             xn = torch.empty_like(x)
             ops.linear(g1, self.w(p + "mlp.fc2.weight"), xn, bias=self.w(p + "mlp.fc2.bias"), resid=xm)
             if save is not None:
-                st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, P=Pm, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1)
+                st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, P=Pm, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1, g1=g1)
                 layers.append(st)
             x = xn
         y = torch.empty_like(x)
@@ -295,7 +295,6 @@ class Engine:
         Np = d.n_img
         W3 = 3 * d.vH
         dg = torch.empty(M, d.vI, device=dev, dtype=BF16)
-        g1 = torch.empty(M, d.vI, device=dev, dtype=BF16)
         dP = torch.empty(B * nh, Np, Np, device=dev, dtype=F32)
         dS = torch.empty(B * nh, Np, Np, device=dev, dtype=BF16)
         dqkv = torch.empty(M, W3, device=dev, dtype=BF16)
@@ -306,10 +305,11 @@ class Engine:
             p = f"{vt}encoder.layers.{i}."
             st = sv["layers"][i]
             # MLP: x' = xm + fc2(gelu(fc1(ln2(xm))))
-            ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg)
-            ops.act_bwd(dg, st["a1"], dg, g1, PZ_EPI_GELU)
+            # dgrad through fc2 with the GELU derivative fused into its epilogue (saved pre-activation a1)
+            ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg, epi=PZ_EPI_DGELU, aux=st["a1"])
             if self.rg(p + "mlp.fc2.weight"):
-                ops.linear_wgrad(dx, g1, self.gw(p + "mlp.fc2.weight"), beta=beta)
+                ops.linear_wgrad(dx, st["g1"], self.gw(p + "mlp.fc2.weight"), beta=beta)
+            st["g1"] = None
             if self.rg(p + "mlp.fc2.bias"):
                 ops.colsum(dx, self.gw(p + "mlp.fc2.bias"), ws, beta=beta)
             if self.rg(p + "mlp.fc1.weight"):
@@ -465,7 +465,7 @@ class Engine:
                 ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU, aux=gu)
                 xn = torch.empty_like(x)
                 ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
-                gs.update(O=O, xm=xm, h2=h2, r2=r2, gu=gu, skip=False)
+                gs.update(O=O, xm=xm, h2=h2, r2=r2, gu=gu, hm=hm, skip=False)
                 X[g.name] = xn
             layers.append(st)
         save["joint"] = layers
@@ -496,14 +496,13 @@ class Engine:
                 M = dx.shape[0]
                 part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
                 # MLP
-                dhm = torch.empty(M, g.inter, device=dev, dtype=BF16)
-                ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dhm)
-                hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+                # dgrad through down_proj with the GeGLU derivative fused into its epilogue:
+                # gu (saved g|u) <- d(gate|up) in place; hm (saved GeGLU output) feeds the down_proj wgrad
                 gu = gs["gu"]
-                ops.geglu_bwd(dhm, gu, gu, hm, M, g.inter)  # gu <- d(gate|up), hm <- recomputed
+                ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), gu, epi=PZ_EPI_DGEGLU, aux=gu)
                 if self.rg(p + "mlp.down_proj.weight"):
-                    ops.linear_wgrad(dx, hm, self.gw(p + "mlp.down_proj.weight"), beta=beta)
-                del hm, dhm
+                    ops.linear_wgrad(dx, gs["hm"], self.gw(p + "mlp.down_proj.weight"), beta=beta)
+                gs["hm"] = None
                 if self.rg(p + "mlp.gate_proj.weight") and self.rg(p + "mlp.up_proj.weight"):
                     ops.linear_wgrad(gu, gs["h2"], self.ar.grad_span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"),
                                      beta=beta)

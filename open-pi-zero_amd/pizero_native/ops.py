@@ -12,6 +12,9 @@ import ctypes as C
 import torch
 
 from ._lib import (
+    PZ_EPI_DGEGLU,
+    PZ_EPI_DGELU,
+    PZ_EPI_DSILU,
     PZ_EPI_GEGLU,
     PZ_EPI_GELU,
     PZ_EPI_NONE,
@@ -23,7 +26,7 @@ from ._lib import (
     lib,
 )
 
-__all__ = ["PZ_EPI_NONE", "PZ_EPI_GELU", "PZ_EPI_GEGLU", "PZ_EPI_SILU"]
+__all__ = ["PZ_EPI_NONE", "PZ_EPI_GELU", "PZ_EPI_GEGLU", "PZ_EPI_SILU", "PZ_EPI_DGELU", "PZ_EPI_DSILU", "PZ_EPI_DGEGLU"]
 
 BF16 = torch.bfloat16
 
@@ -132,12 +135,17 @@ def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha
     return out
 
 
-def linear_dgrad(dy, W, dx, *, beta=False, resid=None):
-    """dx[M,K] (+)= dy[M,N] @ W[N,K] (+ resid)."""
+def linear_dgrad(dy, W, dx, *, beta=False, resid=None, epi=PZ_EPI_NONE, aux=None):
+    """dx[M,K] (+)= dy[M,N] @ W[N,K] (+ resid).
+
+    Backward epilogues (aux read): PZ_EPI_DGELU / PZ_EPI_DSILU multiply by the activation
+    derivative at the saved pre-activation aux[M,K]; PZ_EPI_DGEGLU takes aux = saved [g | u]
+    ([M, 2K]) and writes d(gate|up) into dx[M, 2K] (dx may be aux itself)."""
     M, N = dy.shape
     K = W.shape[1]
     gemm(M, K, N, dy, dy.stride(0), True, W, W.stride(0), False, dx, dx.stride(0), beta=beta,
-         resid=resid, ld_resid=0 if resid is None else resid.stride(0))
+         resid=resid, ld_resid=0 if resid is None else resid.stride(0), epi=epi, aux=aux,
+         ld_aux=0 if aux is None else aux.stride(0), geglu_inter=K if epi == PZ_EPI_DGEGLU else 0)
     return dx
 
 

@@ -170,6 +170,32 @@ def test_wgrad_small_output_uses_split_tail():
     close(dW, dy.float().t() @ x.float(), atol=5e-2)
 
 
+@pytest.mark.parametrize("M", [4, 700, 17664])
+def test_backward_activation_epilogues(M):
+    """dgrad GEMMs with the activation derivative fused (DGELU / DSILU from the saved pre-activation,
+    DGEGLU from saved [g | u] written back in place) vs torch autograd of the same ops in fp32."""
+    from pizero_native import ops
+
+    I, H = 1024, 512
+    dy = bf(M, H, scale=0.5)
+    W = bf(H, I, scale=I ** -0.5)  # next layer's weight [out=H, in=I]
+    pre = bf(M, I)
+    for epi, f in ((ops.PZ_EPI_DGELU, lambda x: torch.nn.functional.gelu(x, approximate="tanh")),
+                   (ops.PZ_EPI_DSILU, torch.nn.functional.silu)):
+        x = pre.float().requires_grad_()
+        f(x).backward(dy.float() @ W.float())
+        out = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+        ops.linear_dgrad(dy, W, out, epi=epi, aux=pre)
+        close(out, x.grad, atol=2e-2)
+    gu = bf(M, 2 * I)
+    g, u = (t.float().requires_grad_() for t in (gu[:, :I], gu[:, I:]))
+    (torch.nn.functional.gelu(g, approximate="tanh") * u).backward(dy.float() @ W.float())
+    buf = gu.clone()
+    ops.linear_dgrad(dy, W, buf, epi=ops.PZ_EPI_DGEGLU, aux=buf)  # in place over the saved g|u
+    close(buf[:, :I], g.grad, atol=2e-2)
+    close(buf[:, I:], u.grad, atol=2e-2)
+
+
 def test_epilogues_gelu_resid_geglu_silu():
     from pizero_native import ops
 

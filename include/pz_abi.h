@@ -149,6 +149,42 @@ int pz_attn_softmax(const pz_softmax_args* a, void* stream);
 int pz_attn_softmax_bwd(const void* P, const float* dP, int64_t lddp, const void* tcap, void* dS,
                         int64_t ldp, int64_t R, int64_t N, float scale, float cap, void* stream);
 
+/* Fused (flash) attention, the two Pi0 shapes (no L x L tensor in HBM; see csrc/pz_flash.hip):
+ *   SigLIP (siglip.py:108-166): H = 16 heads x head_dim 72 per sample, no mask;
+ *   joint (joint_model.py:130-304): H = 1, MQA with the 8 query heads stacked as rows
+ *     (r = token*8 + head), one K/V head of 256, soft-cap + Pi0 block mask (pizero.py:271-306).
+ * Unit z = b*H + h.  Q row r: q + b*q_bstride + h*q_hstride + r*ldq (K, V alike; dQ/dK/dV use the
+ * q/k/v strides).  O / dO row r lives in the output group i with g_row0[i] <= r (< g_row0[i+1]):
+ * g_o[i] + b*g_bstride[i] + (r - g_row0[i])*g_ld[i] + h*o_hstride (dO: g_do[i], same layout).
+ * logits = cap*tanh(scale*q.k/cap) (cap 0: scale*q.k); mask_mode 1: token t = r / rows_per_token
+ * sees keys per the Pi0 block mask of cnt[b] (pad rows t in [cnt, prefix) attend uniformly).
+ * lse: fp32 [Z*H][nq] log-sum-exp per row (written by fwd, read by bwd).  delta: fp32 [Z*H][nq]
+ * rowsum(dO*O) (written by pz_flash_bwd_prep).  Deterministic (no atomics). */
+typedef struct pz_flash_args {
+  int64_t Z, H, nq, nk, head_dim;
+  const void* q; int64_t ldq, q_bstride, q_hstride;
+  const void* k; int64_t ldk, k_bstride, k_hstride;
+  const void* v; int64_t ldv, v_bstride, v_hstride;
+  int32_t n_groups;
+  int64_t g_row0[3];
+  void* g_o[3];
+  int64_t g_bstride[3], g_ld[3];
+  int64_t o_hstride;
+  float* lse;
+  float scale, cap;
+  int32_t mask_mode;
+  const int32_t* cnt; int64_t prefix, cond, rows_per_token;
+  /* backward */
+  const void* g_do[3];
+  float* delta;
+  void* dq; void* dk; void* dv;
+} pz_flash_args;
+int pz_flash_fwd(const pz_flash_args* a, void* stream);
+/* delta[z][r] = sum_d dO[r][d] * O[r][d] (fp32) */
+int pz_flash_bwd_prep(const pz_flash_args* a, void* stream);
+/* dQ and delta (query-parallel), then dK, dV (key-parallel over all query rows of the unit); overwrite */
+int pz_flash_bwd(const pz_flash_args* a, void* stream);
+
 /* SigLIP patch embed im2col (siglip.py:42-48,69-74): pixels bf16 [B,3,H,W] -> cols bf16
  * [B*(H/ps)*(W/ps), ldc] with k = c*ps*ps + ky*ps + kx, zero pad k in [3*ps*ps, ldc) */
 int pz_patchify(const void* pix, void* cols, int64_t B, int64_t H, int64_t W, int64_t ps, int64_t ldc,

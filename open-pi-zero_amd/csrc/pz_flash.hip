@@ -1,0 +1,727 @@
+// Fused (flash) attention for the two attention shapes of the Pi0 path, forward and backward:
+//
+//   * SigLIP self-attention (siglip.py:108-166): 16 heads x 72, 256 tokens, no mask, fp32 softmax;
+//     Q/K/V read in place from the fused q|k|v projection output, O written in place for out_proj.
+//   * the joint mixture attention (joint_model.py:130-304): MQA with ONE shared K/V head of 256 and
+//     the 8 query heads stacked as rows (row r = token * 8 + head, no repeat_kv copy), Gemma
+//     soft-cap 50*tanh(s/50) (joint_model.py:265-268) and the Pi0 block mask regenerated from the
+//     per-sample prefix count (pizero.py:271-306); O rows are scattered straight into the per-
+//     mixture buffers that feed each mixture's o_proj.
+//
+// Nothing of size L x L touches HBM: the forward keeps S/P in registers and saves one fp32
+// log-sum-exp per query row; the backward recomputes P from it.  K/V (forward) and Q/dO
+// (backward) tiles are staged in LDS; MFMA v_mfma_f32_16x16x32_bf16 throughout.
+//
+// Orientation (per wave, 64-lane wave64): the forward computes S^T = K Q^T so each lane owns one
+// query column and 4 consecutive keys per 16x16 block; P^T then feeds O^T = V^T P^T directly as the
+// B operand (no LDS round trip), with the MFMA k order permuted to keys {4g..4g+3, 16+4g..16+4g+3}
+// for lane group g and the matching V^T fragment fetched by two ds_read_b64_tr_b16 (4 keys each).
+// The backward mirrors it with S = Q K^T (key on the lane), so dV^T = dO^T P and dK^T = Q^T dS take
+// P / dS from registers and dO^T / Q^T through transposed LDS reads; dQ = dS K is a separate
+// query-parallel pass (no atomics: deterministic).
+#include "pz_common.h"
+
+namespace {
+
+constexpr int FA_KB = 64;   // keys per staged block (forward, dQ) / per dK-dV workgroup
+constexpr int FA_NW = 4;    // waves per workgroup (backward)
+constexpr int FA_QS = 32;   // query rows per staged step of the dK/dV pass
+
+template <int HD>
+struct FaDims {
+  static constexpr int HDK = (HD + 31) / 32 * 32;  // contraction over head_dim, in 32-steps
+  static constexpr int HDV = (HD + 15) / 16 * 16;  // head_dim as 16-wide output blocks
+  static constexpr int NKS = HDK / 32;
+  static constexpr int NDB = HDV / 16;
+  // LDS row stride (elements): >= HDK, 16-B rows, and chosen so the 4 rows of a transposed read
+  // land on disjoint banks (HD 256: 272 = 136 dwords = 8 mod 64; HD 72: 112; small test heads: HDK + 16)
+  static constexpr int ROW = HD == 256 ? 272 : (HD == 72 ? 112 : HDK + 16);
+  // forward geometry: 128 query rows per workgroup; HD 256 keeps one 16-row block per wave (8 waves,
+  // <= 256 registers so two workgroups share a CU and one stages while the other computes)
+  static constexpr int FNW = HD == 256 ? 8 : 4;
+  static constexpr int FNQB = HD == 256 ? 1 : 2;
+};
+
+__device__ __forceinline__ bool fa_allowed(int64_t i, int64_t j, int64_t cnt, int64_t P, int64_t C) {
+  if (i < P) return i < cnt && j < cnt;
+  if (i < P + C) return j < cnt || (j >= P && j < P + C);
+  return j < cnt || j >= P;
+}
+
+__device__ __forceinline__ s16x4 lds_tr4(const bf16_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+
+// V^T / dO^T / Q^T fragment for MFMA A (m = column c0 + (lane & 15), k-slot 8g + e) taken from a
+// row-major LDS tile T[row][col]: k-slots 0..3 <- rows r0 + 4g + e, 4..7 <- rows r0 + 16 + 4g + e.
+template <int ROW>
+__device__ __forceinline__ bf16x8 frag_tr(const bf16_t* T, int r0, int c0, int lane) {
+  const int g = lane >> 4, w = lane & 15, q = w >> 2, p = w & 3;
+  const s16x4 a = lds_tr4(T + (r0 + 4 * g + q) * ROW + c0 + 4 * p);
+  const s16x4 b = lds_tr4(T + (r0 + 16 + 4 * g + q) * ROW + c0 + 4 * p);
+  s16x8 o;
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+  o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+// row fragment (MFMA A with m = row, or B with n = row): T[r0 + (lane & 15)][c0 + 8g .. +7]
+template <int ROW>
+__device__ __forceinline__ bf16x8 frag_row(const bf16_t* T, int r0, int c0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(T + (r0 + (lane & 15)) * ROW + c0 + 8 * (lane >> 4));
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  s16x8 o;
+  const unsigned u0 = pack2bf(a[0], a[1]), u1 = pack2bf(a[2], a[3]);
+  const unsigned u2 = pack2bf(b[0], b[1]), u3 = pack2bf(b[2], b[3]);
+  o[0] = (short)(u0 & 0xffff); o[1] = (short)(u0 >> 16); o[2] = (short)(u1 & 0xffff); o[3] = (short)(u1 >> 16);
+  o[4] = (short)(u2 & 0xffff); o[5] = (short)(u2 >> 16); o[6] = (short)(u3 & 0xffff); o[7] = (short)(u3 >> 16);
+  return __builtin_bit_cast(bf16x8, o);
+}
+
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Register-staged prefetch of a ROWS x HD tile: load() issues the global loads of the NEXT tile
+// before the current tile's MFMAs, store() writes them to the other LDS buffer afterwards, so the
+// HBM/L2 latency hides behind the compute (one barrier per step).
+template <int HD, int ROW, int ROWS, int NT>
+struct TileStager {
+  static constexpr int CH = HD / 8, TOT = ROWS * CH, PER = (TOT + NT - 1) / NT;
+  u32x4 v[PER];
+  __device__ __forceinline__ void load(const bf16_t* src, int64_t ld, int64_t j0, int64_t n) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT, r = c / CH, ch = c % CH;
+      v[i] = u32x4{0u, 0u, 0u, 0u};
+      if (c < TOT && j0 + r < n) v[i] = *reinterpret_cast<const u32x4*>(src + (j0 + r) * ld + ch * 8);
+    }
+  }
+  // query-side rows [r0, r0 + ROWS) of Q (q strides) or dO (output-group layout)
+  __device__ __forceinline__ void load_q(const pz_flash_args& a, const bf16_t* Q, int64_t b, int64_t h, int64_t r0,
+                                         bool is_do);
+  __device__ __forceinline__ void store(bf16_t* T) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = threadIdx.x + i * NT, r = c / CH, ch = c % CH;
+      if (c < TOT) *reinterpret_cast<u32x4*>(T + r * ROW + ch * 8) = v[i];
+    }
+  }
+};
+
+// zero the padding columns [HD, PADTO) of a staged tile once (loads never write them)
+template <int HD, int PADTO, int ROW, int ROWS, int NT>
+__device__ __forceinline__ void zero_pad_cols(bf16_t* T) {
+  if constexpr (PADTO > HD) {
+    constexpr int CH = (PADTO - HD) / 8;
+    for (int c = threadIdx.x; c < ROWS * CH; c += NT) {
+      const int r = c / CH, ch = c % CH;
+      *reinterpret_cast<u32x4*>(T + r * ROW + HD + ch * 8) = u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+}
+
+struct FaRow {  // where O / dO row r of unit (b, h) lives
+  const pz_flash_args* a;
+  __device__ __forceinline__ int grp(int64_t r) const {
+    int gi = 0;
+    for (int i = 1; i < a->n_groups; ++i)
+      if (r >= a->g_row0[i]) gi = i;
+    return gi;
+  }
+  __device__ __forceinline__ int64_t off(int64_t b, int64_t h, int64_t r, int gi) const {
+    return b * a->g_bstride[gi] + (r - a->g_row0[gi]) * a->g_ld[gi] + h * a->o_hstride;
+  }
+};
+
+template <int HD, int ROW, int ROWS, int NT>
+__device__ __forceinline__ void TileStager<HD, ROW, ROWS, NT>::load_q(const pz_flash_args& a, const bf16_t* Q,
+                                                                      int64_t b, int64_t h, int64_t r0, bool is_do) {
+  const FaRow fr{&a};
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = threadIdx.x + i * NT, rr = c / CH, ch = c % CH;
+    const int64_t r = r0 + rr;
+    v[i] = u32x4{0u, 0u, 0u, 0u};
+    if (c < TOT && r < a.nq) {
+      const bf16_t* src;
+      if (is_do) {
+        const int gi = fr.grp(r);
+        src = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
+      } else {
+        src = Q + r * a.ldq;
+      }
+      v[i] = *reinterpret_cast<const u32x4*>(src + ch * 8);
+    }
+  }
+}
+
+// Mask / logit context in 32-bit registers (token of a query row by a float reciprocal: exact for
+// nq < 2^22, checked on the host) -- no 64-bit division in the inner loops
+struct FaMask {
+  int mode, nk, P, C, cnt;
+  float inv_rpt, scale, cap, inv_cap;
+  __device__ __forceinline__ FaMask(const pz_flash_args& a, int64_t b) {
+    mode = a.mask_mode;
+    nk = (int)a.nk;
+    P = (int)a.prefix;
+    C = (int)a.cond;
+    cnt = mode == 1 ? a.cnt[b] : 0;
+    inv_rpt = mode == 1 ? 1.f / (float)a.rows_per_token : 0.f;
+    scale = a.scale;
+    cap = a.cap;
+    inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
+  }
+  __device__ __forceinline__ int token(int r) const { return (int)(((float)r + 0.5f) * inv_rpt); }
+  __device__ __forceinline__ bool dead(int t) const { return mode == 1 && t < P && t >= cnt; }
+  __device__ __forceinline__ bool allowed(int t, int j) const {
+    if (j >= nk) return false;
+    if (mode != 1) return true;
+    if (t < P) return t < cnt && j < cnt;
+    if (t < P + C) return j < cnt || (j >= P && j < P + C);
+    return j < cnt || j >= P;
+  }
+};
+
+// logits with soft-cap and mask for key j of a query row of token t; dead rows (pad tokens of the
+// prefix, pizero.py:291: finfo.min absorbs s) attend uniformly to every key
+__device__ __forceinline__ float fa_logit(const FaMask& mk, float s, int t, int j) {
+  if (j >= mk.nk) return -INFINITY;
+  if (mk.dead(t)) return 0.f;
+  if (!mk.allowed(t, j)) return -INFINITY;
+  float x = s * mk.scale;
+  if (mk.cap > 0.f) x = mk.cap * tanh_fast(x * mk.inv_cap);
+  return x;
+}
+
+// ------------------------------------------------------------------ forward --
+// grid (ceil(nq / 128), Z * H), FNW waves: wave w owns query rows q0 + 16*FNQB*w .. + 16*FNQB - 1
+template <int HD>
+__global__ void __launch_bounds__(FaDims<HD>::FNW * 64) flash_fwd_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NQB = D::FNQB, NT = D::FNW * 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks2[2][FA_KB * D::ROW];  // double-buffered K / V tiles
+  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][FA_KB * D::ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.y, b = zh / a.H, h = zh % a.H;
+  const int64_t q0 = (int64_t)blockIdx.x * (D::FNW * 16 * NQB) + wave * 16 * NQB;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
+    zero_pad_cols<HD, D::HDV, D::ROW, FA_KB, NT>(Vs2[bi]);
+  }
+  TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
+  stk.load(K, a.ldk, 0, a.nk);
+  stv.load(V, a.ldv, 0, a.nk);
+
+  // Q^T fragments (B operand: k = head dim, n = query) straight from HBM, zero past HD / nq
+  bf16x8 qf[NQB][D::NKS];
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb) {
+    const int64_t r = q0 + qb * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      qf[qb][ks] = (r < a.nq && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+    }
+  }
+  f32x4 o[D::NDB][NQB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db)
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[NQB], l[NQB];
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb) {
+    m[qb] = -INFINITY;
+    l[qb] = 0.f;
+  }
+
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();  // pad columns zeroed
+  stk.store(Ks2[0]);
+  stv.store(Vs2[0]);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Ks2[kb & 1];
+    const bf16_t* Vs = Vs2[kb & 1];
+    const bool more = kb + 1 < nkb;
+    if (more) {  // next K/V tile in flight during this tile's MFMAs
+      stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
+      stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+    }
+    // S^T[key][q] for 64 keys x 16*NQB queries
+    f32x4 s[4][NQB];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int qb = 0; qb < NQB; ++qb) s[i][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 kf = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) s[i][qb] = mfma(kf, qf[qb][ks], s[i][qb]);
+      }
+    // logits, online softmax (each lane: one query column, 16 of the block's 64 keys)
+    bf16x8 pf[2][NQB];  // [k-step of 32 keys][query block]
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) {
+      const int t = mk.token((int)(q0 + qb * 16 + (lane & 15)));
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = kb * FA_KB + i * 16 + 4 * g + e;
+          const float x = fa_logit(mk, s[i][qb][e], t, j);
+          s[i][qb][e] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qb], mx);
+      const float alpha = mn == -INFINITY ? 1.f : __expf(m[qb] - mn);
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float p = mn == -INFINITY ? 0.f : __expf(s[i][qb][e] - mn);
+          s[i][qb][e] = p;
+          sum += p;
+        }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      l[qb] = l[qb] * alpha + sum;
+      m[qb] = mn;
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) o[db][qb] *= alpha;
+      pf[0][qb] = pack8(s[0][qb], s[1][qb]);
+      pf[1][qb] = pack8(s[2][qb], s[3][qb]);
+    }
+    // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) {
+        const bf16x8 vf = frag_tr<D::ROW>(Vs, k2 * 32, db * 16, lane);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) o[db][qb] = mfma(vf, pf[k2][qb], o[db][qb]);
+      }
+    if (more) {
+      stk.store(Ks2[(kb + 1) & 1]);
+      stv.store(Vs2[(kb + 1) & 1]);
+    }
+    __syncthreads();
+  }
+  // O[r][d..d+3] = O^T / l; lse
+  const FaRow fr{&a};
+#pragma unroll
+  for (int qb = 0; qb < NQB; ++qb) {
+    const int64_t r = q0 + qb * 16 + (lane & 15);
+    if (r >= a.nq) continue;
+    const float inv = l[qb] > 0.f ? 1.f / l[qb] : 0.f;
+    const int gi = fr.grp(r);
+    bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD)
+        *reinterpret_cast<u32x2*>(O + d) =
+            u32x2{pack2bf(o[db][qb][0] * inv, o[db][qb][1] * inv), pack2bf(o[db][qb][2] * inv, o[db][qb][3] * inv)};
+    }
+    if (g == 0 && a.lse) a.lse[zh * a.nq + r] = m[qb] + __logf(l[qb]);
+  }
+}
+
+// ----------------------------------------------------------------- backward --
+// logit x of raw score s and dx/ds (scale, soft-cap); masked -> x = -inf
+struct FaLogit {
+  float x, dxds;
+};
+__device__ __forceinline__ FaLogit fa_logit_d(const FaMask& mk, float s, int t, int j) {
+  FaLogit o{-INFINITY, 0.f};
+  const bool dead = mk.dead(t);
+  if (j >= mk.nk || (!dead && !mk.allowed(t, j))) return o;
+  float x = s * mk.scale, d = mk.scale;
+  if (mk.cap > 0.f) {
+    const float th = tanh_fast(x * mk.inv_cap);
+    x = mk.cap * th;
+    d *= 1.f - th * th;
+  }
+  o.x = dead ? 0.f : x;  // dead rows: finfo.min absorbed the value, autograd still passes through
+  o.dxds = d;
+  return o;
+}
+
+// delta[z][r] = sum_d dO[r][d] O[r][d]: one wave per row
+template <int HD>
+__global__ void __launch_bounds__(256) flash_bwd_prep_kernel(pz_flash_args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.Z * a.H * a.nq) return;
+  const int64_t zh = row / a.nq, r = row % a.nq, b = zh / a.H, h = zh % a.H;
+  const FaRow fr{&a};
+  const int gi = fr.grp(r);
+  const int64_t off = fr.off(b, h, r, gi);
+  const bf16_t* O = (const bf16_t*)a.g_o[gi] + off;
+  const bf16_t* dO = (const bf16_t*)a.g_do[gi] + off;
+  float acc = 0.f;
+  for (int d = lane * 4; d < HD; d += 256) {
+    float x[4], y[4];
+    const u32x2 u = *reinterpret_cast<const u32x2*>(O + d), w = *reinterpret_cast<const u32x2*>(dO + d);
+    x[0] = __uint_as_float(u[0] << 16); x[1] = __uint_as_float(u[0] & 0xffff0000u);
+    x[2] = __uint_as_float(u[1] << 16); x[3] = __uint_as_float(u[1] & 0xffff0000u);
+    y[0] = __uint_as_float(w[0] << 16); y[1] = __uint_as_float(w[0] & 0xffff0000u);
+    y[2] = __uint_as_float(w[1] << 16); y[3] = __uint_as_float(w[1] & 0xffff0000u);
+    acc += x[0] * y[0] + x[1] * y[1] + x[2] * y[2] + x[3] * y[3];
+  }
+  acc = warp_sum(acc);
+  if (lane == 0) a.delta[zh * a.nq + r] = acc;
+}
+
+// dK, dV: grid (ceil(nk / 64), Z * H), 4 waves; wave w owns keys kb*64 + 16w + (lane & 15) and
+// sweeps every query row of the unit in staged steps of 32 (Q, dO, lse, delta in LDS)
+template <int HD>
+__global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FA_NW * 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Qs2[2][FA_QS * D::ROW];  // double-buffered Q / dO steps
+  __shared__ __attribute__((aligned(16))) bf16_t Ds2[2][FA_QS * D::ROW];
+  __shared__ float lse2[2][FA_QS], del2[2][FA_QS];
+  __shared__ __attribute__((aligned(16))) bf16_t Kk[FA_KB * D::ROW];  // this workgroup's 64 keys / values
+  __shared__ __attribute__((aligned(16))) bf16_t Vk[FA_KB * D::ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.y, b = zh / a.H, h = zh % a.H;
+  const int k0 = blockIdx.x * FA_KB;
+  const int key = k0 + wave * 16 + (lane & 15);
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {  // row reads reach HDK, transposed reads HDV <= HDK
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Qs2[bi]);
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Ds2[bi]);
+  }
+  TileStager<HD, D::ROW, FA_QS, NT> stq, std_;
+  stq.load_q(a, Q, b, h, 0, false);
+  std_.load_q(a, Q, b, h, 0, true);
+  float lse_v = 0.f, del_v = 0.f;  // threads < FA_QS carry one row's lse / delta
+  auto load_rows = [&](int64_t r0) {
+    const int64_t rr = r0 + threadIdx.x;
+    lse_v = threadIdx.x < FA_QS && rr < a.nq ? a.lse[zh * a.nq + rr] : 0.f;
+    del_v = threadIdx.x < FA_QS && rr < a.nq ? a.delta[zh * a.nq + rr] : 0.f;
+  };
+  load_rows(0);
+  // this workgroup's keys / values, read as B operands (n = key, k = head dim) from LDS:
+  // K for S = Q K^T, V for dP = dO V^T (in LDS rather than registers: the accumulators need them)
+  zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Kk);
+  zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vk);
+  {
+    TileStager<HD, D::ROW, FA_KB, NT> sk;
+    sk.load(K, a.ldk, k0, a.nk);
+    sk.store(Kk);
+    sk.load(V, a.ldv, k0, a.nk);
+    sk.store(Vk);
+  }
+  f32x4 dk[D::NDB], dv[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dk[db] = dv[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nqs = (int)((a.nq + FA_QS - 1) / FA_QS);
+  __syncthreads();  // pad columns zeroed
+  stq.store(Qs2[0]);
+  std_.store(Ds2[0]);
+  if (threadIdx.x < FA_QS) {
+    lse2[0][threadIdx.x] = lse_v;
+    del2[0][threadIdx.x] = del_v;
+  }
+  __syncthreads();
+  for (int qs = 0; qs < nqs; ++qs) {
+    const int64_t r0 = (int64_t)qs * FA_QS;
+    const int cur = qs & 1;
+    const bf16_t* Qs = Qs2[cur];
+    const bf16_t* Ds = Ds2[cur];
+    const float* lse_s = lse2[cur];
+    const float* del_s = del2[cur];
+    const bool more = qs + 1 < nqs;
+    if (more) {  // next query step in flight during this step's MFMAs
+      stq.load_q(a, Q, b, h, r0 + FA_QS, false);
+      std_.load_q(a, Q, b, h, r0 + FA_QS, true);
+      load_rows(r0 + FA_QS);
+    }
+    f32x4 p[2], ds[2];  // [16-row query block]: lane holds rows 16i + 4g + e, key = lane's key
+    bf16x8 kfr[D::NKS], vfr[D::NKS];
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      kfr[ks] = frag_row<D::ROW>(Kk, wave * 16, ks * 32, lane);
+      vfr[ks] = frag_row<D::ROW>(Vk, wave * 16, ks * 32, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 qa[D::NKS], da[D::NKS];  // LDS reads issued ahead of the MFMAs
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        qa[ks] = frag_row<D::ROW>(Qs, i * 16, ks * 32, lane);
+        da[ks] = frag_row<D::ROW>(Ds, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        sv = mfma(qa[ks], kfr[ks], sv);
+        dp = mfma(da[ks], vfr[ks], dp);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = i * 16 + 4 * g + e;
+        const int r = (int)r0 + rr;
+        float pe = 0.f, dse = 0.f;
+        if (r < a.nq) {
+          const FaLogit lg = fa_logit_d(mk, sv[e], mk.token(r), key);
+          pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse_s[rr]);
+          dse = pe * (dp[e] - del_s[rr]) * lg.dxds;
+        }
+        p[i][e] = pe;
+        ds[i][e] = dse;
+      }
+    }
+    // dV^T[d][key] += dO^T[d][q] P[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+    const bf16x8 pb = pack8(p[0], p[1]);
+    const bf16x8 sb = pack8(ds[0], ds[1]);
+    constexpr int HB = (D::NDB + 1) / 2;  // transposed reads in two batches ahead of their MFMAs
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      bf16x8 dt[HB], qt[HB];
+#pragma unroll
+      for (int x = 0; x < HB; ++x) {
+        const int db = hb * HB + x;
+        if (db < D::NDB) {
+          dt[x] = frag_tr<D::ROW>(Ds, 0, db * 16, lane);
+          qt[x] = frag_tr<D::ROW>(Qs, 0, db * 16, lane);
+        }
+      }
+#pragma unroll
+      for (int x = 0; x < HB; ++x) {
+        const int db = hb * HB + x;
+        if (db < D::NDB) {
+          dv[db] = mfma(dt[x], pb, dv[db]);
+          dk[db] = mfma(qt[x], sb, dk[db]);
+        }
+      }
+    }
+    if (more) {
+      stq.store(Qs2[cur ^ 1]);
+      std_.store(Ds2[cur ^ 1]);
+      if (threadIdx.x < FA_QS) {
+        lse2[cur ^ 1][threadIdx.x] = lse_v;
+        del2[cur ^ 1][threadIdx.x] = del_v;
+      }
+    }
+    __syncthreads();
+  }
+  if (key >= a.nk) return;
+  bf16_t* dK = (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + (int64_t)key * a.ldk;
+  bf16_t* dV = (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + (int64_t)key * a.ldv;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) {
+      *reinterpret_cast<u32x2*>(dK + d) = u32x2{pack2bf(dk[db][0], dk[db][1]), pack2bf(dk[db][2], dk[db][3])};
+      *reinterpret_cast<u32x2*>(dV + d) = u32x2{pack2bf(dv[db][0], dv[db][1]), pack2bf(dv[db][2], dv[db][3])};
+    }
+  }
+}
+
+// dQ: grid (ceil(nq / 64), Z * H), 4 waves x 16 query rows; recomputes S^T, dP^T per staged key
+// block.  Also produces delta = rowsum(dO * O) of its rows (read by the dK/dV pass, launched after).
+template <int HD>
+__global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FA_NW * 64;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks2[2][FA_KB * D::ROW];  // double-buffered K / V tiles
+  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][FA_KB * D::ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.y, b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)blockIdx.x * FA_KB + wave * 16 + (lane & 15);  // this lane's query column
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaRow fr{&a};
+
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
+  }
+  TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
+  stk.load(K, a.ldk, 0, a.nk);
+  stv.load(V, a.ldv, 0, a.nk);
+  bf16x8 qf[D::NKS], df[D::NKS];
+  const bool live = r < a.nq;
+  const bf16_t* dOr = nullptr;
+  const bf16_t* Or = nullptr;
+  if (live) {
+    const int gi = fr.grp(r);
+    dOr = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
+    Or = (const bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+  }
+  float del = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < D::NKS; ++ks) {
+    const int c = ks * 32 + 8 * g;
+    const bool ok = live && c < HD;
+    qf[ks] = ok ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+    df[ks] = ok ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
+    if (ok) {
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) del += (float)df[ks][e] * (float)ov[e];
+    }
+  }
+  del += __shfl_xor(del, 16, 64);
+  del += __shfl_xor(del, 32, 64);
+  if (live && g == 0) a.delta[zh * a.nq + r] = del;
+  const float lse = live ? a.lse[zh * a.nq + r] : 0.f;
+  const int tq = mk.token((int)r);
+  f32x4 dq[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();  // pad columns zeroed
+  stk.store(Ks2[0]);
+  stv.store(Vs2[0]);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Ks2[kb & 1];
+    const bf16_t* Vs = Vs2[kb & 1];
+    const bool more = kb + 1 < nkb;
+    if (more) {
+      stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
+      stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+    }
+    f32x4 ds[4];  // dS^T[key 16i + 4g + e][q]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 kfr[D::NKS], vfr[D::NKS];  // all LDS reads of the key block issued ahead of its MFMAs
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        kfr[ks] = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+        vfr[ks] = frag_row<D::ROW>(Vs, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        sv = mfma(kfr[ks], qf[ks], sv);
+        dp = mfma(vfr[ks], df[ks], dp);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = kb * FA_KB + i * 16 + 4 * g + e;
+        float dse = 0.f;
+        if (live) {
+          const FaLogit lg = fa_logit_d(mk, sv[e], tq, j);
+          const float pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse);
+          dse = pe * (dp[e] - del) * lg.dxds;
+        }
+        ds[i][e] = dse;
+      }
+    }
+    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const bf16x8 sb = pack8(ds[2 * k2], ds[2 * k2 + 1]);
+      bf16x8 kt[D::NDB];
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) kt[db] = frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane);
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) dq[db] = mfma(kt[db], sb, dq[db]);
+    }
+    if (more) {
+      stk.store(Ks2[(kb + 1) & 1]);
+      stv.store(Vs2[(kb + 1) & 1]);
+    }
+    __syncthreads();
+  }
+  if (!live) return;
+  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
+  }
+}
+
+}  // namespace
+
+// head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
+#define FA_DISPATCH(HDV_, KERNEL, GRID, ...)                                                        \
+  switch (HDV_) {                                                                                   \
+    case 256: hipLaunchKernelGGL(KERNEL<256>, GRID, __VA_ARGS__); break;                            \
+    case 72: hipLaunchKernelGGL(KERNEL<72>, GRID, __VA_ARGS__); break;                              \
+    case 32: hipLaunchKernelGGL(KERNEL<32>, GRID, __VA_ARGS__); break;                              \
+    default: hipLaunchKernelGGL(KERNEL<16>, GRID, __VA_ARGS__); break;                              \
+  }
+static bool fa_hd_ok(int64_t hd) { return hd == 256 || hd == 72 || hd == 32 || hd == 16; }
+
+extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->q && a->k && a->v && a->Z > 0 && a->H > 0 && a->nq > 0 && a->nk > 0,
+               "flash_fwd: bad args");
+  PZ_CHECK_ARG(fa_hd_ok(a->head_dim), "flash_fwd: head_dim %lld unsupported (16, 32, 72, 256)",
+               (long long)a->head_dim);
+  PZ_CHECK_ARG(a->n_groups >= 1 && a->n_groups <= 3 && a->g_row0[0] == 0, "flash_fwd: output groups");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_ld[i] % 4 == 0, "flash_fwd: group %d", i);
+  PZ_CHECK_ARG(PZ_ALIGNED(a->q, 16) && PZ_ALIGNED(a->k, 16) && PZ_ALIGNED(a->v, 16) && a->ldq % 8 == 0 &&
+                   a->ldk % 8 == 0 && a->ldv % 8 == 0 && a->q_hstride % 8 == 0 && a->k_hstride % 8 == 0 &&
+                   a->v_hstride % 8 == 0 && a->q_bstride % 8 == 0 && a->k_bstride % 8 == 0 &&
+                   a->v_bstride % 8 == 0 && a->o_hstride % 4 == 0,
+               "flash_fwd: operands need 16-byte aligned rows");
+  if (a->mask_mode == 1) PZ_CHECK_ARG(a->cnt && a->rows_per_token > 0, "flash_fwd: block mask needs cnt");
+  PZ_CHECK_ARG(a->nq < (1 << 22) && a->nk < (1 << 22), "flash_fwd: nq/nk too large");
+  PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_fwd: too many units");
+  dim3 grid((unsigned)((a->nq + 127) / 128), (unsigned)(a->Z * a->H));  // 128 query rows per workgroup
+  FA_DISPATCH(a->head_dim, flash_fwd_kernel, grid, dim3((a->head_dim == 256 ? 8 : 4) * 64), 0, (hipStream_t)stream,
+              *a);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+
+extern "C" int pz_flash_bwd_prep(const pz_flash_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->delta && a->n_groups >= 1 && a->n_groups <= 3, "flash_bwd_prep: bad args");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_do[i], "flash_bwd_prep: group %d", i);
+  const int64_t rows = a->Z * a->H * a->nq;
+  PZ_CHECK_ARG(fa_hd_ok(a->head_dim), "flash_bwd_prep: head_dim");
+  FA_DISPATCH(a->head_dim, flash_bwd_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream,
+              *a);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->lse && a->delta && a->dq && a->dk && a->dv, "flash_bwd: bad args");
+  PZ_CHECK_ARG(fa_hd_ok(a->head_dim), "flash_bwd: head_dim");
+  PZ_CHECK_ARG(PZ_ALIGNED(a->dq, 16) && PZ_ALIGNED(a->dk, 16) && PZ_ALIGNED(a->dv, 16), "flash_bwd: alignment");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_do[i] && a->g_ld[i] % 8 == 0, "flash_bwd: dO group %d", i);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 gkv((unsigned)((a->nk + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
+  dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
+  // dQ pass first: it also writes delta, which the dK/dV pass reads
+  FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
+  PZ_CHECK_LAUNCH();
+  FA_DISPATCH(a->head_dim, flash_bwd_kv_kernel, gkv, dim3(FA_NW * 64), 0, st, *a);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

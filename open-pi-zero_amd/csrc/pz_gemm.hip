@@ -1525,8 +1525,10 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   const int64_t T = pl.tiles_m * pl.tiles_n;
   const int64_t q = T / G, r = T % G;
   const int64_t nk = (a->K + 63) / 64;
-  // a leftover round at least half full runs about as fast as its K-pieces would (less contention)
-  if (r == 0 || (q > 0 && 2 * r >= G)) return;
+  // a leftover round at least half full runs about as fast as its K-pieces would (less contention);
+  // after many rounds the workgroups no longer run in lockstep and the leftover tiles fill the gaps
+  // (measured: split worse at q = 17, better at q <= 4)
+  if (r == 0 || (q > 0 && 2 * r >= G) || q > 8) return;
   int64_t s = G / r;
   s = s < 16 ? s : 16;
   s = s < nk / 2 ? s : nk / 2;

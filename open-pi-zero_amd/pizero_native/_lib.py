@@ -55,6 +55,25 @@ class SoftmaxArgs(C.Structure):
     ]
 
 
+class FlashArgs(C.Structure):
+    _fields_ = [
+        ("Z", i64), ("H", i64), ("nq", i64), ("nk", i64), ("head_dim", i64),
+        ("q", vp), ("ldq", i64), ("q_bstride", i64), ("q_hstride", i64),
+        ("k", vp), ("ldk", i64), ("k_bstride", i64), ("k_hstride", i64),
+        ("v", vp), ("ldv", i64), ("v_bstride", i64), ("v_hstride", i64),
+        ("n_groups", i32),
+        ("g_row0", i64 * 3), ("g_o", vp * 3), ("g_bstride", i64 * 3), ("g_ld", i64 * 3),
+        ("o_hstride", i64),
+        ("lse", vp),
+        ("scale", f32), ("cap", f32),
+        ("mask_mode", i32),
+        ("cnt", vp), ("prefix", i64), ("cond", i64), ("rows_per_token", i64),
+        ("g_do", vp * 3),
+        ("delta", vp),
+        ("dq", vp), ("dk", vp), ("dv", vp),
+    ]
+
+
 # name -> argtypes (restype int unless listed in _RESTYPE)
 SIGNATURES = {
     "pz_gemm": [C.POINTER(GemmArgs), vp],
@@ -73,6 +92,9 @@ SIGNATURES = {
     "pz_qkv_rope_split_bwd": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
     "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],
     "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
+    "pz_flash_fwd": [C.POINTER(FlashArgs), vp],
+    "pz_flash_bwd_prep": [C.POINTER(FlashArgs), vp],
+    "pz_flash_bwd": [C.POINTER(FlashArgs), vp],
     "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],
     "pz_embed_merge": [vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, f32, vp],
     "pz_embed_merge_bwd": [vp, vp, vp, i64, i64, i64, i64, i64, f32, vp],

@@ -25,6 +25,7 @@ current stream).  Layout decisions (MI355X-first):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -136,6 +137,9 @@ class Engine:
         self.d = Dims.from_cfg(model.cfg)
         self._tables = {}
         self._ws = {}
+        # joint attention kernel: "gemm" = MFMA GEMMs around the soft-cap/block-mask softmax (default:
+        # faster today), "flash" = the fused pz_flash kernels (no L x L tensors)
+        self.joint_flash = os.environ.get("PZ_JOINT_ATTN", "gemm") == "flash"
         if self.d.nkv != 1:
             raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
 
@@ -221,7 +225,6 @@ class Engine:
             save["cols"] = cols
         nh, hd = d.vheads, d.vH // d.vheads
         Np = d.n_img
-        S = torch.empty(B * nh, Np, Np, device=dev, dtype=F32)
         layers = []
         for i in range(d.vL):
             p = f"{vt}encoder.layers.{i}."
@@ -233,15 +236,11 @@ class Engine:
             qkv = torch.empty(M, 3 * d.vH, device=dev, dtype=BF16)
             ops.linear(h1, self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"), qkv,
                        bias=self.ar.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias"))
-            W3 = 3 * d.vH
-            # S[b,h] = Q_bh K_bh^T  (heads as the inner batch)
-            ops.gemm(Np, Np, hd, qkv, W3, True, qkv[:, d.vH:], W3, True, S, Np, batch=B * nh, batch_inner=nh,
-                     sA=(Np * W3, hd), sB=(Np * W3, hd), sC=(nh * Np * Np, Np * Np))
-            Pm = torch.empty(B * nh, Np, Np, device=dev, dtype=BF16)
-            ops.attn_softmax(S, Np, Pm, Np, B * nh * Np, Np, hd ** -0.5)
+            # fused attention (siglip.py:108-166) in place on the q|k|v rows: O and one fp32
+            # log-sum-exp per (head, query) row; no [B, heads, N, N] tensor exists
             O = torch.empty(M, d.vH, device=dev, dtype=BF16)
-            ops.gemm(Np, hd, Np, Pm, Np, True, qkv[:, 2 * d.vH:], W3, False, O, d.vH, batch=B * nh, batch_inner=nh,
-                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * d.vH, hd))
+            lse = torch.empty(B * nh, Np, device=dev, dtype=F32)
+            ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, Np))
             xm = torch.empty_like(x)
             ops.linear(O, self.w(p + "self_attn.out_proj.weight"), xm, bias=self.w(p + "self_attn.out_proj.bias"),
                        resid=x)
@@ -255,7 +254,7 @@ class Engine:
             xn = torch.empty_like(x)
             ops.linear(g1, self.w(p + "mlp.fc2.weight"), xn, bias=self.w(p + "mlp.fc2.bias"), resid=xm)
             if save is not None:
-                st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, P=Pm, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1, g1=g1)
+                st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, lse=lse, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1, g1=g1)
                 layers.append(st)
             x = xn
         y = torch.empty_like(x)
@@ -295,8 +294,7 @@ class Engine:
         Np = d.n_img
         W3 = 3 * d.vH
         dg = torch.empty(M, d.vI, device=dev, dtype=BF16)
-        dP = torch.empty(B * nh, Np, Np, device=dev, dtype=F32)
-        dS = torch.empty(B * nh, Np, Np, device=dev, dtype=BF16)
+        delta = torch.empty(B * nh, Np, device=dev, dtype=F32)
         dqkv = torch.empty(M, W3, device=dev, dtype=BF16)
         dh = torch.empty(M, d.vH, device=dev, dtype=BF16)
         dxm = torch.empty(M, d.vH, device=dev, dtype=BF16)
@@ -326,17 +324,9 @@ class Engine:
             if self.rg(p + "self_attn.out_proj.bias"):
                 ops.colsum(dxm, self.gw(p + "self_attn.out_proj.bias"), ws, beta=beta)
             ops.linear_dgrad(dxm, self.w(p + "self_attn.out_proj.weight"), dO)
-            qkv, Pm = st["qkv"], st["P"]
-            # dP = dO V^T ; dS ; dQ = dS K ; dK = dS^T Q ; dV = P^T dO
-            ops.gemm(Np, Np, hd, dO, d.vH, True, qkv[:, 2 * d.vH:], W3, True, dP, Np, batch=B * nh, batch_inner=nh,
-                     sA=(Np * d.vH, hd), sB=(Np * W3, hd), sC=(nh * Np * Np, Np * Np))
-            ops.attn_softmax_bwd(Pm, dP, Np, None, dS, Np, B * nh * Np, Np, hd ** -0.5, 0.0)
-            ops.gemm(Np, hd, Np, dS, Np, True, qkv[:, d.vH:], W3, False, dqkv, W3, batch=B * nh, batch_inner=nh,
-                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * W3, hd))
-            ops.gemm(Np, hd, Np, dS, Np, False, qkv, W3, False, dqkv[:, d.vH:], W3, batch=B * nh, batch_inner=nh,
-                     sA=(nh * Np * Np, Np * Np), sB=(Np * W3, hd), sC=(Np * W3, hd))
-            ops.gemm(Np, hd, Np, Pm, Np, False, dO, d.vH, False, dqkv[:, 2 * d.vH:], W3, batch=B * nh,
-                     batch_inner=nh, sA=(nh * Np * Np, Np * Np), sB=(Np * d.vH, hd), sC=(Np * W3, hd))
+            # fused attention backward: dQ | dK | dV straight into the q|k|v gradient rows
+            ops.flash_bwd(ops.siglip_flash_args(st["qkv"], st["O"], st["lse"], B, nh, hd, Np, dO=dO, delta=delta,
+                                                dqkv=dqkv))
             qn, vn = p + "self_attn.q_proj.", p + "self_attn.v_proj."
             if all(self.rg(p + f"self_attn.{k}_proj.weight") for k in "qkv"):
                 ops.linear_wgrad(dqkv, st["h1"], self.ar.grad_span(qn + "weight", vn + "weight"), beta=beta)
@@ -410,12 +400,25 @@ class Engine:
         return e3
 
     # ======================================================== joint layers ==
+    def _joint_flash(self, groups, Q, K, V, Os, lse, cnt, B, Lq, dO=None, delta=None, dq=None, dk=None, dv=None):
+        """pz_flash_args of the joint attention: query rows r = token*nh + head of Q [B, Lq*nh, hd],
+        keys/values K, V [B, Lp, hd]; output groups = the mixtures' O buffers [B*T, nh*hd] in
+        token order (joint_model.py:259-292 with the Pi0 block mask, pizero.py:271-306)."""
+        d = self.d
+        nh, hd, Lp = d.nh, d.hd, K.shape[1]
+        gs = sorted(groups, key=lambda g: g.off)
+        return ops.flash_args(
+            B, 1, Lq * nh, d.L, hd, Q, (hd, Lq * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+            [(g.off * nh, Os[g.name], g.T * nh * hd, hd) for g in gs], 0, lse, 1.0 / math.sqrt(hd), cap=50.0,
+            mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh,
+            dgroups=None if dO is None else [dO[g.name] for g in gs], delta=delta, dq=dq, dk=dk, dv=dv)
+
     def _joint_layers_train(self, groups, X, pos, cnt, B, save):
         """joint_model.py:24-304 x nL for the training pass (all mixtures active)."""
         d = self.d
         dev = X[groups[0].name].device
         L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
-        S = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+        S = None
         layers = []
         for l in range(d.nL):
             last = l == d.nL - 1
@@ -436,13 +439,29 @@ class Engine:
                 ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L, g.off,
                                    Lp, g.off)
                 st["g"][g.name] = {"x": x, "h": h, "r": r}
-            ops.gemm(L * nh, L, hd, Qj, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L * nh * hd, 0),
-                     sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
-            Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
-            tc = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
-            ops.attn_softmax(S, Lp, Pm, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), cap=50.0, tcap=tc, mask_mode=1,
-                             rows_per_batch=L * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
-            st["P"], st["tc"] = Pm, tc
+            Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
+            if self.joint_flash:
+                # fused joint attention (joint_model.py:259-292): soft-cap, block mask from cnt, O rows
+                # scattered into each mixture's o_proj input; one fp32 log-sum-exp per (token, head) row
+                lse = torch.empty(B, L * nh, device=dev, dtype=F32)
+                ops.flash_fwd(self._joint_flash(groups, Qj, Kj, Vj, Os, lse, cnt, B, L))
+                st["lse"], st["O"] = lse, Os
+            else:
+                # S = Q K^T per sample (MQA heads stacked as rows), soft-cap + block-mask softmax, O = P V
+                if S is None:
+                    S = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+                ops.gemm(L * nh, L, hd, Qj, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L * nh * hd, 0),
+                         sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
+                Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+                tc = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+                ops.attn_softmax(S, Lp, Pm, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), cap=50.0, tcap=tc, mask_mode=1,
+                                 rows_per_batch=L * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
+                st["P"], st["tc"] = Pm, tc
+                for g in groups:
+                    if not (last and g.skip_last):
+                        ops.gemm(g.T * nh, hd, Lp, Pm[:, g.off * nh:], Lp, True, Vj, hd, False, Os[g.name], hd, batch=B,
+                                 sA=(L * nh * Lp, 0), sB=(Lp * hd, 0), sC=(g.T * nh * hd, 0))
+                st["O"] = Os
             for g in groups:
                 gs = st["g"][g.name]
                 p = f"{g.prefix}{l}."
@@ -452,9 +471,7 @@ class Engine:
                     X[g.name] = None
                     gs["skip"] = True
                     continue
-                O = torch.empty(M, nh * hd, device=dev, dtype=BF16)
-                ops.gemm(g.T * nh, hd, Lp, Pm[:, g.off * nh:], Lp, True, Vj, hd, False, O, hd, batch=B,
-                         sA=(L * nh * Lp, 0), sB=(Lp * hd, 0), sC=(g.T * nh * hd, 0))
+                O = Os[g.name]
                 xm = torch.empty_like(x)
                 ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
                 h2 = torch.empty_like(x)
@@ -475,8 +492,7 @@ class Engine:
         d = self.d
         L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
         dev = next(v for v in dX.values() if v is not None).device
-        dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
-        dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+        delta = dP = dS = None
         rpp = ops.rows_per_part()
         for l in reversed(range(d.nL)):
             st = sv["joint"][l]
@@ -519,29 +535,42 @@ class Engine:
                 ops.linear_dgrad(dxm, self.w(p + "self_attn.o_proj.weight"), o)
                 dO[g.name] = o
                 dXm[g.name] = dxm
-            Pm, tc, Qj, Kj, Vj = st["P"], st["tc"], st["Q"], st["K"], st["V"]
-            if any_skip:
-                dP.zero_()
-            for g in groups:
-                if g.name not in dO:
-                    continue
-                ops.gemm(g.T * nh, L, hd, dO[g.name], hd, True, Vj, hd, True, dP[:, g.off * nh:], Lp, batch=B,
-                         sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
-            ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
-            # dQ = dS K ; dK = dS^T Q ; dV = sum_g P_g^T dO_g
-            ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
-                     sB=(Lp * hd, 0), sC=(L * nh * hd, 0))
-            ops.gemm(Lp, hd, L * nh, dS, Lp, False, Qj, hd, False, dK, hd, batch=B, sA=(L * nh * Lp, 0),
-                     sB=(L * nh * hd, 0), sC=(Lp * hd, 0))
-            first = True
-            for g in groups:
-                if g.name not in dO:
-                    continue
-                ops.gemm(Lp, hd, g.T * nh, Pm[:, g.off * nh:], Lp, False, dO[g.name], hd, False, dV, hd, batch=B,
-                         sA=(L * nh * Lp, 0), sB=(g.T * nh * hd, 0), sC=(Lp * hd, 0), beta=not first)
-                first = False
-            if first:
-                dV.zero_()
+            if "lse" in st:
+                # fused attention backward (skipped mixtures' outputs reach nothing: dO = 0)
+                for g in groups:
+                    if g.name not in dO:
+                        dO[g.name] = torch.zeros(B * g.T, nh * hd, device=dev, dtype=BF16)
+                if delta is None:
+                    delta = torch.empty(B, L * nh, device=dev, dtype=F32)
+                ops.flash_bwd(self._joint_flash(groups, st["Q"], st["K"], st["V"], st["O"], st["lse"], cnt, B, L,
+                                                dO=dO, delta=delta, dq=dQ, dk=dK, dv=dV))
+            else:
+                if dP is None:
+                    dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+                    dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+                Pm, tc, Qj, Kj, Vj = st["P"], st["tc"], st["Q"], st["K"], st["V"]
+                if any_skip:
+                    dP.zero_()
+                for g in groups:
+                    if g.name not in dO:
+                        continue
+                    ops.gemm(g.T * nh, L, hd, dO[g.name], hd, True, Vj, hd, True, dP[:, g.off * nh:], Lp, batch=B,
+                             sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
+                ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
+                # dQ = dS K ; dK = dS^T Q ; dV = sum_g P_g^T dO_g
+                ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
+                         sB=(Lp * hd, 0), sC=(L * nh * hd, 0))
+                ops.gemm(Lp, hd, L * nh, dS, Lp, False, Qj, hd, False, dK, hd, batch=B, sA=(L * nh * Lp, 0),
+                         sB=(L * nh * hd, 0), sC=(Lp * hd, 0))
+                first = True
+                for g in groups:
+                    if g.name not in dO:
+                        continue
+                    ops.gemm(Lp, hd, g.T * nh, Pm[:, g.off * nh:], Lp, False, dO[g.name], hd, False, dV, hd, batch=B,
+                             sA=(L * nh * Lp, 0), sB=(g.T * nh * hd, 0), sC=(Lp * hd, 0), beta=not first)
+                    first = False
+                if first:
+                    dV.zero_()
             for g in groups:
                 gs = st["g"][g.name]
                 p = f"{g.prefix}{l}."

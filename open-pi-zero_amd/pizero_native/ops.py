@@ -19,6 +19,7 @@ from ._lib import (
     PZ_EPI_GELU,
     PZ_EPI_NONE,
     PZ_EPI_SILU,
+    FlashArgs,
     GemmArgs,
     SmallGemmArgs,
     SoftmaxArgs,
@@ -287,6 +288,49 @@ def attn_softmax(S, lds, P, ldp, R, N, scale, cap=0.0, tcap=None, mask_mode=0, r
 def attn_softmax_bwd(P, dP, lddp, tcap, dS, ldp, R, N, scale, cap):
     call("pz_attn_softmax_bwd", _p(P), _p(dP), lddp, _p(tcap), _p(dS), ldp, R, N, float(scale), float(cap),
          _st())
+
+
+def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, groups, o_hstride, lse, scale,
+               cap=0.0, mask_mode=0, cnt=None, prefix=0, cond=0, rows_per_token=1, dgroups=None, delta=None,
+               dq=None, dk=None, dv=None):
+    """pz_flash_args (include/pz_abi.h).  *_strides = (ld, bstride, hstride) in elements; groups =
+    [(row0, O tensor, bstride, ld), ...] (dgroups: the dO tensors of the same groups)."""
+    a = FlashArgs()
+    a.Z, a.H, a.nq, a.nk, a.head_dim = int(Z), int(H), int(nq), int(nk), int(hd)
+    a.q, (a.ldq, a.q_bstride, a.q_hstride) = _p(q), tuple(int(x) for x in q_strides)
+    a.k, (a.ldk, a.k_bstride, a.k_hstride) = _p(k), tuple(int(x) for x in k_strides)
+    a.v, (a.ldv, a.v_bstride, a.v_hstride) = _p(v), tuple(int(x) for x in v_strides)
+    a.n_groups = len(groups)
+    for i, (r0, o, bs, ld) in enumerate(groups):
+        a.g_row0[i], a.g_o[i], a.g_bstride[i], a.g_ld[i] = int(r0), _p(o), int(bs), int(ld)
+        if dgroups is not None:
+            a.g_do[i] = _p(dgroups[i])
+    a.o_hstride = int(o_hstride)
+    a.lse = _p(lse)
+    a.scale, a.cap, a.mask_mode = float(scale), float(cap), int(mask_mode)
+    a.cnt, a.prefix, a.cond, a.rows_per_token = _p(cnt), int(prefix), int(cond), int(rows_per_token)
+    a.delta, a.dq, a.dk, a.dv = _p(delta), _p(dq), _p(dk), _p(dv)
+    return a
+
+
+def flash_fwd(a):
+    call("pz_flash_fwd", C.byref(a), _st())
+
+
+def flash_bwd(a):
+    """dQ (+ delta = rowsum(dO * O)), then dK/dV (overwritten); a.delta is fp32 scratch [Z*H, nq]."""
+    call("pz_flash_bwd", C.byref(a), _st())
+
+
+def siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=None, delta=None, dqkv=None):
+    """SigLIP attention in place on the fused q|k|v projection rows [B*N, 3*nh*hd]; O [B*N, nh*hd]."""
+    W = qkv.stride(0)
+    H = nh * hd
+    strides = (W, N * W, hd)
+    return flash_args(B, nh, N, N, hd, qkv, strides, qkv[:, H:], strides, qkv[:, 2 * H:], strides,
+                      [(0, O, N * O.stride(0), O.stride(0))], hd, lse, hd ** -0.5,
+                      dgroups=None if dO is None else [dO], delta=delta,
+                      dq=dqkv, dk=None if dqkv is None else dqkv[:, H:], dv=None if dqkv is None else dqkv[:, 2 * H:])
 
 
 def patchify(pix, cols, ps):

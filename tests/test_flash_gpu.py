@@ -1,0 +1,175 @@
+"""Fused (flash) attention kernels vs a plain PyTorch fp32 reference of the same attention.
+
+SigLIP shape (siglip.py:108-166: 16 heads x 72, 256 tokens, no mask) read in place from the fused
+q|k|v rows, and the joint MQA shape (joint_model.py:130-304: 8 query heads stacked as rows, one
+K/V head of 256, soft-cap 50, Pi0 block mask incl. pad rows, pizero.py:271-306) scattered into
+per-mixture output buffers.  Tolerance: P is rounded to bf16 before the PV product (as the
+reference's autocast softmax(...).to(bf16) does), outputs are bf16: ~1e-2 relative.
+"""
+
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import pizero_native
+
+    pizero_native.lib()
+    torch.manual_seed(0)
+
+
+def close(out, ref, rtol=2e-2, atol=2e-2):
+    out, ref = out.float(), ref.float()
+    err = (out - ref).abs()
+    bad = (err > atol + rtol * ref.abs()).sum().item()
+    assert bad == 0, f"{bad} mismatches, max err {err.max().item():.4g}"
+
+
+def joint_mask(cnt, P, C, L):
+    """[B, L, L] bool allowed + [B, L] dead-row flags (pizero.py:271-306 semantics)."""
+    B = len(cnt)
+    i = torch.arange(L).view(L, 1)
+    j = torch.arange(L).view(1, L)
+    allowed = torch.zeros(B, L, L, dtype=torch.bool)
+    dead = torch.zeros(B, L, dtype=torch.bool)
+    for b, c in enumerate(cnt):
+        vlm = (i < P) & (i < c) & (j < c)
+        prop = (i >= P) & (i < P + C) & ((j < c) | ((j >= P) & (j < P + C)))
+        act = (i >= P + C) & ((j < c) | (j >= P))
+        allowed[b] = vlm | prop | act
+        dead[b] = (torch.arange(L) < P) & (torch.arange(L) >= c)
+    return allowed, dead
+
+
+def ref_attention(q, k, v, scale, cap=0.0, allowed=None, dead=None):
+    """q [B, H, Lq, D], k/v [B, H, Lk, D] fp32; allowed [B, Lq, Lk]; dead [B, Lq] -> uniform rows"""
+    s = (q @ k.transpose(-1, -2)) * scale
+    if cap > 0:
+        s = cap * torch.tanh(s / cap)
+    if allowed is not None:
+        s = s.masked_fill(~allowed[:, None], float("-inf"))
+        s = torch.where(dead[:, None, :, None], torch.zeros_like(s), s)
+    lse = torch.logsumexp(s, -1)
+    p = torch.softmax(s, -1)
+    return p @ v, lse
+
+
+def test_flash_fwd_siglip():
+    from pizero_native import ops
+
+    B, nh, hd, N = 3, 16, 72, 256
+    qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
+    O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh, N, device=dev)
+    ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N))
+    x = qkv.float().view(B, N, 3, nh, hd).permute(2, 0, 3, 1, 4)  # [3, B, nh, N, hd]
+    ref, rlse = ref_attention(x[0], x[1], x[2], hd ** -0.5)
+    close(O.view(B, N, nh, hd).permute(0, 2, 1, 3), ref)
+    close(lse.view(B, nh, N), rlse, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("cnt", [[276, 276, 276], [276, 250, 9]])
+def test_flash_fwd_joint_block_mask(cnt):
+    from pizero_native import ops
+
+    B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
+    L = P + C + Hc
+    Lp = (L + 7) // 8 * 8
+    Q = (torch.randn(B, L * nh, hd, device=dev) * 2).to(torch.bfloat16)
+    K = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    V = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    K[:, :L] = (torch.randn(B, L, hd, device=dev) * 2).to(torch.bfloat16)
+    V[:, :L] = torch.randn(B, L, hd, device=dev).to(torch.bfloat16)
+    Ov = torch.empty(B * P, nh * hd, device=dev, dtype=torch.bfloat16)
+    Oe = torch.empty(B * (C + Hc), nh * hd, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B, L * nh, device=dev)
+    cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                       [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + Hc) * nh * hd, hd)], 0, lse, 1 / math.sqrt(hd),
+                       cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh)
+    ops.flash_fwd(a)
+    allowed, dead = joint_mask(cnt, P, C, L)
+    q = Q.float().view(B, L, nh, hd).permute(0, 2, 1, 3)
+    k = K.float()[:, None, :L]
+    v = V.float()[:, None, :L]
+    ref, rlse = ref_attention(q, k, v, 1 / math.sqrt(hd), 50.0, allowed.to(dev), dead.to(dev))
+    ref = ref.permute(0, 2, 1, 3)  # [B, L, nh, hd]
+    close(Ov.view(B, P, nh, hd), ref[:, :P])
+    close(Oe.view(B, C + Hc, nh, hd), ref[:, P:])
+    close(lse.view(B, L, nh), rlse.permute(0, 2, 1), rtol=1e-3, atol=2e-3)
+
+
+def _grads(q, k, v, dO, scale, cap=0.0, allowed=None, dead=None):
+    q, k, v = (t.detach().clone().requires_grad_() for t in (q, k, v))
+    o, _ = ref_attention(q, k, v, scale, cap, allowed, dead)
+    o.backward(dO)
+    return q.grad, k.grad, v.grad
+
+
+def test_flash_bwd_siglip():
+    from pizero_native import ops
+
+    B, nh, hd, N = 2, 16, 72, 256
+    qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
+    O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
+    lse = torch.empty(B * nh, N, device=dev)
+    ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N))
+    dO = torch.randn(B * N, nh * hd, device=dev).to(torch.bfloat16)
+    delta = torch.empty(B * nh, N, device=dev)
+    dqkv = torch.full_like(qkv, float("nan"))
+    ops.flash_bwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv))
+    x = qkv.float().view(B, N, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    g = dO.float().view(B, N, nh, hd).permute(0, 2, 1, 3)
+    dq, dk, dv = _grads(x[0], x[1], x[2], g, hd ** -0.5)
+    got = dqkv.float().view(B, N, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    for out, ref in ((got[0], dq), (got[1], dk), (got[2], dv)):
+        close(out, ref, rtol=3e-2, atol=3e-2 * ref.abs().max().item() / 4)
+
+
+@pytest.mark.parametrize("cnt", [[276, 276], [276, 9]])
+def test_flash_bwd_joint_block_mask(cnt):
+    from pizero_native import ops
+
+    B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
+    L = P + C + Hc
+    Lp = (L + 7) // 8 * 8
+    Q = (torch.randn(B, L * nh, hd, device=dev) * 2).to(torch.bfloat16)
+    K = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    V = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    K[:, :L] = (torch.randn(B, L, hd, device=dev) * 2).to(torch.bfloat16)
+    V[:, :L] = torch.randn(B, L, hd, device=dev).to(torch.bfloat16)
+    Ov = torch.empty(B * P, nh * hd, device=dev, dtype=torch.bfloat16)
+    Oe = torch.empty(B * (C + Hc), nh * hd, device=dev, dtype=torch.bfloat16)
+    dOv = torch.randn(B * P, nh * hd, device=dev).to(torch.bfloat16)
+    dOe = torch.randn(B * (C + Hc), nh * hd, device=dev).to(torch.bfloat16)
+    cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
+    # the pad rows' outputs reach nothing downstream in the model (no row attends to them), so their dO is 0
+    allowed, dead = joint_mask(cnt, P, C, L)
+    dOv.view(B, P, nh * hd)[dead[:, :P].to(dev)] = 0
+    lse = torch.empty(B, L * nh, device=dev)
+    delta = torch.empty(B, L * nh, device=dev)
+    dQ = torch.full_like(Q, float("nan"))
+    dK = torch.zeros_like(K)
+    dV = torch.zeros_like(V)
+    groups = [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + Hc) * nh * hd, hd)]
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                       groups, 0, lse, 1 / math.sqrt(hd), cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C,
+                       rows_per_token=nh, dgroups=[dOv, dOe], delta=delta, dq=dQ, dk=dK, dv=dV)
+    ops.flash_fwd(a)
+    ops.flash_bwd(a)
+    q = Q.float().view(B, L, nh, hd).permute(0, 2, 1, 3)
+    g = torch.cat([dOv.float().view(B, P, nh, hd), dOe.float().view(B, C + Hc, nh, hd)], 1).permute(0, 2, 1, 3)
+    kk = K.float()[:, None, :L].expand(B, nh, L, hd)
+    vv = V.float()[:, None, :L].expand(B, nh, L, hd)
+    dq, dk, dv = _grads(q, kk, vv, g, 1 / math.sqrt(hd), 50.0, allowed.to(dev), dead.to(dev))
+    close(dQ.float().view(B, L, nh, hd).permute(0, 2, 1, 3), dq, atol=3e-2 * dq.abs().max().item() / 4)
+    close(dK.float()[:, :L], dk.sum(1), atol=3e-2 * dk.abs().max().item())
+    close(dV.float()[:, :L], dv.sum(1), atol=3e-2 * dv.abs().max().item())

@@ -130,3 +130,17 @@ def test_full_actions(full):
     _check_actions(g, a, "actions_unclipped")
     a3 = run_infer(m, gi, clip=True)
     np.testing.assert_allclose(a3.float().cpu().numpy(), np.clip(a.float().cpu().numpy(), -1, 1), atol=1e-2)
+
+
+@pytest.mark.parametrize("which", ["tiny", "full"])
+def test_loss_and_grads_fused_joint_attention(which, request):
+    """the fused (flash) joint attention path (PZ_JOINT_ATTN=flash) against the same fixtures"""
+    d, g, m, gi = request.getfixturevalue(which)
+    eng = m._engine()
+    eng.joint_flash = True
+    try:
+        loss = run_loss(m, gi)
+        _check_loss(g, loss.item())
+        _check_grads(g, m)
+    finally:
+        eng.joint_flash = False

@@ -1,0 +1,74 @@
+"""Microbenchmark of the fused attention kernels at the bench shapes (micro-batch 64).
+
+    python tools/flash_bench.py [--iters 10]
+joint: 64 samples x (281 tokens x 8 heads) queries, 281 keys, head 256, soft-cap + block mask;
+siglip: 64 x 16 heads x 256 x 256, head 72.  Prints fwd / bwd ms and TF/s (algorithmic
+FLOP: fwd 4*nq*nk*hd per unit, bwd 2.5x fwd).
+"""
+import argparse
+import math
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "open-pi-zero_amd"))
+import torch  # noqa: E402
+
+from pizero_native import ops  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    dev = "cuda"
+    B, P, C, H, nh, hd = 64, 276, 1, 4, 8, 256
+    L = P + C + H
+    Lp = (L + 7) // 8 * 8
+    Q = torch.randn(B, L * nh, hd, device=dev).to(torch.bfloat16)
+    K = torch.randn(B, Lp, hd, device=dev).to(torch.bfloat16)
+    V = torch.randn(B, Lp, hd, device=dev).to(torch.bfloat16)
+    Ov = torch.empty(B * P, nh * hd, device=dev, dtype=torch.bfloat16)
+    Oe = torch.empty(B * (C + H), nh * hd, device=dev, dtype=torch.bfloat16)
+    dOv, dOe = torch.randn_like(Ov), torch.randn_like(Oe)
+    lse = torch.empty(B, L * nh, device=dev)
+    delta = torch.empty_like(lse)
+    dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
+    cnt = torch.full((B,), P, device=dev, dtype=torch.int32)
+    fa = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                        [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + H) * nh * hd, hd)], 0, lse, 1 / math.sqrt(hd),
+                        cap=50.0, mask_mode=1, cnt=cnt, prefix=P, cond=C, rows_per_token=nh, dgroups=[dOv, dOe],
+                        delta=delta, dq=dQ, dk=dK, dv=dV)
+    fl = 4.0 * B * L * nh * L * hd
+    tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
+    tb = timeit(lambda: ops.flash_bwd(fa), a.iters)
+    print(f"joint  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
+    nh, hd, N = 16, 72, 256
+    qkv = torch.randn(B * N, 3 * nh * hd, device=dev).to(torch.bfloat16)
+    O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
+    dO = torch.randn_like(O)
+    lse = torch.empty(B * nh, N, device=dev)
+    delta = torch.empty_like(lse)
+    dqkv = torch.empty_like(qkv)
+    sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
+    fl = 4.0 * B * nh * N * N * hd
+    tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
+    tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
+    print(f"siglip fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,6 +21,8 @@ for s in $STEPS; do
     infprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/infprof" -o infer \
         -- python3 tools/infer_bench.py --iters 20 > "$OUT/infprof.log" 2>&1 ;;
+    flashbench)
+      timeout -k 10 300 python -u tools/flash_bench.py > "$OUT/flash_bench.log" 2>&1 ;;
     gemmbench)
       timeout -k 10 400 python -u tools/gemm_bench.py --iters 10 > "$OUT/gemm_bench.log" 2>&1 ;;
     pmc)

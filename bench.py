@@ -60,6 +60,22 @@ def synthetic_batch(model, B, device, gen):
     )
 
 
+def pmc_traffic(kname, shape):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes
+    (profiles/r01/pmc_dominant.json, tools/pmc_dominant.sh + tools/pmc_summary.py): FETCH_SIZE x2
+    (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another kernel/shape."""
+    path = os.path.join(ROOT, "profiles", "r01", "pmc_dominant.json")
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return {"traffic": None}
+    if not kname.startswith(pm.get("kernel", "?")) or list(pm.get("shape_MNK", [])) != list(shape):
+        return {"traffic": None}
+    return {"traffic": pm["traffic_bytes"], "traffic_unit": "bytes/launch",
+            "traffic_algorithmic": pm["algorithmic_bytes"], "traffic_source": "profiles/r01/pmc_dominant.json"}
+
+
 def cpu_baseline(seconds_budget=25.0):
     """Oracle (CPU fp32 restatement) fwd+bwd of one bridge sample on this host's cores."""
     from oracle import pizero_oracle as O
@@ -261,7 +277,8 @@ def main():
             "roofline": {"bound": "mfma", "kernel": kname + " (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,
                          "achieved": achieved, "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS, "traffic": None},
+                         "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS,
+                         **pmc_traffic(kname, [Mg, Ng, Kg])},
             "inference": infer,
             "cpu_baseline": cpu,
             "loss_mean": float(loss_acc.item()) / (accum * args.steps * max(1, world)),

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 3
+#define PZ_ABI_VERSION 4
 
 enum {
   PZ_OK = 0,
@@ -178,6 +178,8 @@ typedef struct pz_flash_args {
   const void* g_do[3];
   float* delta;
   void* dq; void* dk; void* dv;
+  /* optional fp32 scratch (16-byte aligned) for the query-split dK/dV partials; NULL: no split */
+  float* ws; int64_t ws_bytes;
 } pz_flash_args;
 int pz_flash_fwd(const pz_flash_args* a, void* stream);
 /* delta[z][r] = sum_d dO[r][d] * O[r][d] (fp32) */

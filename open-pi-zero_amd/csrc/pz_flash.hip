@@ -414,16 +414,20 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Qs2[bi]);
     zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Ds2[bi]);
   }
+  // query split (blockIdx.z of gridDim.z): this workgroup sweeps query steps [qs0, qs1)
+  const int nqs_all = (int)((a.nq + FA_QS - 1) / FA_QS);
+  const int per = (nqs_all + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int qs0 = min(nqs_all, (int)blockIdx.z * per), qs1 = min(nqs_all, qs0 + per);
   TileStager<HD, D::ROW, FA_QS, NT> stq, std_;
-  stq.load_q(a, Q, b, h, 0, false);
-  std_.load_q(a, Q, b, h, 0, true);
+  stq.load_q(a, Q, b, h, (int64_t)qs0 * FA_QS, false);
+  std_.load_q(a, Q, b, h, (int64_t)qs0 * FA_QS, true);
   float lse_v = 0.f, del_v = 0.f;  // threads < FA_QS carry one row's lse / delta
   auto load_rows = [&](int64_t r0) {
     const int64_t rr = r0 + threadIdx.x;
     lse_v = threadIdx.x < FA_QS && rr < a.nq ? a.lse[zh * a.nq + rr] : 0.f;
     del_v = threadIdx.x < FA_QS && rr < a.nq ? a.delta[zh * a.nq + rr] : 0.f;
   };
-  load_rows(0);
+  load_rows((int64_t)qs0 * FA_QS);
   // this workgroup's keys / values, read as B operands (n = key, k = head dim) from LDS:
   // K for S = Q K^T, V for dP = dO V^T (in LDS rather than registers: the accumulators need them)
   zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Kk);
@@ -439,7 +443,6 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
 #pragma unroll
   for (int db = 0; db < D::NDB; ++db) dk[db] = dv[db] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nqs = (int)((a.nq + FA_QS - 1) / FA_QS);
   __syncthreads();  // pad columns zeroed
   stq.store(Qs2[0]);
   std_.store(Ds2[0]);
@@ -448,14 +451,14 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     del2[0][threadIdx.x] = del_v;
   }
   __syncthreads();
-  for (int qs = 0; qs < nqs; ++qs) {
+  for (int qs = qs0; qs < qs1; ++qs) {
     const int64_t r0 = (int64_t)qs * FA_QS;
-    const int cur = qs & 1;
+    const int cur = (qs - qs0) & 1;
     const bf16_t* Qs = Qs2[cur];
     const bf16_t* Ds = Ds2[cur];
     const float* lse_s = lse2[cur];
     const float* del_s = del2[cur];
-    const bool more = qs + 1 < nqs;
+    const bool more = qs + 1 < qs1;
     if (more) {  // next query step in flight during this step's MFMAs
       stq.load_q(a, Q, b, h, r0 + FA_QS, false);
       std_.load_q(a, Q, b, h, r0 + FA_QS, true);
@@ -531,6 +534,20 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     __syncthreads();
   }
   if (key >= a.nk) return;
+  if (gridDim.z > 1) {  // fp32 partial sums of this query split -> ws[split][unit][key][HD] (dK), then dV
+    const int64_t slab = (int64_t)gridDim.y * a.nk * HD;
+    float* pk = a.ws + ((int64_t)blockIdx.z * gridDim.y + zh) * a.nk * HD + (int64_t)key * HD;
+    float* pv = pk + (int64_t)gridDim.z * slab;
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD) {
+        *reinterpret_cast<f32x4*>(pk + d) = dk[db];
+        *reinterpret_cast<f32x4*>(pv + d) = dv[db];
+      }
+    }
+    return;
+  }
   bf16_t* dK = (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + (int64_t)key * a.ldk;
   bf16_t* dV = (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + (int64_t)key * a.ldv;
 #pragma unroll
@@ -541,6 +558,25 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
       *reinterpret_cast<u32x2*>(dV + d) = u32x2{pack2bf(dv[db][0], dv[db][1]), pack2bf(dv[db][2], dv[db][3])};
     }
   }
+}
+
+// sum of the query-split partials (fixed order) -> bf16 dK / dV; one thread per 4 elements
+template <int HD>
+__global__ void __launch_bounds__(256) flash_bwd_kv_reduce_kernel(pz_flash_args a, int splits) {
+  const int64_t units = a.Z * a.H, per_unit = a.nk * (HD / 4);
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= 2 * units * per_unit) return;
+  const bool is_v = idx >= units * per_unit;
+  const int64_t i = is_v ? idx - units * per_unit : idx;
+  const int64_t zh = i / per_unit, rem = i % per_unit, key = rem / (HD / 4), d = (rem % (HD / 4)) * 4;
+  const int64_t slab = units * a.nk * HD;
+  const float* src = a.ws + (is_v ? (int64_t)splits * slab : 0) + zh * a.nk * HD + key * HD + d;
+  f32x4 acc = *reinterpret_cast<const f32x4*>(src);
+  for (int sp = 1; sp < splits; ++sp) acc += *reinterpret_cast<const f32x4*>(src + sp * slab);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  bf16_t* dst = is_v ? (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + key * a.ldv
+                     : (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + key * a.ldk;
+  *reinterpret_cast<u32x2*>(dst + d) = u32x2{pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3])};
 }
 
 // dQ: grid (ceil(nq / 64), Z * H), 4 waves x 16 query rows; recomputes S^T, dP^T per staged key
@@ -716,12 +752,27 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
   PZ_CHECK_ARG(PZ_ALIGNED(a->dq, 16) && PZ_ALIGNED(a->dk, 16) && PZ_ALIGNED(a->dv, 16), "flash_bwd: alignment");
   for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_do[i] && a->g_ld[i] % 8 == 0, "flash_bwd: dO group %d", i);
   hipStream_t st = (hipStream_t)stream;
-  dim3 gkv((unsigned)((a->nk + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
+  // query split of the dK/dV pass when it has too few workgroups to fill the chip (joint MQA: 5 key
+  // blocks per sample); fp32 partials in the caller's workspace, summed by a second pass
+  const int64_t nkb = (a->nk + FA_KB - 1) / FA_KB;
+  int64_t splits = 1;
+  if (a->ws && a->head_dim % 4 == 0) {
+    splits = (1024 + nkb * a->Z * a->H - 1) / (nkb * a->Z * a->H);
+    splits = splits < 8 ? splits : 8;
+    while (splits > 1 && splits * 2 * a->Z * a->H * a->nk * a->head_dim * 4 > a->ws_bytes) --splits;
+  }
+  dim3 gkv((unsigned)nkb, (unsigned)(a->Z * a->H), (unsigned)splits);
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
   FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
   PZ_CHECK_LAUNCH();
   FA_DISPATCH(a->head_dim, flash_bwd_kv_kernel, gkv, dim3(FA_NW * 64), 0, st, *a);
+  if (splits > 1) {
+    PZ_CHECK_LAUNCH();
+    const int64_t n4 = 2 * a->Z * a->H * a->nk * (a->head_dim / 4);
+    FA_DISPATCH(a->head_dim, flash_bwd_kv_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, *a,
+                (int)splits);
+  }
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -310,7 +310,25 @@ def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, group
     a.scale, a.cap, a.mask_mode = float(scale), float(cap), int(mask_mode)
     a.cnt, a.prefix, a.cond, a.rows_per_token = _p(cnt), int(prefix), int(cond), int(rows_per_token)
     a.delta, a.dq, a.dk, a.dv = _p(delta), _p(dq), _p(dk), _p(dv)
+    if dq is not None:  # fp32 scratch for the query-split dK/dV partials
+        ws = flash_workspace(dq.device)
+        a.ws, a.ws_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
     return a
+
+
+_FLASH_WS_BYTES = 320 << 20
+_FLASH_WS = {}
+
+
+def flash_workspace(device):
+    """Per-device fp32 scratch of the fused attention backward (8 query splits x dK, dV of a
+    64-sample micro-batch = 295 MB); allocated once, stream-ordered like the GEMM workspace."""
+    dev = torch.device(device)
+    ws = _FLASH_WS.get(dev)
+    if ws is None:
+        ws = torch.empty(_FLASH_WS_BYTES // 4, dtype=torch.float32, device=dev)
+        _FLASH_WS[dev] = ws
+    return ws
 
 
 def flash_fwd(a):

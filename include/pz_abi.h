@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 4
+#define PZ_ABI_VERSION 5
 
 enum {
   PZ_OK = 0,
@@ -180,6 +180,9 @@ typedef struct pz_flash_args {
   void* dq; void* dk; void* dv;
   /* optional fp32 scratch (16-byte aligned) for the query-split dK/dV partials; NULL: no split */
   float* ws; int64_t ws_bytes;
+  /* mask token of query row r = (r + mask_row0) / rows_per_token (denoise steps: queries start at
+   * the action tokens, pizero.py:461-481) */
+  int64_t mask_row0;
 } pz_flash_args;
 int pz_flash_fwd(const pz_flash_args* a, void* stream);
 /* delta[z][r] = sum_d dO[r][d] * O[r][d] (fp32) */

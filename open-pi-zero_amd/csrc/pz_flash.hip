@@ -161,7 +161,7 @@ __device__ __forceinline__ void TileStager<HD, ROW, ROWS, NT>::load_q(const pz_f
 // Mask / logit context in 32-bit registers (token of a query row by a float reciprocal: exact for
 // nq < 2^22, checked on the host) -- no 64-bit division in the inner loops
 struct FaMask {
-  int mode, nk, P, C, cnt;
+  int mode, nk, P, C, cnt, row0;
   float inv_rpt, scale, cap, inv_cap;
   __device__ __forceinline__ FaMask(const pz_flash_args& a, int64_t b) {
     mode = a.mask_mode;
@@ -170,11 +170,12 @@ struct FaMask {
     C = (int)a.cond;
     cnt = mode == 1 ? a.cnt[b] : 0;
     inv_rpt = mode == 1 ? 1.f / (float)a.rows_per_token : 0.f;
+    row0 = (int)a.mask_row0;
     scale = a.scale;
     cap = a.cap;
     inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
   }
-  __device__ __forceinline__ int token(int r) const { return (int)(((float)r + 0.5f) * inv_rpt); }
+  __device__ __forceinline__ int token(int r) const { return (int)(((float)(r + row0) + 0.5f) * inv_rpt); }
   __device__ __forceinline__ bool dead(int t) const { return mode == 1 && t < P && t >= cnt; }
   __device__ __forceinline__ bool allowed(int t, int j) const {
     if (j >= nk) return false;
@@ -725,7 +726,7 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
                    a->v_bstride % 8 == 0 && a->o_hstride % 4 == 0,
                "flash_fwd: operands need 16-byte aligned rows");
   if (a->mask_mode == 1) PZ_CHECK_ARG(a->cnt && a->rows_per_token > 0, "flash_fwd: block mask needs cnt");
-  PZ_CHECK_ARG(a->nq < (1 << 22) && a->nk < (1 << 22), "flash_fwd: nq/nk too large");
+  PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->nk < (1 << 22) && a->mask_row0 >= 0, "flash_fwd: nq/nk too large");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_fwd: too many units");
   dim3 grid((unsigned)((a->nq + 127) / 128), (unsigned)(a->Z * a->H));  // 128 query rows per workgroup
   FA_DISPATCH(a->head_dim, flash_fwd_kernel, grid, dim3((a->head_dim == 256 ? 8 : 4) * 64), 0, (hipStream_t)stream,

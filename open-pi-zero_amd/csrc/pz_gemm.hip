@@ -989,23 +989,107 @@ __device__ __forceinline__ void epi8p_fast(const GemmP& p, int64_t cofs, int64_t
   }
 }
 
+// ---- LDS-staged output images (interior tiles) ------------------------------------------------
+// A swapped-operand MFMA accumulator gives each lane 4 consecutive columns of one row, so direct
+// stores are 8 B per lane spread over 16 rows (32-B pieces of many cache lines per instruction).
+// Plain and GeGLU interior tiles instead write bf16 256 x 128 images into the idle LDS (16-B chunk
+// index XOR-swizzled by row: conflict-free 8-B writes and 16-B reads) and copy them out row-
+// contiguously, 16 B per lane (each wave instruction = 4 full 256-B row segments).
+__device__ __forceinline__ void img_put(char* img, int row, int col, u32x2 v) {
+  const int ch = col >> 3;
+  *reinterpret_cast<u32x2*>(img + row * 256 + ((ch ^ (row & 15)) << 4) + ((col >> 2) & 1) * 8) = v;
+}
+__device__ __forceinline__ void img_flush(const char* img, bf16_t* dst, int64_t ld) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = threadIdx.x + i * NT2, row = c >> 4, ch = c & 15;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(img + row * 256 + ((ch ^ (row & 15)) << 4));
+    *reinterpret_cast<u32x4*>(dst + row * ld + ch * 8) = v;
+  }
+}
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 template <bool GEGLU>
 __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
                                            int wr, int wc, int lane, const f32x4 (&acc)[8][4], char* smem) {
-  if (GEGLU) {  // stores only
+  const int g4 = 4 * (lane >> 4), rl = lane & 15;
+  if (GEGLU) {
+    if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
+      // pass 1: h (smem) -> C and g (smem + 64 KiB) -> aux[:, :I]; pass 2: u (smem) -> aux[:, I:]
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float gg[4], hh[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gg[r] = acc[rb][j][r] * p.alpha;
+            hh[r] = gelu_tanh(gg[r]) * (acc[rb][2 + j][r] * p.alpha);
+          }
+          const int row = wr * 128 + rb * 16 + rl, col = wc * 32 + j * 16 + g4;
+          img_put(smem, row, col, u32x2{pack2bf(hh[0], hh[1]), pack2bf(hh[2], hh[3])});
+          img_put(smem + 65536, row, col, u32x2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])});
+        }
+      lds_sync();
+      img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc);
+      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux);
+      lds_sync();
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float uu[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) uu[r] = acc[rb][2 + j][r] * p.alpha;
+          img_put(smem, wr * 128 + rb * 16 + rl, wc * 32 + j * 16 + g4,
+                  u32x2{pack2bf(uu[0], uu[1]), pack2bf(uu[2], uu[3])});
+        }
+      lds_sync();
+      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux);
+      return;
+    }
 #pragma unroll
     for (int rb = 0; rb < 8; ++rb) {
-      const int64_t m = m0 + wr * 128 + rb * 16 + (lane & 15);
+      const int64_t m = m0 + wr * 128 + rb * 16 + rl;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + 4 * (lane >> 4), acc[rb][j], acc[rb][2 + j]);
+      for (int j = 0; j < 2; ++j) store_geglu4(p, cofs, m, n0 + wc * 32 + j * 16 + g4, acc[rb][j], acc[rb][2 + j]);
     }
     return;
   }
   const int64_t m = m0 + wr * 128 + (lane & 15), nb = n0 + wc * 64 + 4 * (lane >> 4);
   if (m0 + BT <= p.M && n0 + BT <= p.N) {
     switch (fast_mode(p)) {
-      case FM_STORE: epi8p_fast<FM_STORE>(p, cofs, rofs, m, nb, acc); break;
+      case FM_STORE: {  // two 256 x 128 images (columns 0..127 | 128..255), one pass
+        float bias[4][4];
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          if (p.bias) {
+            unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias[cb]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bias[cb][r] = 0.f;
+          }
+        }
+        char* img = smem + (wc >> 1) * 65536;
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[cb][r];
+            img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+          }
+        lds_sync();
+        bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0;
+        img_flush(smem, C, p.ldc);
+        img_flush(smem + 65536, C + 128, p.ldc);
+        break;
+      }
       case FM_F32: epi8p_fast<FM_F32>(p, cofs, rofs, m, nb, acc); break;
       case FM_DACT: epi8p_fast<FM_DACT>(p, cofs, rofs, m, nb, acc); break;
       case FM_DGEGLU: epi8p_fast<FM_DGEGLU>(p, cofs, rofs, m, nb, acc); break;

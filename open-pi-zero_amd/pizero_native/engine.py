@@ -140,6 +140,8 @@ class Engine:
         # joint attention kernel: "gemm" = MFMA GEMMs around the soft-cap/block-mask softmax (default:
         # faster today), "flash" = the fused pz_flash kernels (no L x L tensors)
         self.joint_flash = os.environ.get("PZ_JOINT_ATTN", "gemm") == "flash"
+        # inference (prefill / denoise) attention: fused kernel unless PZ_INFER_ATTN=gemm
+        self.infer_flash = os.environ.get("PZ_INFER_ATTN", "flash") == "flash"
         if self.d.nkv != 1:
             raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
 
@@ -743,8 +745,7 @@ class Engine:
         X = {"vlm": Xv, "proprio": Xp}
         pos = {"vlm": vpos, "proprio": ppos}
         Q = torch.empty(B, L1, nh * hd, device=dev, dtype=BF16)
-        S = torch.empty(B, L1 * nh, Lp, device=dev, dtype=F32)
-        Pm = torch.empty(B, L1 * nh, Lp, device=dev, dtype=BF16)
+        S = Pm = None
         for l in range(d.nL):
             last = l == d.nL - 1
             Kj, Vj = kcache[l], vcache[l]
@@ -770,6 +771,17 @@ class Engine:
                 hs[g.name] = h
             if last:
                 break
+            if self.infer_flash:  # fused attention over the L1 prefix keys (no L1 x L1 tensor)
+                Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
+                ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, g.T, Os[g.name]) for g in groups], L1, L1, 0,
+                                                     cnt, B))
+                for g in groups:
+                    p = f"{g.prefix}{l}."
+                    X[g.name] = self._post_attn_O(g, p, X[g.name], Os[g.name])
+                continue
+            if S is None:
+                S = torch.empty(B, L1 * nh, Lp, device=dev, dtype=F32)
+                Pm = torch.empty(B, L1 * nh, Lp, device=dev, dtype=BF16)
             ops.gemm(L1 * nh, L1, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L1 * nh * hd, 0),
                      sB=(Lp * hd, 0), sC=(L1 * nh * Lp, 0))
             ops.attn_softmax(S, Lp, Pm, Lp, B * L1 * nh, L1, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,
@@ -779,6 +791,32 @@ class Engine:
                 x = X[g.name]
                 X[g.name] = self._post_attn(g, p, x, Pm, Vj, B, L1, Lp)
         return kcache, vcache
+
+    def _attn_flash_infer(self, Q, K, V, outs, Lq, nk, tok0, cnt, B):
+        """pz_flash_args for the inference attention: queries = Lq tokens starting at joint token tok0
+        (rows token*nh + head of Q [B, Lq*nh, hd]), keys = the first nk cached tokens; outs =
+        [(token offset, T, O [B*T, nh*hd])] in token order."""
+        d = self.d
+        nh, hd, Lp = d.nh, d.hd, K.shape[1]
+        return ops.flash_args(
+            B, 1, Lq * nh, nk, hd, Q, (hd, Lq * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+            [((off - tok0) * nh, O, T * nh * hd, hd) for off, T, O in outs], 0, None, 1.0 / math.sqrt(hd), cap=50.0,
+            mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh, mask_row0=tok0 * nh)
+
+    def _post_attn_O(self, g, p, x, O):
+        """o_proj (+resid), post-attention RMSNorm, GeGLU MLP (+resid) of one mixture."""
+        d = self.d
+        M = x.shape[0]
+        dev = x.device
+        xm = torch.empty_like(x)
+        ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
+        h2 = torch.empty_like(x)
+        ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)
+        hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+        ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
+        xn = torch.empty_like(x)
+        ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
+        return xn
 
     def _post_attn(self, g, p, x, Pm, Vj, B, Lq, Lp, qrow0=None):
         d = self.d
@@ -812,8 +850,7 @@ class Engine:
         g = Group("action", "joint_model.mixtures.action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI, d.a_theta,
                   False, "action")
         Q = torch.empty(B, d.H, nh * hd, device=dev, dtype=BF16)
-        S = torch.empty(B, d.H * nh, Lp, device=dev, dtype=F32)
-        Pm = torch.empty(B, d.H * nh, Lp, device=dev, dtype=BF16)
+        S = Pm = O = None
         for l in range(d.nL):
             p = f"{g.prefix}{l}."
             Kj, Vj = kcache[l], vcache[l]
@@ -823,6 +860,15 @@ class Engine:
             qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
             ops.linear(h, self.qkv_w(p), qkv)
             ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
+            if self.infer_flash:  # fused attention of the action queries over every cached key
+                if O is None:
+                    O = torch.empty(B * d.H, nh * hd, device=dev, dtype=BF16)
+                ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, d.H, O)], d.H, L, g.off, cnt, B))
+                x = self._post_attn_O(g, p, x, O)
+                continue
+            if S is None:
+                S = torch.empty(B, d.H * nh, Lp, device=dev, dtype=F32)
+                Pm = torch.empty(B, d.H * nh, Lp, device=dev, dtype=BF16)
             ops.gemm(d.H * nh, L, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(d.H * nh * hd, 0),
                      sB=(Lp * hd, 0), sC=(d.H * nh * Lp, 0))
             ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,

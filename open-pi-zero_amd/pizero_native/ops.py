@@ -292,7 +292,7 @@ def attn_softmax_bwd(P, dP, lddp, tcap, dS, ldp, R, N, scale, cap):
 
 def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, groups, o_hstride, lse, scale,
                cap=0.0, mask_mode=0, cnt=None, prefix=0, cond=0, rows_per_token=1, dgroups=None, delta=None,
-               dq=None, dk=None, dv=None):
+               dq=None, dk=None, dv=None, mask_row0=0):
     """pz_flash_args (include/pz_abi.h).  *_strides = (ld, bstride, hstride) in elements; groups =
     [(row0, O tensor, bstride, ld), ...] (dgroups: the dO tensors of the same groups)."""
     a = FlashArgs()
@@ -309,6 +309,7 @@ def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, group
     a.lse = _p(lse)
     a.scale, a.cap, a.mask_mode = float(scale), float(cap), int(mask_mode)
     a.cnt, a.prefix, a.cond, a.rows_per_token = _p(cnt), int(prefix), int(cond), int(rows_per_token)
+    a.mask_row0 = int(mask_row0)
     a.delta, a.dq, a.dk, a.dv = _p(delta), _p(dq), _p(dk), _p(dv)
     if dq is not None:  # fp32 scratch for the query-split dK/dV partials
         ws = flash_workspace(dq.device)

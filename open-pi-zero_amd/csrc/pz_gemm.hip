@@ -1013,6 +1013,112 @@ __device__ __forceinline__ void lds_sync() {
   asm volatile("" ::: "memory");
 }
 
+// staged epilogue with side inputs (interior tiles): alpha*acc (+bias) -> two bf16 256 x 128 LDS images,
+// then each thread finishes 16-B row chunks: residual / old C / saved activations are read as 16-B
+// row-contiguous loads (a batch of 8 chunks in flight), outputs written as 16-B stores.
+//   FM_BF16: [aux = pre; act(pre)] (+ resid) (+ old C);  FM_DACT: * act'(aux);  FM_DGEGLU: d(gate|up)
+__device__ __forceinline__ void unpack8(const u32x4& w, float (&o)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    o[2 * i] = __uint_as_float(w[i] << 16);
+    o[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack8v(const float (&v)[8]) {
+  return u32x4{pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]), pack2bf(v[6], v[7])};
+}
+
+template <int FM>
+__device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
+                                             int wr, int wc, int lane, const f32x4 (&acc)[8][4], char* smem) {
+  const int g4 = 4 * (lane >> 4), rl = lane & 15;
+  const int64_t nb = n0 + wc * 64 + g4;
+  char* img = smem + (wc >> 1) * 65536;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (FM == FM_BF16 && p.bias) unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[r];
+      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+    }
+  }
+  lds_sync();
+  bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0;
+  const bf16_t* X0 = nullptr;  // side input 0: aux (DACT: pre-activation, DGEGLU: g) or old C
+  const bf16_t* X1 = nullptr;  // side input 1: resid or DGEGLU u
+  int64_t ld0 = 0, ld1 = 0;
+  if (FM == FM_DACT || FM == FM_DGEGLU) {
+    X0 = p.aux + m0 * p.ld_aux + n0;
+    ld0 = p.ld_aux;
+    if (FM == FM_DGEGLU) {
+      X1 = X0 + p.geglu_I;
+      ld1 = p.ld_aux;
+    }
+  } else {
+    if (p.beta) {
+      X0 = C;
+      ld0 = p.ldc;
+    }
+    if (p.resid) {
+      X1 = p.resid + rofs + m0 * p.ld_resid + n0;
+      ld1 = p.ld_resid;
+    }
+  }
+  const bool act = FM == FM_BF16 && (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU);
+  const bool gelu = p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_DGELU;
+#pragma unroll
+  for (int half = 0; half < 4; ++half) {  // 4 batches of 4 chunks: a batch's loads issued together
+    u32x4 a0[4], a1[4], iv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = threadIdx.x + (half * 4 + i) * NT2;  // 0 .. 8191 over the two images
+      const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
+      const int col = im * 128 + ch * 8;
+      iv[i] = *reinterpret_cast<const u32x4*>(smem + im * 65536 + row * 256 + ((ch ^ (row & 15)) << 4));
+      a0[i] = X0 ? *reinterpret_cast<const u32x4*>(X0 + row * ld0 + col) : u32x4{0u, 0u, 0u, 0u};
+      a1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = threadIdx.x + (half * 4 + i) * NT2;
+      const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
+      const int col = im * 128 + ch * 8;
+      float v[8], x0[8], x1[8];
+      unpack8(iv[i], v);
+      unpack8(a0[i], x0);
+      unpack8(a1[i], x1);
+      bf16_t* Cp = C + row * p.ldc + col;
+      if (FM == FM_DGEGLU) {
+        float dg[8], du[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          dg[e] = v[e] * x1[e] * gelu_tanh_grad(x0[e]);
+          du[e] = v[e] * gelu_tanh(x0[e]);
+        }
+        *reinterpret_cast<u32x4*>(Cp) = pack8v(dg);
+        *reinterpret_cast<u32x4*>(Cp + p.geglu_I) = pack8v(du);
+      } else if (FM == FM_DACT) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] *= gelu ? gelu_tanh_grad(x0[e]) : silu_grad(x0[e]);
+        *reinterpret_cast<u32x4*>(Cp) = pack8v(v);
+      } else {
+        if (act) {
+          if (p.aux) *reinterpret_cast<u32x4*>(p.aux + (m0 + row) * p.ld_aux + n0 + col) = iv[i];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = gelu ? gelu_tanh(v[e]) : silu(v[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += x1[e] + x0[e];  // resid, old C (zeros when absent)
+        *reinterpret_cast<u32x4*>(Cp) = pack8v(v);
+      }
+    }
+  }
+}
+
 template <bool GEGLU>
 __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
                                            int wr, int wc, int lane, const f32x4 (&acc)[8][4], char* smem) {
@@ -1091,9 +1197,9 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
         break;
       }
       case FM_F32: epi8p_fast<FM_F32>(p, cofs, rofs, m, nb, acc); break;
-      case FM_DACT: epi8p_fast<FM_DACT>(p, cofs, rofs, m, nb, acc); break;
-      case FM_DGEGLU: epi8p_fast<FM_DGEGLU>(p, cofs, rofs, m, nb, acc); break;
-      default: epi8p_fast<FM_BF16>(p, cofs, rofs, m, nb, acc); break;
+      case FM_DACT: epi8p_staged<FM_DACT>(p, cofs, rofs, m0, n0, wr, wc, lane, acc, smem); break;
+      case FM_DGEGLU: epi8p_staged<FM_DGEGLU>(p, cofs, rofs, m0, n0, wr, wc, lane, acc, smem); break;
+      default: epi8p_staged<FM_BF16>(p, cofs, rofs, m0, n0, wr, wc, lane, acc, smem); break;
     }
     return;
   }

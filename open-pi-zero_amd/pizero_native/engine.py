@@ -722,6 +722,53 @@ class Engine:
         if self.post_backward is not None:
             self.post_backward()
 
+    # ================================================== JointModel alone ==
+    def joint_train(self, embeds, pos, cnt, dout, beta=False):
+        """JointModel.forward + backward alone (joint_model.py:328-383) on given embeddings -- the
+        harness of config C5 (3 images + chunk 50, which the reference composes at this level since
+        its PiZero takes one image per sample).  embeds: {"vlm": [B, P, gH], "proprio": [B, C, aH],
+        "action": [B, H, aH]} bf16 (scaled by sqrt(hidden) here, joint_model.py:348-355); dout: d(loss)
+        wrt the final-normed action hidden states [B, H, aH].  Accumulates parameter gradients into
+        the gradient arena and returns (action hidden [B, H, aH] bf16, {name: d embeds})."""
+        d = self.d
+        Ev, Ep, Ea = embeds["vlm"], embeds["proprio"], embeds["action"]
+        B = Ev.shape[0]
+        dev = Ev.device
+        if not self.m._tied:
+            raise NotImplementedError("joint_train expects tie_action_proprio_weights() (pizero.py:262-264)")
+        Xv = torch.empty(B * d.P, d.gH, device=dev, dtype=BF16)
+        ops.copy_rows(Ev.reshape(B * d.P, d.gH), d.gH, 0, Xv, d.gH, 0, 1, B * d.P, d.gH, scale=math.sqrt(d.gH))
+        T = d.C + d.H
+        sa = math.sqrt(d.aH)
+        Xe = torch.empty(B * T, d.aH, device=dev, dtype=BF16)
+        ops.copy_rows(Ep.reshape(B * d.C, d.aH), d.aH, d.C * d.aH, Xe, d.aH, T * d.aH, B, d.C, d.aH, scale=sa)
+        ops.copy_rows(Ea.reshape(B * d.H, d.aH), d.aH, d.H * d.aH, Xe[d.C:], d.aH, T * d.aH, B, d.H, d.aH, scale=sa)
+        groups = self.groups(True)
+        save = {}
+        X = self._joint_layers_train(groups, {"vlm": Xv, "expert": Xe}, pos, cnt, B, save)
+        Xl = X["expert"]
+        ya = torch.empty_like(Xl)
+        ra = torch.empty(Xl.shape[0], device=dev, dtype=F32)
+        ops.rmsnorm(Xl, self.w("joint_model.mixtures.action.norm.weight"), ya, ra, d.rms_eps)
+        dya = torch.zeros_like(ya)  # proprio rows are not outputs (joint_model.py:375-380 skip list)
+        ops.copy_rows(dout.reshape(B * d.H, d.aH).to(BF16), d.aH, d.H * d.aH, dya[d.C:], d.aH, T * d.aH, B, d.H, d.aH)
+        rpp = ops.rows_per_part()
+        dXl = torch.empty_like(dya)
+        part = torch.empty((B * T + rpp - 1) // rpp, d.aH, device=dev, dtype=F32)
+        ops.rmsnorm_bwd(dya, Xl, self.w("joint_model.mixtures.action.norm.weight"), ra, dXl, dw_part=part)
+        self._norm_grads("joint_model.mixtures.action.norm.", part, None, beta)
+        dX = self._joint_layers_backward(groups, {"vlm": None, "expert": dXl}, pos, cnt, B, save, beta)
+        dEv = torch.empty(B, d.P, d.gH, device=dev, dtype=BF16)
+        ops.copy_rows(dX["vlm"], d.gH, 0, dEv.view(B * d.P, d.gH), d.gH, 0, 1, B * d.P, d.gH, scale=math.sqrt(d.gH))
+        dEp = torch.empty(B, d.C, d.aH, device=dev, dtype=BF16)
+        dEa = torch.empty(B, d.H, d.aH, device=dev, dtype=BF16)
+        ops.copy_rows(dX["expert"], d.aH, T * d.aH, dEp.view(B * d.C, d.aH), d.aH, d.C * d.aH, B, d.C, d.aH, scale=sa)
+        ops.copy_rows(dX["expert"][d.C:], d.aH, T * d.aH, dEa.view(B * d.H, d.aH), d.aH, d.H * d.aH, B, d.H, d.aH,
+                      scale=sa)
+        out = torch.empty(B, d.H, d.aH, device=dev, dtype=BF16)
+        ops.copy_rows(ya[d.C:], d.aH, T * d.aH, out.view(B * d.H, d.aH), d.aH, d.H * d.aH, B, d.H, d.aH)
+        return out, {"vlm": dEv, "proprio": dEp, "action": dEa}
+
     # ============================================================ inference ==
     def prefill(self, ids, pix, cnt, vpos, ppos, proprios, kcache, vcache):
         """pizero.py:430-451: SigLIP + prefix pass over {vlm, proprio}; writes post-RoPE K/V caches."""

@@ -1,0 +1,122 @@
+"""Golden fixture for config C5 (BASELINE.json configs[4], the Pi0-paper shape) from the REFERENCE.
+
+Run from the repo root (build container only):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden_c5.py
+
+The reference PiZero has one image per sample (pizero.py:389-413), so C5 -- 3 images (768 image
+tokens) + 20 text + 1 proprio + an action chunk of 50, L = 839 -- is composed at the JointModel
+level: the reference's own ``JointModel`` (joint_model.py:307-383, built from the
+bridge.yaml joint config at full Gemma-2B / action-expert dims, proprio mixture tied to action
+weights as pizero.py:262-264 does) runs forward + backward on generator-defined embeddings,
+with the reference's own block mask / positions (pizero.py:271-324, 8 pad text tokens).  Loss =
+sum(action_hidden * R) for a generator-defined R.  Stored: the action hidden states, the input
+embedding gradients (norm + first 64 values) and ~30 parameter gradients (norm + first 64), in
+fp32 and in bf16 (the reference's own bf16-vs-fp32 deviation sets the GPU tolerance).
+Inputs are regenerated from seeds on both sides (oracle/synth.py; pz_fill_uniform on device).
+Nothing under /root/reference is copied; this script only imports it.
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+
+from make_golden import install_stubs, ref_cfg  # noqa: E402
+from oracle.pizero_oracle import FULL_DIMS, synth_weights  # noqa: E402
+from oracle.synth import synth_tensor  # noqa: E402
+
+C5_DIMS = dict(FULL_DIMS, max_seq_len=788, horizon_steps=50)
+C5_CNT = 780  # image/text tokens actually present (8 pad text tokens exercise the pad rows)
+C5_INPUTS = {  # name -> (shape, scale) of the generator-defined inputs (offset 0)
+    "c5/embeds.vlm": ((1, 788, 2048), 1.0),
+    "c5/embeds.proprio": ((1, 1, 1024), 1.0),
+    "c5/embeds.action": ((1, 50, 1024), 1.0),
+    "c5/R": ((1, 50, 1024), 1.0),
+}
+
+
+def c5_grad_names():
+    names = []
+    for mix in ("vlm", "action"):
+        for i in (0, 9, 17):
+            p = f"mixtures.{mix}.layers.{i}."
+            names += [p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight", p + "self_attn.o_proj.weight",
+                      p + "mlp.gate_proj.weight", p + "mlp.down_proj.weight", p + "input_layernorm.weight"]
+            if not (mix == "vlm" and i == 17):
+                names += [p + "self_attn.v_proj.weight", p + "post_attention_layernorm.weight"]
+    names += ["mixtures.action.norm.weight"]
+    return names
+
+
+def run(dtype):
+    from hydra.utils import instantiate
+    from src.model.vla import pizero as pz
+
+    d = C5_DIMS
+    cfg = ref_cfg(d)
+    torch.manual_seed(0)
+    joint = instantiate(cfg.joint)
+    W = synth_weights(d)
+    sd = joint.state_dict()
+    joint.load_state_dict({k: torch.as_tensor(W["joint_model." + k]) for k in sd}, strict=True)
+    # tie proprio <- action (pizero.py:262-264)
+    joint.mixtures["proprio"] = joint.mixtures["action"]
+    joint.to(dtype)
+    ns = types.SimpleNamespace(max_image_text_tokens=788, num_proprio_tokens=1, num_action_tokens=50,
+                               total_num_tokens=839)
+    am = torch.zeros(1, 788, dtype=torch.int64)
+    am[:, :C5_CNT] = 1
+    mask, vpos, ppos, apos = pz.PiZero.build_causal_mask_and_position_ids(ns, am, dtype)
+    inp = {k: torch.from_numpy(synth_tensor(k, s, 0.0, sc)) for k, (s, sc) in C5_INPUTS.items()}
+    leaves = {n: inp[f"c5/embeds.{n}"].to(dtype).requires_grad_() for n in ("vlm", "proprio", "action")}
+    embeds = {n: leaves[n] * 1 for n in ("vlm", "proprio", "action")}  # JointModel scales in place
+    out = joint(attention_mask=mask, position_ids_all={"vlm": vpos, "proprio": ppos, "action": apos},
+                embeds_all=embeds)
+    ya = out["action"]
+    loss = (ya.float() * inp["c5/R"]).sum()
+    loss.backward()
+    res = {"action_hidden": ya.detach().float().numpy()}
+    for n, lf in leaves.items():
+        g = lf.grad.detach().double()
+        res[f"dembeds/{n}/norm"] = np.float64(g.norm().item())
+        res[f"dembeds/{n}/head"] = g.flatten()[:64].numpy()
+    named = dict(joint.named_parameters())
+    for n in c5_grad_names():
+        p = named.get(n) if n in named else named.get(n.replace("mixtures.action.", "mixtures.proprio."))
+        if p is None or p.grad is None:
+            res[f"gradnorm/{n}"] = np.float64(-1.0)
+            continue
+        g = p.grad.detach().double()
+        res[f"gradnorm/{n}"] = np.float64(g.norm().item())
+        res[f"gradhead/{n}"] = g.flatten()[:64].numpy()
+    return res
+
+
+def main():
+    install_stubs()
+    sys.path.insert(0, REF)
+    torch.set_num_threads(os.cpu_count() or 8)
+    out = {"cnt": np.int64(C5_CNT), "grad_names": np.array(c5_grad_names())}
+    for tag, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        t0 = time.time()
+        r = run(dt)
+        print(f"{tag}: {time.time() - t0:.1f}s", flush=True)
+        for k, v in r.items():
+            out[f"{tag}/{k}"] = v
+    path = os.path.join(ROOT, "tests", "golden", "c5.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+if __name__ == "__main__":
+    main()

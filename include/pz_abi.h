@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 5
+#define PZ_ABI_VERSION 6
 
 enum {
   PZ_OK = 0,
@@ -71,6 +71,11 @@ typedef struct pz_gemm_args {
    * workgroups into fp32 slabs and a second kernel sums them and applies the epilogue.
    * NULL / 0 disables the split.  Deterministic (no atomics). */
   void* workspace; int64_t ws_bytes;
+  /* optional fused Gemma RMSNorm of the A rows (paligemma/modules.py:7-21): A is the raw x and
+   * the product uses x*rsqrt(mean_k(x^2)+norm_eps)*(1+norm_w[k]) (norm_w bf16 [K]).  Only for
+   * the few-row path (M <= 16, k-contiguous A and B, K % 32 == 0: inference denoise rows);
+   * PZ_ERR_ARG otherwise.  NULL disables. */
+  const void* norm_w; float norm_eps;
 } pz_gemm_args;
 int pz_gemm(const pz_gemm_args* args, void* stream);
 /* name of the kernel pz_gemm would launch for args (profiling / bench labels); never fails */

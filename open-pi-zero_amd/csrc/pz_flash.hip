@@ -218,9 +218,14 @@ __global__ void __launch_bounds__(FaDims<HD>::FNW * 64) flash_fwd_kernel(pz_flas
     zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
     zero_pad_cols<HD, D::HDV, D::ROW, FA_KB, NT>(Vs2[bi]);
   }
+  // key split (gridDim.z > 1, few query blocks: inference): key blocks [kb_begin, kb_end) only,
+  // unnormalised O + (m, l) partials to the workspace, merged by flash_fwd_combine_kernel
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  const int per = (nkb + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int kb_begin = (int)blockIdx.z * per, kb_end = min(nkb, kb_begin + per);
   TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
-  stk.load(K, a.ldk, 0, a.nk);
-  stv.load(V, a.ldv, 0, a.nk);
+  stk.load(K, a.ldk, (int64_t)kb_begin * FA_KB, a.nk);
+  stv.load(V, a.ldv, (int64_t)kb_begin * FA_KB, a.nk);
 
   // Q^T fragments (B operand: k = head dim, n = query) straight from HBM, zero past HD / nq
   bf16x8 qf[NQB][D::NKS];
@@ -245,15 +250,14 @@ __global__ void __launch_bounds__(FaDims<HD>::FNW * 64) flash_fwd_kernel(pz_flas
     l[qb] = 0.f;
   }
 
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
   __syncthreads();  // pad columns zeroed
   stk.store(Ks2[0]);
   stv.store(Vs2[0]);
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bf16_t* Ks = Ks2[kb & 1];
-    const bf16_t* Vs = Vs2[kb & 1];
-    const bool more = kb + 1 < nkb;
+  for (int kb = kb_begin; kb < kb_end; ++kb) {
+    const bf16_t* Ks = Ks2[(kb - kb_begin) & 1];
+    const bf16_t* Vs = Vs2[(kb - kb_begin) & 1];
+    const bool more = kb + 1 < kb_end;
     if (more) {  // next K/V tile in flight during this tile's MFMAs
       stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
       stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
@@ -319,10 +323,30 @@ __global__ void __launch_bounds__(FaDims<HD>::FNW * 64) flash_fwd_kernel(pz_flas
         for (int qb = 0; qb < NQB; ++qb) o[db][qb] = mfma(vf, pf[k2][qb], o[db][qb]);
       }
     if (more) {
-      stk.store(Ks2[(kb + 1) & 1]);
-      stv.store(Vs2[(kb + 1) & 1]);
+      stk.store(Ks2[(kb + 1 - kb_begin) & 1]);
+      stv.store(Vs2[(kb + 1 - kb_begin) & 1]);
     }
     __syncthreads();
+  }
+  if (gridDim.z > 1) {
+    float* pO = (float*)a.ws;
+    float* pml = pO + (int64_t)gridDim.z * gridDim.y * a.nq * HD;
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) {
+      const int64_t r = q0 + qb * 16 + (lane & 15);
+      if (r >= a.nq) continue;
+      const int64_t row = ((int64_t)blockIdx.z * gridDim.y + zh) * a.nq + r;
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) {
+        const int d = db * 16 + 4 * g;
+        if (d < HD) *reinterpret_cast<f32x4*>(pO + row * HD + d) = o[db][qb];
+      }
+      if (g == 0) {
+        pml[2 * row] = m[qb];
+        pml[2 * row + 1] = l[qb];
+      }
+    }
+    return;
   }
   // O[r][d..d+3] = O^T / l; lse
   const FaRow fr{&a};
@@ -342,6 +366,36 @@ __global__ void __launch_bounds__(FaDims<HD>::FNW * 64) flash_fwd_kernel(pz_flas
     }
     if (g == 0 && a.lse) a.lse[zh * a.nq + r] = m[qb] + __logf(l[qb]);
   }
+}
+
+// key-split merge: one thread per (unit, query row, 4 head dims); fixed split order
+template <int HD>
+__global__ void __launch_bounds__(256) flash_fwd_combine_kernel(pz_flash_args a, int nsp) {
+  const int64_t ZH = a.Z * a.H;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ZH * a.nq * (HD / 4)) return;
+  const int d = (int)(i % (HD / 4)) * 4;
+  const int64_t zr = i / (HD / 4), r = zr % a.nq, zh = zr / a.nq;
+  const float* pO = (const float*)a.ws;
+  const float* pml = pO + (int64_t)nsp * ZH * a.nq * HD;
+  float M = -INFINITY;
+  for (int s = 0; s < nsp; ++s) M = fmaxf(M, pml[2 * ((s * ZH + zh) * a.nq + r)]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float L = 0.f;
+  for (int s = 0; s < nsp; ++s) {
+    const int64_t row = (s * ZH + zh) * a.nq + r;
+    const float ms = pml[2 * row];
+    if (ms == -INFINITY) continue;
+    const float w = __expf(ms - M);
+    L += w * pml[2 * row + 1];
+    acc += w * *reinterpret_cast<const f32x4*>(pO + row * HD + d);
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const FaRow fr{&a};
+  const int gi = fr.grp(r);
+  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(zh / a.H, zh % a.H, r, gi);
+  *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(acc[0] * inv, acc[1] * inv), pack2bf(acc[2] * inv, acc[3] * inv)};
+  if (d == 0 && a.lse) a.lse[zh * a.nq + r] = M + __logf(L);
 }
 
 // ----------------------------------------------------------------- backward --
@@ -602,9 +656,14 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
     zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
     zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
   }
+  // key split (gridDim.z > 1, few query blocks: inference): key blocks [kb_begin, kb_end) only,
+  // unnormalised O + (m, l) partials to the workspace, merged by flash_fwd_combine_kernel
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  const int per = (nkb + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int kb_begin = (int)blockIdx.z * per, kb_end = min(nkb, kb_begin + per);
   TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
-  stk.load(K, a.ldk, 0, a.nk);
-  stv.load(V, a.ldv, 0, a.nk);
+  stk.load(K, a.ldk, (int64_t)kb_begin * FA_KB, a.nk);
+  stv.load(V, a.ldv, (int64_t)kb_begin * FA_KB, a.nk);
   bf16x8 qf[D::NKS], df[D::NKS];
   const bool live = r < a.nq;
   const bf16_t* dOr = nullptr;
@@ -636,15 +695,14 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
 #pragma unroll
   for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
   __syncthreads();  // pad columns zeroed
   stk.store(Ks2[0]);
   stv.store(Vs2[0]);
   __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bf16_t* Ks = Ks2[kb & 1];
-    const bf16_t* Vs = Vs2[kb & 1];
-    const bool more = kb + 1 < nkb;
+  for (int kb = kb_begin; kb < kb_end; ++kb) {
+    const bf16_t* Ks = Ks2[(kb - kb_begin) & 1];
+    const bf16_t* Vs = Vs2[(kb - kb_begin) & 1];
+    const bool more = kb + 1 < kb_end;
     if (more) {
       stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
       stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
@@ -728,10 +786,29 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   if (a->mask_mode == 1) PZ_CHECK_ARG(a->cnt && a->rows_per_token > 0, "flash_fwd: block mask needs cnt");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->nk < (1 << 22) && a->mask_row0 >= 0, "flash_fwd: nq/nk too large");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_fwd: too many units");
-  dim3 grid((unsigned)((a->nq + 127) / 128), (unsigned)(a->Z * a->H));  // 128 query rows per workgroup
-  FA_DISPATCH(a->head_dim, flash_fwd_kernel, grid, dim3((a->head_dim == 256 ? 8 : 4) * 64), 0, (hipStream_t)stream,
-              *a);
+  const int64_t qblk = (a->nq + 127) / 128, units = qblk * a->Z * a->H;  // 128 query rows per workgroup
+  // few workgroups (inference: one action chunk, one prefix): split the keys over up to 16
+  // workgroups per unit when the caller gave a workspace for the partials
+  const int64_t nkb = (a->nk + FA_KB - 1) / FA_KB;
+  int64_t sp = 1;
+  if (a->ws && units < 128 && nkb > 1 && a->head_dim % 4 == 0) {
+    sp = (256 + units - 1) / units;
+    sp = sp < nkb ? sp : nkb;
+    sp = sp < 16 ? sp : 16;
+    while (sp > 1 && sp * a->Z * a->H * a->nq * (a->head_dim + 2) * 4 > a->ws_bytes) --sp;
+    const int64_t per = (nkb + sp - 1) / sp;
+    sp = (nkb + per - 1) / per;  // no empty split
+  }
+  dim3 grid((unsigned)qblk, (unsigned)(a->Z * a->H), (unsigned)sp);
+  hipStream_t st = (hipStream_t)stream;
+  FA_DISPATCH(a->head_dim, flash_fwd_kernel, grid, dim3((a->head_dim == 256 ? 8 : 4) * 64), 0, st, *a);
   PZ_CHECK_LAUNCH();
+  if (sp > 1) {
+    const int64_t n = a->Z * a->H * a->nq * (a->head_dim / 4);
+    FA_DISPATCH(a->head_dim, flash_fwd_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a,
+                (int)sp);
+    PZ_CHECK_LAUNCH();
+  }
   return PZ_OK;
 }
 

@@ -47,6 +47,9 @@ struct GemmP {
   // dp_tiles + u is K-piece (u % tail_s) (tail_kt K-tiles) of tile dp_tiles + u / tail_s, whose raw
   // accumulators go to ws[u] (256 KiB, thread-major) for gemm8p_tail_epilogue.
   int dp_tiles, tail_s, tail_kt;
+  // fused Gemma RMSNorm of the A rows (skinny path only): bf16 (1 + w) weights [K] or NULL
+  const bf16_t* nw;
+  float neps;
 };
 
 __device__ __forceinline__ int sw_tr(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
@@ -1438,6 +1441,202 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc, smem);
 }
 
+// ---- k-half variant of the ping-pong kernel -----------------------------------
+// Same tile (256 x 256 x 64, 8 waves of 128 x 64), same accumulator layout, epilogue and split
+// tail as gemm8p_kernel, but each K-tile is consumed in TWO segments per wave -- k 0..31 then
+// k 32..63, each 32 MFMAs over the whole 128 x 64 wave tile -- instead of four 16-MFMA quadrant
+// segments: half the barriers per K-tile and twice the matrix work beside each partner's
+// LDS-read segment.  LDS regions are k-halves (per buffer: A h0 | A h1 | B h0 | B h1, 16 KiB
+// each): k-contiguous images are [256 rows][32 k] (64-B rows, 16-B chunk c of row r at
+// c ^ 3*((r >> 3) & 1): conflict-free ds_read_b128), k-strided ones the [32 k][256 rows] images of
+// gemm8p_kernel.  Region (kt, h) is refilled with tile kt + 2 as soon as both wave groups have read
+// it (h0 in segment 2 of kt, h1 in segment 0 of kt + 1): ~1.5 K-tiles of loads stay in flight.
+constexpr int KH_REG = 16384;
+
+template <bool GEGLU>
+__device__ __forceinline__ int64_t kh_rowB(int v, int64_t row0, int64_t R, int64_t gI) {
+  if (GEGLU) {  // virtual column v: wave (v >> 6), gate/up (v >> 5 & 1)
+    int64_t g = row0 + (v >> 6) * 32 + (v & 31);
+    g = g < gI ? g : gI - 1;
+    return ((v >> 5) & 1) ? gI + g : g;
+  }
+  const int64_t g = row0 + v;
+  return g < R ? g : R - 1;
+}
+
+// per-thread global source of DMA instruction i (0/1) of the k-half-0 region image of an operand
+template <bool KC, bool GEGLU>
+__device__ __forceinline__ const bf16_t* kh_src(const bf16_t* base, int64_t ld, int i, int t, int64_t row0,
+                                                int64_t R, int64_t gI) {
+  if (KC) {
+    const int r = i * 128 + (t >> 2);
+    const int ch = (t & 3) ^ (3 * ((r >> 3) & 1));
+    return base + kh_rowB<GEGLU>(r, row0, R, gI) * ld + 8 * ch;
+  } else {
+    const int k = i * 16 + (t >> 5);
+    const int c = (t & 31) ^ (sw_tr(k) >> 1);
+    int64_t g = row0 + 8 * c;
+    g = g <= R - 8 ? g : R - 8;
+    return base + (int64_t)k * ld + g;
+  }
+}
+
+template <bool KC>
+__device__ __forceinline__ bf16x8 kh_frag(const char* opbase, int h, int rb, int lane) {
+  if (KC) {
+    const char* reg = opbase + h * KH_REG;
+    const int r = rb * 16 + (lane & 15);
+    const int ch = lane >> 4;
+    return *reinterpret_cast<const bf16x8*>(reg + r * 64 + ((ch ^ (3 * ((r >> 3) & 1))) << 4));
+  } else {
+    return frag_tr_asm<512>(opbase, rb, h, lane);  // k-half h = k-rows 32h.. at 16 KiB * h
+  }
+}
+
+template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
+__global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nk_all = (int)((p.K + 63) / 64);
+  int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
+  if (p.tail_s && lid >= p.dp_tiles) {
+    const int u = lid - p.dp_tiles;
+    piece = u;
+    lid = p.dp_tiles + u / p.tail_s;
+    kt0 = (u % p.tail_s) * p.tail_kt;
+    nk = min(nk_all - kt0, p.tail_kt);
+  }
+  int tm, tn;
+  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  const int64_t m0 = (int64_t)tm * BT;
+  const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int64_t z = blockIdx.y;
+  const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
+  const bf16_t* Ab = p.A + zo * p.sAo + zi * p.sAi;
+  const bf16_t* Bb = p.B + zo * p.sBo + zi * p.sBi;
+
+  const int64_t stepA = AKC ? 64 : 64 * p.lda;
+  const int64_t stepB = BKC ? 64 : 64 * p.ldb;
+  const int64_t halfA = AKC ? 32 : 32 * p.lda;
+  const int64_t halfB = BKC ? 32 : 32 * p.ldb;
+  const bf16_t* srcA[2];
+  const bf16_t* srcB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    srcA[i] = kh_src<AKC, false>(Ab, p.lda, i, t, m0, p.M, 0) + kt0 * stepA;
+    srcB[i] = kh_src<BKC, GEGLU>(Bb, p.ldb, i, t, n0, p.N, p.geglu_I) + kt0 * stepB;
+  }
+  const int krem = (KTAIL && kt0 + nk == nk_all) ? (int)(p.K - (int64_t)(nk_all - 1) * 64) : 64;
+  // K % 64 != 0: every lane's source of the last K-tile is clamped into the tensor (finite data)
+  // and the A fragments of k >= krem are zeroed before the MFMAs
+  auto clamp_tail = [&](const bf16_t* g, bool kc, int h, int i, int64_t ld, int kt) {
+    if (KTAIL && krem < 64 && kt == nk - 1) {
+      if (kc) {
+        const int r = i * 128 + (t >> 2);
+        const int kl = 32 * h + 8 * ((t & 3) ^ (3 * ((r >> 3) & 1)));
+        if (kl >= krem) g -= kl - (krem - 8);
+      } else {
+        const int kl = 32 * h + i * 16 + (t >> 5);
+        if (kl >= krem) g -= (int64_t)(kl - (krem - 1)) * ld;
+      }
+    }
+    return g;
+  };
+  // k-half h of K-tile kt (both operands): 2 + 2 DMA instructions per wave
+  auto issue = [&](int kt, int h) {
+    char* dst = smem + (kt & 1) * P8_BUF + h * KH_REG + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      glds16(clamp_tail(srcA[i] + kt * stepA + h * halfA, AKC, h, i, p.lda, kt), dst + i * 8192);
+      glds16(clamp_tail(srcB[i] + kt * stepB + h * halfB, BKC, h, i, p.ldb, kt), dst + 2 * KH_REG + i * 8192);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[8], bfr[4];
+  auto read_frags = [&](const char* buf, int h) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = kh_frag<AKC>(buf, h, wr * 8 + i, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = kh_frag<BKC>(buf + 2 * KH_REG, h, wc * 4 + j, lane);
+  };
+  auto mask_tail_a = [&](int kt, int h) {
+    if (KTAIL && krem < 64 && kt == nk - 1) {
+      if (32 * h + 8 * (lane >> 4) >= krem) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) af[i] = bf16x8{};
+      }
+    }
+  };
+  auto mfma_half = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // issue order: (0,0) (0,1) (1,0) | per tile kt: (kt+1,1) in segment 0, (kt+2,0) in segment 2.
+  // Waits (4 DMA instructions per wave per k-half): segment 0 retires (kt,1), segment 2 retires
+  // (kt+1,0); each is followed by the barrier the next reader of that region passes.
+  issue(0, 0);
+  issue(0, 1);
+  if (nk > 1) {
+    issue(1, 0);
+    PZ_WAIT_VM(8);
+  } else {
+    PZ_WAIT_VM(4);
+  }
+  PZ_RAW_BARRIER();
+  if (wr == 1) PZ_RAW_BARRIER();  // stagger: waves 4..7 run one barrier behind
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* buf = smem + (kt & 1) * P8_BUF;
+    const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+    // segment 0: read k-half 0
+    if (n1) issue(kt + 1, 1);
+    read_frags(buf, 0);
+    if (n1) PZ_WAIT_VM(8);
+    else PZ_WAIT_VM(0);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    // segment 1: MFMAs of k-half 0
+    mask_tail_a(kt, 0);
+    mfma_half();
+    PZ_RAW_BARRIER();
+    // segment 2: read k-half 1
+    if (n2) issue(kt + 2, 0);
+    read_frags(buf, 1);
+    if (n2) PZ_WAIT_VM(8);
+    else if (n1) PZ_WAIT_VM(4);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    // segment 3: MFMAs of k-half 1
+    mask_tail_a(kt, 1);
+    mfma_half();
+    PZ_RAW_BARRIER();
+  }
+  if (wr == 0) PZ_RAW_BARRIER();
+
+  if (piece >= 0) {
+    f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)piece * (32 * NT2);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) W[(rb * 4 + cb) * NT2 + t] = acc[rb][cb];
+    return;
+  }
+  epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc, smem);
+}
+
 // Split tail, second pass: 16 blocks of 512 threads per leftover tile (one accumulator row-block rb and
 // one column half each, so the partial sums stream through many CUs); thread t sums the tail_s
 // partial accumulators it owned in gemm8p_kernel (fixed order) and applies the same epilogue.
@@ -1473,41 +1672,60 @@ __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
 // flight) and reduced through LDS.  W = 4/8/16 by K so every wave has >= 4
 // chunks of 32.  Operands k-contiguous (nn.Linear weight layout).
 // -------------------------------------------------------------------------
-template <int W>
+template <int W, int NC>
 __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
   constexpr int SK_WAVES = W;
   __shared__ f32x4 red[SK_WAVES][64];
+  __shared__ float redn[SK_WAVES][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const bool geglu = p.epi == PZ_EPI_GEGLU;
+  const bool nrm = p.nw != nullptr;
   const int64_t ncols = geglu ? p.geglu_I : p.N;
-  const int64_t n0 = (int64_t)blockIdx.x * 16;
+  // NC < 16 output columns per block (more blocks for narrow outputs): the 16 MFMA columns repeat
+  // the NC real ones (same addresses, no extra traffic) and only the first NC are stored
+  const int64_t n0 = (int64_t)blockIdx.x * NC;
   const int64_t z = blockIdx.y;
   const int64_t zo = z / p.batch_inner, zi = z % p.batch_inner;
   const bf16_t* A = p.A + zo * p.sAo + zi * p.sAi;
   const bf16_t* B = p.B + zo * p.sBo + zi * p.sBi;
   const int64_t m = lane & 15;
-  const int64_t nr = n0 + (lane & 15);
+  const int64_t nr = n0 + (lane & 15) % NC;
   const bool mok = m < p.M, nok = nr < ncols;
   const int64_t kchunks = p.K / 32;  // K % 32 == 0 required (host checked)
   f32x4 acc = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
+  float ss = 0.f;
   const bf16_t* Arow = A + m * p.lda + 8 * (lane >> 4);
   const bf16_t* Brow = B + nr * p.ldb + 8 * (lane >> 4);
   const bf16_t* Brow2 = B + (p.geglu_I + nr) * p.ldb + 8 * (lane >> 4);
+  const bf16_t* Wn = p.nw + 8 * (lane >> 4);
   const int64_t per = (kchunks + SK_WAVES - 1) / SK_WAVES;
   const int64_t kb = wave * per, ke = min(kchunks, kb + per);
   int64_t kc = kb;
   auto run = [&](auto U_) {
     constexpr int U = decltype(U_)::value;
     for (; kc + U <= ke; kc += U) {
-      bf16x8 a[U], b[U], b2[U];
+      bf16x8 a[U], b[U], b2[U], wv[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         a[u] = mok ? *reinterpret_cast<const bf16x8*>(Arow + (kc + u) * 32) : bf16x8{};
         b[u] = nok ? *reinterpret_cast<const bf16x8*>(Brow + (kc + u) * 32) : bf16x8{};
         if (geglu) b2[u] = nok ? *reinterpret_cast<const bf16x8*>(Brow2 + (kc + u) * 32) : bf16x8{};
+        if (nrm) wv[u] = *reinterpret_cast<const bf16x8*>(Wn + (kc + u) * 32);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        if (nrm) {  // sum of squares of the raw row; the product takes x * (1 + w), rsqrt applied after
+          const u32x4 xa = __builtin_bit_cast(u32x4, a[u]), xw = __builtin_bit_cast(u32x4, wv[u]);
+          u32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x0 = __uint_as_float(xa[e] << 16), x1 = __uint_as_float(xa[e] & 0xffff0000u);
+            const float w0 = __uint_as_float(xw[e] << 16), w1 = __uint_as_float(xw[e] & 0xffff0000u);
+            ss += x0 * x0 + x1 * x1;
+            o[e] = pack2bf(x0 * (1.f + w0), x1 * (1.f + w1));
+          }
+          a[u] = __builtin_bit_cast(bf16x8, o);
+        }
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u], a[u], acc, 0, 0, 0);
         if (geglu) acc2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[u], a[u], acc2, 0, 0, 0);
       }
@@ -1518,6 +1736,11 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
   run(std::integral_constant<int, 1>{});
   // D[n_local = 4*(lane>>4)+r][m = lane&15]
   red[wave][lane] = acc;
+  if (nrm) {
+    ss += __shfl_xor(ss, 16, 64);
+    ss += __shfl_xor(ss, 32, 64);
+    if (lane < 16) redn[wave][lane] = ss;
+  }
   __syncthreads();
   if (wave == 0) {
     for (int w = 1; w < SK_WAVES; ++w) acc += red[w][lane];
@@ -1532,16 +1755,21 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
   if (wave != 0) return;
   const int64_t mm = lane & 15;
   if (mm >= p.M) return;
+  float scale = p.alpha;
+  if (nrm) {
+    float t = 0.f;
+    for (int w = 0; w < SK_WAVES; ++w) t += redn[w][mm];
+    scale *= rsqrtf(t / (float)p.K + p.neps);
+  }
   const int64_t n = n0 + 4 * (lane >> 4);
   const int64_t cofs = zo * p.sCo + zi * p.sCi;
   const int64_t rofs = zo * p.sRo + zi * p.sRi;
-  float v[4];
   for (int r = 0; r < 4; ++r) {
     const int64_t nn = n + r;
-    if (nn >= ncols) continue;
-    float x = acc[r] * p.alpha;
+    if (4 * (lane >> 4) + r >= NC || nn >= ncols) continue;
+    float x = acc[r] * scale;
     if (geglu) {
-      const float g = x, u = acc2[r] * p.alpha;
+      const float g = x, u = acc2[r] * scale;
       if (p.aux) {
         p.aux[mm * p.ld_aux + nn] = f2bf(g);
         p.aux[mm * p.ld_aux + p.geglu_I + nn] = f2bf(u);
@@ -1555,7 +1783,6 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
       }
       if (p.resid) x += bf2f(p.resid[rofs + mm * p.ld_resid + nn]);
     }
-    v[r] = x;
     if (p.c_fp32) {
       float* Cp = reinterpret_cast<float*>(p.C) + cofs + mm * p.ldc + nn;
       *Cp = p.beta ? *Cp + x : x;
@@ -1564,7 +1791,6 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
       *Cp = f2bf(p.beta ? bf2f(*Cp) + x : x);
     }
   }
-  (void)v;
 }
 
 // -------------------------------------------------------------------------
@@ -1679,13 +1905,14 @@ static int launch256(const GemmP& p, int64_t batch, hipStream_t st) {
 }
 
 static bool use_8phase();
+static bool use_khalf(bool akc, bool bkc);
 
 namespace {
 enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
-  int wm, tag, skinny_w, splits;
+  int wm, tag, skinny_w, skinny_nc, splits;
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
 };
@@ -1743,7 +1970,16 @@ Plan make_plan(const pz_gemm_args* a) {
     const int64_t kch = a->K / 32;
     pl.kind = PATH_SKINNY;
     pl.skinny_w = kch >= 64 ? 16 : (kch >= 32 ? 8 : 4);
-    pl.tiles_n = (ncols + 15) / 16;
+    // PZ_SKINNY_MINNC=8|4: fewer columns per block for narrow outputs until the blocks cover the CUs
+    // (A/B runs; measured slower at B=1 -- 9.9 vs 8.8 us for the 1024-wide o/down projections -- so
+    // every block takes 16 columns by default)
+    const char* e = getenv("PZ_SKINNY_MINNC");
+    const int min_nc = e ? atoi(e) : 16;
+    pl.skinny_nc = 16;
+    while (pl.skinny_nc > 4 && pl.skinny_nc / 2 >= min_nc &&
+           a->batch * ((ncols + pl.skinny_nc - 1) / pl.skinny_nc) < device_cus())
+      pl.skinny_nc /= 2;
+    pl.tiles_n = (ncols + pl.skinny_nc - 1) / pl.skinny_nc;
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
@@ -1794,16 +2030,16 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   const Plan pl = make_plan(a);
   switch (pl.kind) {
     case PATH_SKINNY:
-      snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d>", pl.skinny_w);
+      snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
       break;
     case PATH_256:
       if (use_8phase() && pl.tail_s)
-        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s, %s>+gemm8p_tail_epilogue(tail %lld x %d)",
-                 bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0),
+        snprintf(buf, sizeof(buf), "%s<%s, %s, %s, %s>+gemm8p_tail_epilogue(tail %lld x %d)",
+                 use_khalf(pl.akc, pl.bkc) ? "gemm8k_kernel" : "gemm8p_kernel", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0),
                  (long long)(pl.tiles_m * pl.tiles_n - pl.dp_tiles), pl.tail_s);
       else if (use_8phase())
-        snprintf(buf, sizeof(buf), "gemm8p_kernel<%s, %s, %s, %s>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
-                 bstr(a->K % 64 != 0));
+        snprintf(buf, sizeof(buf), "%s<%s, %s, %s, %s>", use_khalf(pl.akc, pl.bkc) ? "gemm8k_kernel" : "gemm8p_kernel",
+                 bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0));
       else
         snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
                  BK256);
@@ -1819,11 +2055,18 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   return buf;
 }
 
-template <int W>
-static int launch_skinny(const GemmP& p, int64_t tiles_n, int64_t batch, hipStream_t st) {
-  hipLaunchKernelGGL(gemm_skinny_kernel<W>, dim3((unsigned)tiles_n, (unsigned)batch), dim3(W * 64), 0, st, p);
+template <int W, int NC>
+static int launch_skinny_nc(const GemmP& p, int64_t tiles_n, int64_t batch, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_skinny_kernel<W, NC>), dim3((unsigned)tiles_n, (unsigned)batch), dim3(W * 64), 0, st, p);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
+}
+
+template <int W>
+static int launch_skinny(const GemmP& p, int nc, int64_t tiles_n, int64_t batch, hipStream_t st) {
+  if (nc == 4) return launch_skinny_nc<W, 4>(p, tiles_n, batch, st);
+  if (nc == 8) return launch_skinny_nc<W, 8>(p, tiles_n, batch, st);
+  return launch_skinny_nc<W, 16>(p, tiles_n, batch, st);
 }
 
 template <bool AKC, bool BKC, int WM, int TAG>
@@ -1839,14 +2082,26 @@ static int launch_tile_any(GemmP& p, const Plan& pl, int64_t batch, hipStream_t 
   return PZ_OK;
 }
 
+// main loop of the 256-tile kernels: k-half segments (gemm8k_kernel) when an operand is k-strided,
+// quadrant segments (gemm8p_kernel) when both are k-contiguous -- there the k-half images' 64-B row
+// pieces cost more than the halved barrier count saves (measured on every Pi0 NT shape).
+// PZ_GEMM_MAIN=quad|khalf forces one (A/B runs; read per call).
+static bool use_khalf(bool akc, bool bkc) {
+  const char* e = getenv("PZ_GEMM_MAIN");
+  if (e && strcmp(e, "quad") == 0) return false;
+  if (e && strcmp(e, "khalf") == 0) return true;
+  return !(akc && bkc);
+}
+
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
-  auto kern = gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
-  static bool attr_set = false;
-  if (!attr_set) {
+  const bool kh = use_khalf(AKC, BKC);
+  auto kern = kh ? gemm8k_kernel<AKC, BKC, GEGLU, KTAIL> : gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
+  static bool attr_set[2] = {false, false};
+  if (!attr_set[kh]) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
+    attr_set[kh] = true;
   }
   const int T = p.tiles_m * p.tiles_n;
   const int units = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
@@ -1929,14 +2184,20 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.c_fp32 = a->c_fp32;
   p.beta = a->beta_accum;
   p.alpha = a->alpha;
+  p.nw = (const bf16_t*)a->norm_w;
+  p.neps = a->norm_eps;
   hipStream_t st = (hipStream_t)stream;
 
   const Plan pl = make_plan(a);
+  if (a->norm_w)
+    PZ_CHECK_ARG(pl.kind == PATH_SKINNY && PZ_ALIGNED(a->norm_w, 16),
+                 "pz_gemm: fused RMSNorm needs the few-row path (M <= 16, k-contiguous A/B, K %% 32 == 0) "
+                 "and a 16-byte aligned weight");
   if (pl.kind == PATH_SKINNY) {
     PZ_CHECK_ARG(a->batch < 65536, "pz_gemm: batch too large");
-    if (pl.skinny_w == 16) return launch_skinny<16>(p, pl.tiles_n, a->batch, st);
-    if (pl.skinny_w == 8) return launch_skinny<8>(p, pl.tiles_n, a->batch, st);
-    return launch_skinny<4>(p, pl.tiles_n, a->batch, st);
+    if (pl.skinny_w == 16) return launch_skinny<16>(p, pl.skinny_nc, pl.tiles_n, a->batch, st);
+    if (pl.skinny_w == 8) return launch_skinny<8>(p, pl.skinny_nc, pl.tiles_n, a->batch, st);
+    return launch_skinny<4>(p, pl.skinny_nc, pl.tiles_n, a->batch, st);
   }
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;

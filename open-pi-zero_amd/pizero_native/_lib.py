@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 5  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 6  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 
@@ -33,6 +33,7 @@ class GemmArgs(C.Structure):
         ("bias", vp), ("resid", vp), ("ld_resid", i64), ("aux", vp), ("ld_aux", i64),
         ("geglu_inter", i64),
         ("workspace", vp), ("ws_bytes", i64),
+        ("norm_w", vp), ("norm_eps", f32),
     ]
 
 

@@ -848,7 +848,8 @@ class Engine:
         return ops.flash_args(
             B, 1, Lq * nh, nk, hd, Q, (hd, Lq * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
             [((off - tok0) * nh, O, T * nh * hd, hd) for off, T, O in outs], 0, None, 1.0 / math.sqrt(hd), cap=50.0,
-            mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh, mask_row0=tok0 * nh)
+            mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh, mask_row0=tok0 * nh,
+            key_split=True)
 
     def _post_attn_O(self, g, p, x, O):
         """o_proj (+resid), post-attention RMSNorm, GeGLU MLP (+resid) of one mixture."""
@@ -857,10 +858,14 @@ class Engine:
         dev = x.device
         xm = torch.empty_like(x)
         ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
-        h2 = torch.empty_like(x)
-        ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)
         hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
-        ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
+        if M <= 16:  # few rows (denoise / proprio): RMSNorm fused into the gate|up GEMM
+            ops.linear(xm, self.gu_w(p), hm, epi=PZ_EPI_GEGLU,
+                       norm=(self.w(p + "post_attention_layernorm.weight"), d.rms_eps))
+        else:
+            h2 = torch.empty_like(x)
+            ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)
+            ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
         xn = torch.empty_like(x)
         ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
         return xn
@@ -902,10 +907,13 @@ class Engine:
             p = f"{g.prefix}{l}."
             Kj, Vj = kcache[l], vcache[l]
             M = x.shape[0]
-            h = torch.empty_like(x)
-            ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
             qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
-            ops.linear(h, self.qkv_w(p), qkv)
+            if M <= 16:  # RMSNorm fused into the q|k|v GEMM
+                ops.linear(x, self.qkv_w(p), qkv, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+            else:
+                h = torch.empty_like(x)
+                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
+                ops.linear(h, self.qkv_w(p), qkv)
             ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
             if self.infer_flash:  # fused attention of the action queries over every cached key
                 if O is None:

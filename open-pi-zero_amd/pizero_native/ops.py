@@ -53,18 +53,19 @@ def set_probe(pred):
 
 def gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, *, epi=PZ_EPI_NONE, alpha=1.0, beta=False,
          bias=None, resid=None, ld_resid=0, aux=None, ld_aux=0, geglu_inter=0, batch=1, batch_inner=1,
-         sA=(0, 0), sB=(0, 0), sC=(0, 0), sR=(0, 0)):
-    """Raw GEMM: see pz_gemm_args in include/pz_abi.h.  Element strides."""
+         sA=(0, 0), sB=(0, 0), sC=(0, 0), sR=(0, 0), norm=None):
+    """Raw GEMM: see pz_gemm_args in include/pz_abi.h.  Element strides.  norm = (w, eps): fused
+    Gemma RMSNorm of the A rows (few-row path only)."""
     if _PROBE is not None and _PROBE[0](M, N, K, epi, batch):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-              geglu_inter, batch, batch_inner, sA, sB, sC, sR)
+              geglu_inter, batch, batch_inner, sA, sB, sC, sR, norm)
         e1.record()
         _PROBE[1].append((e0, e1))
         return
     _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-          geglu_inter, batch, batch_inner, sA, sB, sC, sR)
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR, norm)
 
 
 _WS_BYTES = 64 << 20
@@ -83,7 +84,7 @@ def workspace(device=None):
 
 
 def _args(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-          geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws=None):
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws=None, norm=None):
     a = GemmArgs()
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.A, a.lda, a.a_kcontig = _p(A), int(lda), int(bool(a_kc))
@@ -99,14 +100,16 @@ def _args(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, 
     a.aux, a.ld_aux, a.geglu_inter = _p(aux), int(ld_aux), int(geglu_inter)
     if ws is not None:
         a.workspace, a.ws_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
+    if norm is not None:
+        a.norm_w, a.norm_eps = _p(norm[0]), float(norm[1])
     return a
 
 
 def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-          geglu_inter, batch, batch_inner, sA, sB, sC, sR):
+          geglu_inter, batch, batch_inner, sA, sB, sC, sR, norm=None):
     ws = workspace(Cm.device) if batch == 1 else None
     a = _args(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, resid, ld_resid, aux, ld_aux,
-              geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws)
+              geglu_inter, batch, batch_inner, sA, sB, sC, sR, ws, norm)
     call("pz_gemm", C.byref(a), _st())
 
 
@@ -121,18 +124,19 @@ def gemm_kernel_name(M, N, K, *, a_kc=True, b_kc=True, epi=PZ_EPI_NONE, geglu_in
     return lib().pz_gemm_kernel_name(C.byref(a)).decode()
 
 
-def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha=1.0, beta=False):
-    """out[M,N] = epi(x[M,K] @ W[N,K]^T): nn.Linear forward (x, out may be row-strided 2-D views)."""
+def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha=1.0, beta=False, norm=None):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T): nn.Linear forward (x, out may be row-strided 2-D views).
+    norm = (w, eps): x is first Gemma-RMS-normalised inside the GEMM (M <= 16 rows only)."""
     M, K = x.shape
     N = W.shape[0]
     if epi == PZ_EPI_GEGLU:
         I = N // 2
         gemm(M, N, K, x, x.stride(0), True, W, W.stride(0), True, out, out.stride(0), epi=epi,
-             aux=aux, ld_aux=0 if aux is None else aux.stride(0), geglu_inter=I, alpha=alpha)
+             aux=aux, ld_aux=0 if aux is None else aux.stride(0), geglu_inter=I, alpha=alpha, norm=norm)
         return out
     gemm(M, N, K, x, x.stride(0), True, W, W.stride(0), True, out, out.stride(0), epi=epi, alpha=alpha,
          beta=beta, bias=bias, resid=resid, ld_resid=0 if resid is None else resid.stride(0), aux=aux,
-         ld_aux=0 if aux is None else aux.stride(0))
+         ld_aux=0 if aux is None else aux.stride(0), norm=norm)
     return out
 
 
@@ -292,9 +296,10 @@ def attn_softmax_bwd(P, dP, lddp, tcap, dS, ldp, R, N, scale, cap):
 
 def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, groups, o_hstride, lse, scale,
                cap=0.0, mask_mode=0, cnt=None, prefix=0, cond=0, rows_per_token=1, dgroups=None, delta=None,
-               dq=None, dk=None, dv=None, mask_row0=0):
+               dq=None, dk=None, dv=None, mask_row0=0, key_split=False):
     """pz_flash_args (include/pz_abi.h).  *_strides = (ld, bstride, hstride) in elements; groups =
-    [(row0, O tensor, bstride, ld), ...] (dgroups: the dO tensors of the same groups)."""
+    [(row0, O tensor, bstride, ld), ...] (dgroups: the dO tensors of the same groups).  key_split:
+    hand the forward the workspace so launches with few query blocks split the keys."""
     a = FlashArgs()
     a.Z, a.H, a.nq, a.nk, a.head_dim = int(Z), int(H), int(nq), int(nk), int(hd)
     a.q, (a.ldq, a.q_bstride, a.q_hstride) = _p(q), tuple(int(x) for x in q_strides)
@@ -311,8 +316,8 @@ def flash_args(Z, H, nq, nk, hd, q, q_strides, k, k_strides, v, v_strides, group
     a.cnt, a.prefix, a.cond, a.rows_per_token = _p(cnt), int(prefix), int(cond), int(rows_per_token)
     a.mask_row0 = int(mask_row0)
     a.delta, a.dq, a.dk, a.dv = _p(delta), _p(dq), _p(dk), _p(dv)
-    if dq is not None:  # fp32 scratch for the query-split dK/dV partials
-        ws = flash_workspace(dq.device)
+    if dq is not None or key_split:  # fp32 scratch: dK/dV query-split / forward key-split partials
+        ws = flash_workspace(q.device)
         a.ws, a.ws_bytes = ws.data_ptr(), ws.numel() * ws.element_size()
     return a
 

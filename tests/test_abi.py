@@ -26,7 +26,7 @@ def test_library_exports_all_declared_symbols():
     for s in declared_symbols():
         assert hasattr(L, s), s
         assert s in SIGNATURES, f"{s} has no ctypes signature"
-    assert L.pz_abi_version() == 5
+    assert L.pz_abi_version() == 6
 
 
 def test_error_path_without_gpu():

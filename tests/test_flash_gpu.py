@@ -76,8 +76,9 @@ def test_flash_fwd_siglip():
     close(lse.view(B, nh, N), rlse, rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("key_split", [False, True])
 @pytest.mark.parametrize("cnt", [[276, 276, 276], [276, 250, 9]])
-def test_flash_fwd_joint_block_mask(cnt):
+def test_flash_fwd_joint_block_mask(cnt, key_split):
     from pizero_native import ops
 
     B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
@@ -94,7 +95,7 @@ def test_flash_fwd_joint_block_mask(cnt):
     cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
     a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
                        [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + Hc) * nh * hd, hd)], 0, lse, 1 / math.sqrt(hd),
-                       cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh)
+                       cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh, key_split=key_split)
     ops.flash_fwd(a)
     allowed, dead = joint_mask(cnt, P, C, L)
     q = Q.float().view(B, L, nh, hd).permute(0, 2, 1, 3)
@@ -105,6 +106,34 @@ def test_flash_fwd_joint_block_mask(cnt):
     close(Ov.view(B, P, nh, hd), ref[:, :P])
     close(Oe.view(B, C + Hc, nh, hd), ref[:, P:])
     close(lse.view(B, L, nh), rlse.permute(0, 2, 1), rtol=1e-3, atol=2e-3)
+
+
+@pytest.mark.parametrize("B,cnt", [(1, [276]), (2, [276, 100])])
+def test_flash_fwd_denoise_key_split(B, cnt):
+    """Inference denoise shape: only the action rows query (mask_row0 = first action row), keys =
+    the cached prefix + proprio + the chunk; the key-split forward (one workgroup per key block +
+    merge) against the fp32 reference."""
+    from pizero_native import ops
+
+    P, C, Hc, nh, hd = 276, 1, 4, 8, 256
+    L = P + C + Hc
+    Lp = (L + 7) // 8 * 8
+    Q = (torch.randn(B, Hc * nh, hd, device=dev) * 2).to(torch.bfloat16)
+    K = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    V = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    K[:, :L] = (torch.randn(B, L, hd, device=dev) * 2).to(torch.bfloat16)
+    V[:, :L] = torch.randn(B, L, hd, device=dev).to(torch.bfloat16)
+    O = torch.full((B * Hc, nh * hd), float("nan"), device=dev, dtype=torch.bfloat16)
+    cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
+    a = ops.flash_args(B, 1, Hc * nh, L, hd, Q, (hd, Hc * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                       [(0, O, Hc * nh * hd, hd)], 0, None, 1 / math.sqrt(hd), cap=50.0, mask_mode=1, cnt=cnt_t,
+                       prefix=P, cond=C, rows_per_token=nh, mask_row0=(P + C) * nh, key_split=True)
+    ops.flash_fwd(a)
+    allowed, dead = joint_mask(cnt, P, C, L)
+    q = Q.float().view(B, Hc, nh, hd).permute(0, 2, 1, 3)
+    ref, _ = ref_attention(q, K.float()[:, None, :L], V.float()[:, None, :L], 1 / math.sqrt(hd), 50.0,
+                           allowed[:, P + C:].to(dev), dead[:, P + C:].to(dev))
+    close(O.view(B, Hc, nh, hd), ref.permute(0, 2, 1, 3))
 
 
 def _grads(q, k, v, dO, scale, cap=0.0, allowed=None, dead=None):

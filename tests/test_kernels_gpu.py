@@ -91,7 +91,7 @@ def test_gemm256_layouts_with_tails(akc, bkc, K):
     from pizero_native import ops
 
     M, N = 2600, 4104
-    assert ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc).startswith("gemm8p_kernel")
+    assert ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc).startswith(("gemm8p_kernel", "gemm8k_kernel"))
     A = bf(M, K, scale=0.5)
     Bm = bf(N, K, scale=0.5)
     ref = A.float() @ Bm.float().t()
@@ -132,7 +132,7 @@ def test_gemm8p_split_tail(akc, bkc, M, N, K):
     from pizero_native import ops
 
     name = ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc)
-    assert name.startswith("gemm8p_kernel") and "tail" in name, name
+    assert name.startswith(("gemm8p_kernel", "gemm8k_kernel")) and "tail" in name, name
     A = bf(M, K, scale=0.5)
     Bm = bf(N, K, scale=0.5)
     ref = A.float() @ Bm.float().t()
@@ -266,6 +266,55 @@ def test_skinny_widths(K):
         assert "skinny" in ops.gemm_kernel_name(M, 1040, K)
         ops.linear(x, W, out, bias=b)
         close(out, x.float() @ W.float().t() + b.float())
+
+
+@pytest.mark.parametrize("min_nc", ["16", "4"])
+@pytest.mark.parametrize("N", [1024, 1040, 2560, 4100])
+def test_skinny_column_blocks(N, min_nc, monkeypatch):
+    """PZ_SKINNY_MINNC=4: narrow outputs take 8 or 4 columns per block; ragged last block."""
+    from pizero_native import ops
+
+    monkeypatch.setenv("PZ_SKINNY_MINNC", min_nc)
+    K = 2048
+    for M in (1, 4, 16):
+        x, W, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(M, N)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        name = ops.gemm_kernel_name(M, N, K)
+        assert name.startswith("gemm_skinny_kernel<16, "), name
+        ops.linear(x, W, out, resid=r)
+        close(out, x.float() @ W.float().t() + r.float())
+
+
+def _rms_ref(x, w, eps):
+    """paligemma/modules.py:7-21 in fp32, rounded to bf16 like the unfused path"""
+    xf = x.float()
+    return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * (1 + w.float())).to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("K,N", [(1024, 2560), (2048, 1024)])
+def test_skinny_fused_rmsnorm(K, N):
+    """Gemma RMSNorm fused into the few-row GEMM (inference denoise q|k|v and gate|up) vs
+    rmsnorm -> GEMM in fp32; also the GeGLU epilogue."""
+    from pizero_native import ops
+
+    eps = 1e-6
+    for M in (1, 4, 16):
+        x = bf(M, K, scale=3.0)
+        w = bf(K, scale=0.5)
+        W = bf(N, K, scale=K ** -0.5)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, out, norm=(w, eps))
+        # the fused path rounds x * (1 + w) to bf16 (rsqrt applied to the fp32 sums) where the unfused
+        # one rounds the normalised row: ~1 bf16 ulp of the output apart
+        close(out, _rms_ref(x, w, eps).float() @ W.float().t(), rtol=2e-2, atol=4e-2)
+        I = N // 2
+        h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, norm=(w, eps))
+        raw = _rms_ref(x, w, eps).float() @ W.float().t()
+        close(h, torch.nn.functional.gelu(raw[:, :I], approximate="tanh") * raw[:, I:], rtol=3e-2, atol=6e-2)
+    with pytest.raises(RuntimeError):  # many rows: not the few-row path
+        x = bf(64, K)
+        ops.linear(x, W, torch.empty(64, N, device=dev, dtype=torch.bfloat16), norm=(w, eps))
 
 
 def test_small_gemm():

@@ -656,14 +656,10 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
     zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
     zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
   }
-  // key split (gridDim.z > 1, few query blocks: inference): key blocks [kb_begin, kb_end) only,
-  // unnormalised O + (m, l) partials to the workspace, merged by flash_fwd_combine_kernel
   const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
-  const int per = (nkb + (int)gridDim.z - 1) / (int)gridDim.z;
-  const int kb_begin = (int)blockIdx.z * per, kb_end = min(nkb, kb_begin + per);
   TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
-  stk.load(K, a.ldk, (int64_t)kb_begin * FA_KB, a.nk);
-  stv.load(V, a.ldv, (int64_t)kb_begin * FA_KB, a.nk);
+  stk.load(K, a.ldk, 0, a.nk);
+  stv.load(V, a.ldv, 0, a.nk);
   bf16x8 qf[D::NKS], df[D::NKS];
   const bool live = r < a.nq;
   const bf16_t* dOr = nullptr;
@@ -699,10 +695,10 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
   stk.store(Ks2[0]);
   stv.store(Vs2[0]);
   __syncthreads();
-  for (int kb = kb_begin; kb < kb_end; ++kb) {
-    const bf16_t* Ks = Ks2[(kb - kb_begin) & 1];
-    const bf16_t* Vs = Vs2[(kb - kb_begin) & 1];
-    const bool more = kb + 1 < kb_end;
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Ks2[kb & 1];
+    const bf16_t* Vs = Vs2[kb & 1];
+    const bool more = kb + 1 < nkb;
     if (more) {
       stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
       stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
@@ -759,6 +755,370 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
   }
 }
 
+// ---- resident variants (SigLIP: nq, nk <= 256) ---------------------------------
+// The whole key side (forward, dQ) or query side (dK/dV) of a unit is staged in LDS once, by
+// loads all in flight together: one global-latency round per workgroup instead of one per
+// 64-key / 32-query step, which the step-staged kernels above expose at SigLIP's small per-step
+// work (16 heads x 72).  8 waves per workgroup (two per SIMD), dynamic LDS up to 142 KiB.
+constexpr int FR_MAX = 256, FR_NW = 8;
+
+// 1-D grid of nblk workgroups per unit: the nblk workgroups of one unit get ids of one residue mod 8,
+// i.e. land on one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2 for the
+// unit's resident operand, which every one of them stages
+__device__ __forceinline__ void fa_unit_block(int nblk, int units, int64_t& zh, int& blk) {
+  const int id = blockIdx.x;
+  if (units % 8 == 0) {
+    const int xcd = id & 7, local = id >> 3;
+    zh = (int64_t)(local / nblk) * 8 + xcd;
+    blk = local % nblk;
+  } else {
+    zh = id / nblk;
+    blk = id % nblk;
+  }
+}
+
+template <int HD>
+__global__ void __launch_bounds__(FR_NW * 64) flash_fwd_res_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FR_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Vall = Kall + FR_MAX * D::ROW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + FR_NW * 16 - 1) / (FR_NW * 16)), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t q0 = (int64_t)qblk * (FR_NW * 16) + wave * 16;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stk, stv;
+    stk.load(K, a.ldk, 0, a.nk);
+    stv.load(V, a.ldv, 0, a.nk);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Kall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Vall);
+    stk.store(Kall);
+    stv.store(Vall);
+  }
+  bf16x8 qf[D::NKS];
+  const int64_t rq = q0 + (lane & 15);
+#pragma unroll
+  for (int ks = 0; ks < D::NKS; ++ks) {
+    const int c = ks * 32 + 8 * g;
+    qf[ks] = (rq < a.nq && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + rq * a.ldq + c) : bf16x8{};
+  }
+  f32x4 o[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const int t = mk.token((int)rq);
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Kall + kb * FA_KB * D::ROW;
+    const bf16_t* Vs = Vall + kb * FA_KB * D::ROW;
+    f32x4 sc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[i] = mfma(frag_row<D::ROW>(Ks, i * 16, ks * 32, lane), qf[ks], sc[i]);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = fa_logit(mk, sc[i][e], t, kb * FA_KB + i * 16 + 4 * g + e);
+        sc[i][e] = x;
+        mx = fmaxf(mx, x);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = mn == -INFINITY ? 0.f : __expf(sc[i][e] - mn);
+        sc[i][e] = pv;
+        sum += pv;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l = l * alpha + sum;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) o[db] *= alpha;
+    const bf16x8 pf0 = pack8(sc[0], sc[1]), pf1 = pack8(sc[2], sc[3]);
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      o[db] = mfma(frag_tr<D::ROW>(Vs, 0, db * 16, lane), pf0, o[db]);
+      o[db] = mfma(frag_tr<D::ROW>(Vs, 32, db * 16, lane), pf1, o[db]);
+    }
+  }
+  if (rq >= a.nq) return;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  const FaRow fr{&a};
+  const int gi = fr.grp(rq);
+  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, rq, gi);
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD)
+      *reinterpret_cast<u32x2*>(O + d) =
+          u32x2{pack2bf(o[db][0] * inv, o[db][1] * inv), pack2bf(o[db][2] * inv, o[db][3] * inv)};
+  }
+  if (g == 0 && a.lse) a.lse[zh * a.nq + rq] = m + __logf(l);
+}
+
+// dQ (+ delta) with every key / value of the unit resident: grid (ceil(nq / 128), Z * H)
+template <int HD>
+__global__ void __launch_bounds__(FR_NW * 64) flash_bwd_q_res_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FR_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Vall = Kall + FR_MAX * D::ROW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + FR_NW * 16 - 1) / (FR_NW * 16)), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)qblk * (FR_NW * 16) + wave * 16 + (lane & 15);
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaRow fr{&a};
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stk, stv;
+    stk.load(K, a.ldk, 0, a.nk);
+    stv.load(V, a.ldv, 0, a.nk);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Kall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Vall);
+    stk.store(Kall);
+    stv.store(Vall);
+  }
+  bf16x8 qf[D::NKS], df[D::NKS];
+  const bool live = r < a.nq;
+  const bf16_t* dOr = nullptr;
+  const bf16_t* Or = nullptr;
+  if (live) {
+    const int gi = fr.grp(r);
+    dOr = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
+    Or = (const bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+  }
+  float del = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < D::NKS; ++ks) {
+    const int c = ks * 32 + 8 * g;
+    const bool ok = live && c < HD;
+    qf[ks] = ok ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+    df[ks] = ok ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
+    if (ok) {
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) del += (float)df[ks][e] * (float)ov[e];
+    }
+  }
+  del += __shfl_xor(del, 16, 64);
+  del += __shfl_xor(del, 32, 64);
+  if (live && g == 0) a.delta[zh * a.nq + r] = del;
+  const float lse = live ? a.lse[zh * a.nq + r] : 0.f;
+  const int tq = mk.token((int)r);
+  f32x4 dq[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Kall + kb * FA_KB * D::ROW;
+    const bf16_t* Vs = Vall + kb * FA_KB * D::ROW;
+    f32x4 ds[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 kfr[D::NKS], vfr[D::NKS];
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        kfr[ks] = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+        vfr[ks] = frag_row<D::ROW>(Vs, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        sv = mfma(kfr[ks], qf[ks], sv);
+        dp = mfma(vfr[ks], df[ks], dp);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = kb * FA_KB + i * 16 + 4 * g + e;
+        float dse = 0.f;
+        if (live) {
+          const FaLogit lg = fa_logit_d(mk, sv[e], tq, j);
+          const float pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse);
+          dse = pe * (dp[e] - del) * lg.dxds;
+        }
+        ds[i][e] = dse;
+      }
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const bf16x8 sb = pack8(ds[2 * k2], ds[2 * k2 + 1]);
+      bf16x8 kt[D::NDB];
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) kt[db] = frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane);
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) dq[db] = mfma(kt[db], sb, dq[db]);
+    }
+  }
+  if (!live) return;
+  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
+  }
+}
+
+// dK, dV with every query row (Q, dO, lse, delta) of the unit resident: grid (ceil(nk / 64), Z * H);
+// wave w owns keys 16 (w & 3).. of the block and sweeps query half (w >> 2); halves summed in LDS
+template <int HD>
+__global__ void __launch_bounds__(FR_NW * 64) flash_bwd_kv_res_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FR_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Qall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Dall = Qall + FR_MAX * D::ROW;
+  bf16_t* Kk = Dall + FR_MAX * D::ROW;
+  bf16_t* Vk = Kk + FA_KB * D::ROW;
+  float* lse_all = reinterpret_cast<float*>(Vk + FA_KB * D::ROW);
+  float* del_all = lse_all + FR_MAX;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int kw = wave & 3, qh = wave >> 2;
+  int64_t zh;
+  int kblk;
+  fa_unit_block((int)((a.nk + FA_KB - 1) / FA_KB), (int)(a.Z * a.H), zh, kblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int k0 = kblk * FA_KB;
+  const int key = k0 + kw * 16 + (lane & 15);
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stq, std_;
+    TileStager<HD, D::ROW, FA_KB, NT> sk, sv;
+    stq.load_q(a, Q, b, h, 0, false);
+    std_.load_q(a, Q, b, h, 0, true);
+    sk.load(K, a.ldk, k0, a.nk);
+    sv.load(V, a.ldv, k0, a.nk);
+    const int tr = threadIdx.x;
+    const float lv = tr < FR_MAX && tr < a.nq ? a.lse[zh * a.nq + tr] : 0.f;
+    const float dv_ = tr < FR_MAX && tr < a.nq ? a.delta[zh * a.nq + tr] : 0.f;
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Qall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Dall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Kk);
+    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vk);
+    stq.store(Qall);
+    std_.store(Dall);
+    sk.store(Kk);
+    sv.store(Vk);
+    if (tr < FR_MAX) {
+      lse_all[tr] = lv;
+      del_all[tr] = dv_;
+    }
+  }
+  f32x4 dk[D::NDB], dv[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dk[db] = dv[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  bf16x8 kfr[D::NKS], vfr[D::NKS];
+#pragma unroll
+  for (int ks = 0; ks < D::NKS; ++ks) {
+    kfr[ks] = frag_row<D::ROW>(Kk, kw * 16, ks * 32, lane);
+    vfr[ks] = frag_row<D::ROW>(Vk, kw * 16, ks * 32, lane);
+  }
+  const int nqs = (int)((a.nq + FA_QS - 1) / FA_QS);
+  const int half = (nqs + 1) / 2;
+  const int qs0 = qh * half, qs1 = min(nqs, qs0 + half);
+  for (int qs = qs0; qs < qs1; ++qs) {
+    const int r0 = qs * FA_QS;
+    const bf16_t* Qs = Qall + r0 * D::ROW;
+    const bf16_t* Ds = Dall + r0 * D::ROW;
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      bf16x8 qa[D::NKS], da[D::NKS];
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        qa[ks] = frag_row<D::ROW>(Qs, i * 16, ks * 32, lane);
+        da[ks] = frag_row<D::ROW>(Ds, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        sv = mfma(qa[ks], kfr[ks], sv);
+        dp = mfma(da[ks], vfr[ks], dp);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rr = r0 + i * 16 + 4 * g + e;
+        float pe = 0.f, dse = 0.f;
+        if (rr < a.nq) {
+          const FaLogit lg = fa_logit_d(mk, sv[e], mk.token(rr), key);
+          pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse_all[rr]);
+          dse = pe * (dp[e] - del_all[rr]) * lg.dxds;
+        }
+        p[i][e] = pe;
+        ds[i][e] = dse;
+      }
+    }
+    const bf16x8 pb = pack8(p[0], p[1]);
+    const bf16x8 sb = pack8(ds[0], ds[1]);
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      dv[db] = mfma(frag_tr<D::ROW>(Ds, 0, db * 16, lane), pb, dv[db]);
+      dk[db] = mfma(frag_tr<D::ROW>(Qs, 0, db * 16, lane), sb, dk[db]);
+    }
+  }
+  // query halves: waves 4..7 hand their partial sums to waves 0..3 through LDS (Q image reused)
+  __syncthreads();
+  f32x4* red = reinterpret_cast<f32x4*>(fa_smem);
+  if (qh == 1) {
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      red[((kw * D::NDB + db) * 2 + 0) * 64 + lane] = dk[db];
+      red[((kw * D::NDB + db) * 2 + 1) * 64 + lane] = dv[db];
+    }
+  }
+  __syncthreads();
+  if (qh == 1 || key >= a.nk) return;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    dk[db] += red[((kw * D::NDB + db) * 2 + 0) * 64 + lane];
+    dv[db] += red[((kw * D::NDB + db) * 2 + 1) * 64 + lane];
+  }
+  bf16_t* dK = (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + (int64_t)key * a.ldk;
+  bf16_t* dV = (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + (int64_t)key * a.ldv;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) {
+      *reinterpret_cast<u32x2*>(dK + d) = u32x2{pack2bf(dk[db][0], dk[db][1]), pack2bf(dk[db][2], dk[db][3])};
+      *reinterpret_cast<u32x2*>(dV + d) = u32x2{pack2bf(dv[db][0], dv[db][1]), pack2bf(dv[db][2], dv[db][3])};
+    }
+  }
+}
+
+constexpr int FR_SMEM_KQ = 2 * FR_MAX * FaDims<72>::ROW * 2;  // forward / dQ: K + V images
+constexpr int FR_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FA_KB * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
+
 }  // namespace
 
 // head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
@@ -770,6 +1130,21 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
     default: hipLaunchKernelGGL(KERNEL<16>, GRID, __VA_ARGS__); break;                              \
   }
 static bool fa_hd_ok(int64_t hd) { return hd == 256 || hd == 72 || hd == 32 || hd == 16; }
+
+// SigLIP shape: the whole key / query side of a unit fits the resident kernels' LDS images
+static bool fa_resident(const pz_flash_args* a) {
+  const char* e = getenv("PZ_FLASH_RESIDENT");  // "0": step-staged kernels (A/B runs; read per call)
+  if (e && e[0] == '0') return false;
+  return a->head_dim == 72 && a->nq <= FR_MAX && a->nk <= FR_MAX;
+}
+
+template <class Kern>
+static void fa_smem_attr(Kern k, int bytes, bool& done) {
+  if (!done) {
+    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    done = true;
+  }
+}
 
 extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->q && a->k && a->v && a->Z > 0 && a->H > 0 && a->nq > 0 && a->nk > 0,
@@ -801,6 +1176,14 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   }
   dim3 grid((unsigned)qblk, (unsigned)(a->Z * a->H), (unsigned)sp);
   hipStream_t st = (hipStream_t)stream;
+  if (sp == 1 && fa_resident(a)) {
+    static bool attr = false;
+    fa_smem_attr(flash_fwd_res_kernel<72>, FR_SMEM_KQ, attr);
+    hipLaunchKernelGGL(flash_fwd_res_kernel<72>, dim3((unsigned)((a->nq + FR_NW * 16 - 1) / (FR_NW * 16) * a->Z * a->H)),
+                       dim3(FR_NW * 64), FR_SMEM_KQ, st, *a);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   FA_DISPATCH(a->head_dim, flash_fwd_kernel, grid, dim3((a->head_dim == 256 ? 8 : 4) * 64), 0, st, *a);
   PZ_CHECK_LAUNCH();
   if (sp > 1) {
@@ -842,6 +1225,18 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
   dim3 gkv((unsigned)nkb, (unsigned)(a->Z * a->H), (unsigned)splits);
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
+  if (fa_resident(a)) {
+    static bool aq = false, akv = false;
+    fa_smem_attr(flash_bwd_q_res_kernel<72>, FR_SMEM_KQ, aq);
+    fa_smem_attr(flash_bwd_kv_res_kernel<72>, FR_SMEM_KV, akv);
+    hipLaunchKernelGGL(flash_bwd_q_res_kernel<72>, dim3((unsigned)((a->nq + FR_NW * 16 - 1) / (FR_NW * 16) * a->Z * a->H)),
+                       dim3(FR_NW * 64), FR_SMEM_KQ, st, *a);
+    PZ_CHECK_LAUNCH();
+    hipLaunchKernelGGL(flash_bwd_kv_res_kernel<72>, dim3((unsigned)(nkb * a->Z * a->H)), dim3(FR_NW * 64),
+                       FR_SMEM_KV, st, *a);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
   PZ_CHECK_LAUNCH();
   FA_DISPATCH(a->head_dim, flash_bwd_kv_kernel, gkv, dim3(FA_NW * 64), 0, st, *a);

@@ -1138,10 +1138,13 @@ static bool fa_resident(const pz_flash_args* a) {
   return a->head_dim == 72 && a->nq <= FR_MAX && a->nk <= FR_MAX;
 }
 
+// Raise the kernel's dynamic-LDS limit once; a refusal is cleared here (the launch is checked on
+// its own) so it cannot surface as a later launch's error
 template <class Kern>
 static void fa_smem_attr(Kern k, int bytes, bool& done) {
   if (!done) {
-    hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) != hipSuccess)
+      (void)hipGetLastError();
     done = true;
   }
 }

@@ -27,6 +27,8 @@ for s in $STEPS; do
       timeout -k 10 400 python -u tools/gemm_bench.py --iters 10 > "$OUT/gemm_bench.log" 2>&1 ;;
     pmc)
       bash tools/pmc_dominant.sh "$OUT/pmc" ;;
+    census)
+      timeout -k 10 300 python -u tools/gemm_census.py > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "step $s ok"

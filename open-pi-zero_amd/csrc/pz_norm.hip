@@ -7,7 +7,7 @@
 
 namespace {
 
-constexpr int ROWS_PER_PART = 64;  // rows folded into one fp32 partial row of dw/db
+constexpr int ROWS_PER_PART = 16;  // rows folded into one fp32 partial row of dw/db (4 per wave: enough workgroups to hide latency)
 
 __device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
   u32x4 r = *reinterpret_cast<const u32x4*>(p);
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const bf16_t* __restri
   }
 }
 
-// one block = ROWS_PER_PART rows (4 waves x 16 rows); dw partial per block
+// one block = ROWS_PER_PART rows (4 waves x 4 rows); dw partial per block
 template <int MAXC>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,

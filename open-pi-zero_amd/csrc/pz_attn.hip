@@ -171,6 +171,136 @@ __global__ void __launch_bounds__(256) softmax_kernel(pz_softmax_args a) {
   }
 }
 
+// Vectorised variants (rows 16-B aligned, ld % 4 == 0): one wave per row, each lane owns groups of 4
+// consecutive columns (float4 logits, 8-B bf16 stores), 32-bit index math, fast tanh for the cap.
+__device__ __forceinline__ u32x2 pack4bf(const float (&v)[4]) { return u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])}; }
+
+template <int MAXV>
+__global__ void __launch_bounds__(256) softmax4_kernel(pz_softmax_args a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.R) return;
+  const float* s = a.S + row * a.lds;
+  int b = 0, qi = 0;
+  if (a.mask_mode != 0) {
+    const int rr = (int)row, rpb = (int)a.rows_per_batch;
+    b = rr / rpb;
+    qi = (int)a.qoff + (rr - b * rpb) / (int)a.heads;
+  }
+  const int cnt = a.mask_mode == 1 ? a.cnt[b] : 0;
+  const int P = (int)a.prefix, Cc = (int)a.cond, N = (int)a.N;
+  const float* mrow = a.mask_mode == 2 ? a.mask + b * a.mask_bstride + (qi - a.qoff) * a.ldm : nullptr;
+  const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
+  float x[MAXV][4], th[MAXV][4];
+  bool ok[MAXV][4];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < MAXV; ++e) {
+    const int j0 = 4 * (lane + 64 * e);
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f};
+    if (j0 < N) sv = *reinterpret_cast<const f32x4*>(s + j0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = j0 + i;
+      float v = j < N ? sv[i] * a.scale : 0.f;  // padded columns may hold anything
+      th[e][i] = 0.f;
+      if (a.cap > 0.f && j < N) {
+        th[e][i] = tanh_fast(v * inv_cap);
+        v = a.cap * th[e][i];
+      }
+      x[e][i] = v;
+      bool al = j < N;
+      if (al && a.mask_mode == 1) al = block_allowed(qi, j, cnt, P, Cc);
+      else if (al && a.mask_mode == 2) al = mrow[j] > -1e30f;
+      ok[e][i] = al;
+      if (al) mx = fmaxf(mx, v);
+    }
+  }
+  mx = warp_max(mx);
+  bf16_t* prow = (bf16_t*)a.P + row * a.ldp;
+  bf16_t* trow = a.tcap ? (bf16_t*)a.tcap + row * a.ldp : nullptr;
+  const int ldp = (int)a.ldp;
+  if (mx == -INFINITY) {  // fully masked row: finfo.min + s absorbs s -> uniform (pizero.py:291)
+    const float u = 1.f / (float)N;
+    for (int j0 = 4 * lane; j0 < ldp; j0 += 256) {
+      float v[4] = {j0 < N ? u : 0.f, j0 + 1 < N ? u : 0.f, j0 + 2 < N ? u : 0.f, j0 + 3 < N ? u : 0.f};
+      *reinterpret_cast<u32x2*>(prow + j0) = pack4bf(v);
+      if (trow) *reinterpret_cast<u32x2*>(trow + j0) = u32x2{0u, 0u};
+    }
+    return;
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < MAXV; ++e)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pv = ok[e][i] ? __expf(x[e][i] - mx) : 0.f;
+      x[e][i] = pv;
+      sum += pv;
+    }
+  const float inv = 1.f / warp_sum(sum);
+#pragma unroll
+  for (int e = 0; e < MAXV; ++e) {
+    const int j0 = 4 * (lane + 64 * e);
+    if (j0 < ldp) {  // columns N..ldp-1 come out 0 (x = 0, th = 0 there)
+      float v[4] = {x[e][0] * inv, x[e][1] * inv, x[e][2] * inv, x[e][3] * inv};
+      *reinterpret_cast<u32x2*>(prow + j0) = pack4bf(v);
+      if (trow) *reinterpret_cast<u32x2*>(trow + j0) = pack4bf(th[e]);
+    }
+  }
+}
+
+template <int MAXV>
+__global__ void __launch_bounds__(256) softmax_bwd4_kernel(const bf16_t* __restrict__ Pm, const float* __restrict__ dP,
+                                                           int64_t lddp, const bf16_t* __restrict__ tcap, bf16_t* dS,
+                                                           int64_t ldp, int64_t R, int N, float scale, float cap) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const bf16_t* prow = Pm + row * ldp;
+  const float* drow = dP + row * lddp;
+  float p[MAXV][4], d[MAXV][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int e = 0; e < MAXV; ++e) {
+    const int j0 = 4 * (lane + 64 * e);
+    u32x2 pw = {0u, 0u};
+    f32x4 dv = {0.f, 0.f, 0.f, 0.f};
+    if (j0 < N) {
+      pw = *reinterpret_cast<const u32x2*>(prow + j0);
+      dv = *reinterpret_cast<const f32x4*>(drow + j0);
+    }
+    p[e][0] = __uint_as_float(pw[0] << 16);
+    p[e][1] = __uint_as_float(pw[0] & 0xffff0000u);
+    p[e][2] = __uint_as_float(pw[1] << 16);
+    p[e][3] = __uint_as_float(pw[1] & 0xffff0000u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      d[e][i] = j0 + i < N ? dv[i] : 0.f;
+      dot += p[e][i] * d[e][i];
+    }
+  }
+  dot = warp_sum(dot);
+  bf16_t* orow = dS + row * ldp;
+#pragma unroll
+  for (int e = 0; e < MAXV; ++e) {
+    const int j0 = 4 * (lane + 64 * e);
+    if (j0 < (int)ldp) {
+      float g[4];
+      u32x2 tw = {0u, 0u};
+      if (cap > 0.f && j0 < N) tw = *reinterpret_cast<const u32x2*>(tcap + row * ldp + j0);
+      const float t[4] = {__uint_as_float(tw[0] << 16), __uint_as_float(tw[0] & 0xffff0000u),
+                          __uint_as_float(tw[1] << 16), __uint_as_float(tw[1] & 0xffff0000u)};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        g[i] = j0 + i < N ? p[e][i] * (d[e][i] - dot) * scale : 0.f;
+        if (cap > 0.f) g[i] *= (1.f - t[i] * t[i]);
+      }
+      *reinterpret_cast<u32x2*>(orow + j0) = pack4bf(g);
+    }
+  }
+}
+
 template <int MAXE>
 __global__ void __launch_bounds__(256) softmax_bwd_kernel(const bf16_t* __restrict__ P,
                                                           const float* __restrict__ dP, int64_t lddp,
@@ -254,6 +384,14 @@ extern "C" int pz_attn_softmax(const pz_softmax_args* a, void* stream) {
   if (a->mask_mode == 2) PZ_CHECK_ARG(a->mask && a->rows_per_batch > 0 && a->heads > 0, "attn_softmax: mask");
   dim3 grid((unsigned)((a->R + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
+  const bool vec = a->lds % 4 == 0 && a->ldp % 4 == 0 && PZ_ALIGNED(a->S, 16) && PZ_ALIGNED(a->P, 8) &&
+                   (!a->tcap || PZ_ALIGNED(a->tcap, 8)) && a->R < (1LL << 31) && a->ldp <= 1024;
+  if (vec) {
+    if (a->ldp <= 512) hipLaunchKernelGGL(softmax4_kernel<2>, grid, dim3(256), 0, st, *a);
+    else hipLaunchKernelGGL(softmax4_kernel<4>, grid, dim3(256), 0, st, *a);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   if (a->N <= 256) hipLaunchKernelGGL(softmax_kernel<4>, grid, dim3(256), 0, st, *a);
   else if (a->N <= 512) hipLaunchKernelGGL(softmax_kernel<8>, grid, dim3(256), 0, st, *a);
   else hipLaunchKernelGGL(softmax_kernel<16>, grid, dim3(256), 0, st, *a);
@@ -266,6 +404,17 @@ extern "C" int pz_attn_softmax_bwd(const void* P, const float* dP, int64_t lddp,
   PZ_CHECK_ARG(P && dP && dS && R > 0 && N > 0 && N <= 1024 && (cap <= 0.f || tcap), "attn_softmax_bwd: bad args");
   dim3 grid((unsigned)((R + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
+  if (lddp % 4 == 0 && ldp % 4 == 0 && ldp <= 1024 && PZ_ALIGNED(dP, 16) && PZ_ALIGNED(P, 8) && PZ_ALIGNED(dS, 8) &&
+      (cap <= 0.f || PZ_ALIGNED(tcap, 8))) {
+    if (ldp <= 512)
+      hipLaunchKernelGGL(softmax_bwd4_kernel<2>, grid, dim3(256), 0, st, (const bf16_t*)P, dP, lddp,
+                         (const bf16_t*)tcap, (bf16_t*)dS, ldp, R, (int)N, scale, cap);
+    else
+      hipLaunchKernelGGL(softmax_bwd4_kernel<4>, grid, dim3(256), 0, st, (const bf16_t*)P, dP, lddp,
+                         (const bf16_t*)tcap, (bf16_t*)dS, ldp, R, (int)N, scale, cap);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   if (N <= 256)
     hipLaunchKernelGGL(softmax_bwd_kernel<4>, grid, dim3(256), 0, st, (const bf16_t*)P, dP, lddp,
                        (const bf16_t*)tcap, (bf16_t*)dS, ldp, R, N, scale, cap);

@@ -444,6 +444,7 @@ def test_softmax_block_mask_softcap_fwd_bwd():
     cnt = torch.tensor([10, 7], dtype=torch.int32, device=dev)
     R = B * L * nh
     S = torch.randn(R, Lp, device=dev) * 40
+    S[:, L:] = float("nan")  # padded logit columns are never written by the S GEMM
     Pm = torch.empty(R, Lp, device=dev, dtype=torch.bfloat16)
     tc = torch.empty(R, Lp, device=dev, dtype=torch.bfloat16)
     ops.attn_softmax(S, Lp, Pm, Lp, R, L, 1 / 16, cap=50.0, tcap=tc, mask_mode=1, rows_per_batch=L * nh, heads=nh,
@@ -462,6 +463,7 @@ def test_softmax_block_mask_softcap_fwd_bwd():
     ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, R, L, 1 / 16, 50.0)
     valid = allowed.any(-1)  # fully-masked rows: gradient unused downstream
     close(dS[valid, :L], s.grad[valid] / 16, atol=3e-3)
+    assert (dS[:, L:] == 0).all() and not tc.isnan().any()
 
 
 def test_qkv_rope_split_roundtrip():

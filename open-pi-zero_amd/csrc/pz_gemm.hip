@@ -1983,7 +1983,12 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
-  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= 512 && ncols >= (pl.geglu ? 256 : 512)) {
+  // rows from which the 256-tile kernels are tried: 256 for the GeGLU GEMM and long-K GEMMs (prefill
+  // at B=1, 276 rows: 64 vs 78 us and 51 vs 56 us measured), 512 otherwise (narrow prefill GEMMs
+  // are faster on 128-row tiles); PZ_GEMM_256_MINM overrides (A/B runs)
+  const char* mm = getenv("PZ_GEMM_256_MINM");
+  const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192) ? 256 : 512);
+  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= (pl.geglu ? 256 : 512)) {
     const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;
     Plan cand = pl;
     cand.kind = PATH_256;

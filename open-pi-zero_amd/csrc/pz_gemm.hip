@@ -539,11 +539,22 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmP p, int S) {
   const int64_t m = idx / groups, n = (idx - m * groups) * 4;
   const float* W = p.ws + m * p.ldw + n;
   const int64_t slab = p.M * p.ldw;
-  f32x4 s = *reinterpret_cast<const f32x4*>(W);
-  for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(W + z * slab);
+  // slabs loaded 4 at a time (all in flight together), summed in slab order (deterministic)
+  auto sum_slabs = [&](const float* src) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < S; z += 4) {
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = z + u < S ? *reinterpret_cast<const f32x4*>(src + (z + u) * slab) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += v[u];
+    }
+    return acc;
+  };
+  const f32x4 s = sum_slabs(W);
   if (geglu) {
-    f32x4 u = *reinterpret_cast<const f32x4*>(W + p.geglu_I);
-    for (int z = 1; z < S; ++z) u += *reinterpret_cast<const f32x4*>(W + z * slab + p.geglu_I);
+    const f32x4 u = sum_slabs(W + p.geglu_I);
     store_geglu4(p, 0, m, n, s, u);
   } else {
     store_out4(p, 0, 0, m, n, s);
@@ -1649,10 +1660,23 @@ __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
   const f32x4* W = reinterpret_cast<const f32x4*>(p.ws) + (int64_t)tile * p.tail_s * (32 * NT2);
   // GeGLU pairs gate cb = h with up cb = h + 2; plain outputs take cb = 2h, 2h + 1
   const int c0 = GEGLU ? h : 2 * h, c1 = GEGLU ? h + 2 : 2 * h + 1;
-  f32x4 a0 = W[(rb * 4 + c0) * NT2 + t], a1 = W[(rb * 4 + c1) * NT2 + t];
-  for (int z = 1; z < p.tail_s; ++z) {
-    a0 += W[(int64_t)z * (32 * NT2) + (rb * 4 + c0) * NT2 + t];
-    a1 += W[(int64_t)z * (32 * NT2) + (rb * 4 + c1) * NT2 + t];
+  // pieces loaded 4 at a time (all in flight together), summed in piece order (deterministic)
+  const f32x4* W0 = W + (rb * 4 + c0) * NT2 + t;
+  const f32x4* W1 = W + (rb * 4 + c1) * NT2 + t;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < p.tail_s; z += 4) {
+    f32x4 v0[4], v1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool ok = z + u < p.tail_s;
+      v0[u] = ok ? W0[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
+      v1[u] = ok ? W1[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a0 += v0[u];
+      a1 += v1[u];
+    }
   }
   const int64_t m = (int64_t)tm * BT + wr * 128 + rb * 16 + (lane & 15);
   if (GEGLU) {

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 6
+#define PZ_ABI_VERSION 8
 
 enum {
   PZ_OK = 0,
@@ -137,7 +137,9 @@ int pz_qkv_rope_split_bwd(const void* dq, const void* dk, const void* dv, const 
  * uniform, like finfo.min in joint_model.py:271 / pizero.py:291); fp32 softmax (joint_model.py:273).
  * mask_mode 0: none; 1: Pi0 block mask from per-sample prefix counts cnt[b] (pizero.py:271-306),
  * query row r -> token qoff + (r % rows_per_batch)/heads, batch r / rows_per_batch;
- * 2: additive fp32 mask [b][qtok][ldm].  tcap (bf16, NULL ok) saves tanh for backward. */
+ * 2: general additive fp32 mask (joint_model.py:271 adds any [B,1,Lq,Lk] mask): logit += mask[b][qtok][j]
+ * at mask + b*mask_bstride + (qtok - qoff)*ldm (finfo.min entries absorb the logit exactly as in the
+ * reference; a row whose logits are all -inf is uniform).  tcap (bf16, NULL ok) saves tanh for backward. */
 typedef struct pz_softmax_args {
   const float* S; int64_t lds;
   void* P; int64_t ldp;
@@ -209,8 +211,10 @@ int pz_embed_merge(const int64_t* ids, const void* table, int64_t vocab, const v
 int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* dimg, int64_t B, int64_t P,
                        int64_t D, int64_t n_img, int64_t image_token, float img_scale, void* stream);
 
-/* SinusoidalPosEmb (vla/modules.py:9-22) from fp32 t[B] -> bf16 [B, D] */
-int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, void* stream);
+/* SinusoidalPosEmb (vla/modules.py:9-22) from fp32 t[B] -> bf16 [B, D].  mode 0: fp32 math (the fp32
+ * oracle); mode 1: the reference's arithmetic in a bf16 model (bf16 arange, every op rounded to bf16) */
+int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, int32_t mode,
+                  void* stream);
 /* out[b*H+h] = [temb[b], e1[b*H+h]] (vla/modules.py:46-51), bf16 */
 int pz_concat_time(const void* temb, const void* e1, void* out, int64_t B, int64_t H, int64_t D,
                    void* stream);
@@ -239,10 +243,35 @@ int pz_act_bwd(const void* dh, int64_t lddh, const void* pre, int64_t ldpre, voi
  * fp32 moments, gradient pre-scaled by *gscale (device scalar: clip coefficient). */
 int pz_adamw(void* p, const void* g, float* m, float* v, int64_t n, float lr, float beta1,
              float beta2, float eps, float wd, float bc1, float bc2, const float* gscale, void* stream);
-/* sum of squares of bf16 g[0..n) accumulated (atomic, fp32) into acc[0] */
-int pz_sumsq(const void* g, int64_t n, float* acc, void* stream);
-/* clip_grad_norm_ coefficient (train.py:371-374): coef = min(1, max_norm/(sqrt(acc)+1e-6)) */
-int pz_clip_coef(const float* acc, float* coef, float* norm_out, float max_norm, void* stream);
+/* sum of squares of bf16 g[0..n): writes exactly PZ_SUMSQ_PARTS fp32 partials to parts[] (no atomics) */
+#define PZ_SUMSQ_PARTS 2048
+int pz_sumsq(const void* g, int64_t n, float* parts, void* stream);
+/* clip_grad_norm_ coefficient (train.py:371-374; torch.nn.utils.clip_grad_norm_):
+ * norm = sqrt(sum of parts[0..nparts) in a fixed order), coef = min(1, max_norm/(norm+1e-6)) */
+int pz_clip_coef(const float* parts, int64_t nparts, float* coef, float* norm_out, float max_norm,
+                 void* stream);
+
+/* Blockwise 8-bit AdamW (bnb.optim.AdamW8bit, train.py:171-175,194-198; restated in
+ * oracle/adamw8bit.py) over one contiguous run of bf16 params p / grads g.  seg: nseg rows of 4 int64
+ * {element offset in the run, numel, first 256-element block, fp32-state offset or -1}: rows with
+ * -1 keep uint8 codes s1 (m, signed map qmap1) / s2 (v, unsigned map qmap2) indexed like p and one
+ * fp32 absmax per block (absmax1/2[block]); the others keep fp32 m32/v32 (bnb min_8bit_size).
+ * Per element: g *= gscale[0] (NULL: 1); m = b1*m + omb1*g; v = b2*v + omb2*g*g;
+ * p += step * m / (sqrt(v) + epsc); p *= decay; requantise with the block's new absmax.  Host
+ * precomputes omb = 1-b, step = -lr*sqrt(1-b2^t)/(1-b1^t), epsc = eps*sqrt(1-b2^t), decay = 1-lr*wd
+ * (float32).  Every op rounded separately (bit-exact with the oracle).  Deterministic. */
+typedef struct pz_adamw8_args {
+  void* p; const void* g;
+  uint8_t* s1; uint8_t* s2;
+  float* absmax1; float* absmax2;
+  float* m32; float* v32;
+  const int64_t* seg;
+  int64_t nseg, nblocks;
+  const float* qmap1; const float* qmap2;
+  float beta1, beta2, omb1, omb2, step, epsc, decay;
+  const float* gscale;
+} pz_adamw8_args;
+int pz_adamw8bit(const pz_adamw8_args* a, void* stream);
 
 /* deterministic counter-based fill (oracle/synth.py twin): x[i] = off + scale*u(seed, i) */
 int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float off, float scale,

@@ -21,10 +21,12 @@ OUT = os.path.join(HERE, "libpizero_hip.so")
 BUILD = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["pz_gemm.hip", "pz_norm.hip", "pz_attn.hip", "pz_misc.hip", "pz_flash.hip"]
+SOURCES = ["pz_gemm.hip", "pz_norm.hip", "pz_attn.hip", "pz_misc.hip", "pz_flash.hip", "pz_optim.hip"]
 HEADERS = [os.path.join(CSRC, "pz_common.h"), os.path.join(ROOT, "include", "pz_abi.h")]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-Wno-unused-value", "-munsafe-fp-atomics"]
+# per-file extra flags: the 8-bit optimizer is held bit-exact to its float32 oracle, so no FMA contraction
+FILE_FLAGS = {"pz_optim.hip": ["-ffp-contract=off"]}
 
 
 def _needs(obj: str, deps: list[str]) -> bool:
@@ -38,7 +40,7 @@ def _compile(src: str, force: bool) -> str:
     s = os.path.join(CSRC, src)
     obj = os.path.join(BUILD, src.replace(".hip", ".o"))
     if force or _needs(obj, [s] + HEADERS):
-        cmd = [HIPCC, *FLAGS, "-c", s, "-o", obj]
+        cmd = [HIPCC, *FLAGS, *FILE_FLAGS.get(src, []), "-c", s, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")

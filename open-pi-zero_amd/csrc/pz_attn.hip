@@ -127,10 +127,13 @@ __global__ void __launch_bounds__(256) softmax_kernel(pz_softmax_args a) {
     if (j < a.N) {
       float v = s[j] * a.scale;
       if (a.cap > 0.f) v = a.cap * tanhf(v / a.cap);
-      x[e] = v;
       bool al = true;
       if (a.mask_mode == 1) al = block_allowed(qi, j, cnt, a.prefix, a.cond);
-      else if (a.mask_mode == 2) al = mrow[j] > -1e30f;
+      else if (a.mask_mode == 2) {  // additive (joint_model.py:271): finfo.min absorbs v, like the reference
+        v += mrow[j];
+        al = v > -INFINITY;
+      }
+      x[e] = v;
       ok[e] = al;
       if (al) mx = fmaxf(mx, v);
     }
@@ -208,10 +211,13 @@ __global__ void __launch_bounds__(256) softmax4_kernel(pz_softmax_args a) {
         th[e][i] = tanh_fast(v * inv_cap);
         v = a.cap * th[e][i];
       }
-      x[e][i] = v;
       bool al = j < N;
       if (al && a.mask_mode == 1) al = block_allowed(qi, j, cnt, P, Cc);
-      else if (al && a.mask_mode == 2) al = mrow[j] > -1e30f;
+      else if (al && a.mask_mode == 2) {  // additive mask
+        v += mrow[j];
+        al = v > -INFINITY;
+      }
+      x[e][i] = v;
       ok[e][i] = al;
       if (al) mx = fmaxf(mx, v);
     }

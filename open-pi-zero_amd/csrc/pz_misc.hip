@@ -76,15 +76,25 @@ __global__ void embed_merge_bwd_kernel(const int64_t* __restrict__ ids, const bf
   for (int64_t d = threadIdx.x; d < D; d += blockDim.x) dst[d] = f2bf(bf2f(src[d]) * img_scale);
 }
 
-__global__ void time_embed_kernel(const float* __restrict__ t, bf16_t* out, int64_t B, int D, float max_period) {
+// mode 0: fp32 frequencies and product (the fp32 oracle's semantics);
+// mode 1: the reference's bf16 arithmetic when the model runs in bf16 (vla/modules.py:15-22 with t in bf16,
+// train.py:311): arange(half) in bf16 (integers above 256 round to even), every op's result rounded to bf16
+__global__ void time_embed_kernel(const float* __restrict__ t, bf16_t* out, int64_t B, int D, float max_period,
+                                  int mode) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= B * D) return;
   const int64_t b = idx / D;
   const int j = (int)(idx % D), half = D / 2;
   const int i = j < half ? j : j - half;
-  const float e = logf(max_period) / (float)(half - 1);
-  const float f = expf((float)i * -e);
-  const float a = t[b] * f;
+  const float e = (float)(log((double)max_period) / (double)(half - 1));
+  float a;
+  if (mode == 0) {
+    a = t[b] * expf((float)i * -e);
+  } else {
+    const float ib = bf2f(f2bf((float)i));
+    const float f = bf2f(f2bf(expf(bf2f(f2bf(ib * -e)))));
+    a = bf2f(f2bf(bf2f(f2bf(t[b])) * f));
+  }
   out[idx] = f2bf(j < half ? sinf(a) : cosf(a));
 }
 
@@ -210,7 +220,9 @@ __global__ void adamw_kernel(bf16_t* __restrict__ p, const bf16_t* __restrict__ 
   }
 }
 
-__global__ void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n, float* acc) {
+// one fp32 partial per block (no atomics): the global norm is summed in a fixed order by
+// clip_coef_kernel, so the clip coefficient -- and training -- is bitwise reproducible
+__global__ void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n, float* parts) {
   __shared__ float red[4];
   float s = 0.f;
   const int64_t n8 = n / 8;
@@ -228,13 +240,20 @@ __global__ void sumsq_kernel(const bf16_t* __restrict__ g, int64_t n, float* acc
       s += a * a;
     }
   s = block_sum<4>(s, red);
-  if (threadIdx.x == 0) atomicAdd(acc, s);
+  if (threadIdx.x == 0) parts[blockIdx.x] = s;
 }
 
-__global__ void clip_coef_kernel(const float* acc, float* coef, float* norm_out, float max_norm) {
-  const float nrm = sqrtf(acc[0]);
-  if (norm_out) norm_out[0] = nrm;
-  coef[0] = fminf(1.f, max_norm / (nrm + 1e-6f));
+__global__ void clip_coef_kernel(const float* __restrict__ parts, int64_t nparts, float* coef, float* norm_out,
+                                 float max_norm) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < nparts; i += blockDim.x) s += parts[i];
+  s = block_sum<4>(s, red);
+  if (threadIdx.x == 0) {
+    const float nrm = sqrtf(s);
+    if (norm_out) norm_out[0] = nrm;
+    coef[0] = fminf(1.f, max_norm / (nrm + 1e-6f));
+  }
 }
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
@@ -299,10 +318,11 @@ extern "C" int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* di
   return PZ_OK;
 }
 
-extern "C" int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, void* stream) {
-  PZ_CHECK_ARG(t && out && B > 0 && D % 2 == 0 && D >= 4, "time_embed: bad args");
+extern "C" int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, int32_t mode,
+                             void* stream) {
+  PZ_CHECK_ARG(t && out && B > 0 && D % 2 == 0 && D >= 4 && (mode == 0 || mode == 1), "time_embed: bad args");
   hipLaunchKernelGGL(time_embed_kernel, dim3(nblk(B * D)), dim3(256), 0, ST, t, (bf16_t*)out, B, (int)D,
-                     max_period);
+                     max_period, (int)mode);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
@@ -401,18 +421,17 @@ extern "C" int pz_adamw(void* p, const void* g, float* m, float* v, int64_t n, f
   return PZ_OK;
 }
 
-extern "C" int pz_sumsq(const void* g, int64_t n, float* acc, void* stream) {
-  PZ_CHECK_ARG(g && acc && n >= 0 && PZ_ALIGNED(g, 16), "sumsq: bad args (16-byte alignment)");
-  if (n == 0) return PZ_OK;
-  const int64_t blocks = n / 2048 + 1 < 4096 ? n / 2048 + 1 : 4096;
-  hipLaunchKernelGGL(sumsq_kernel, dim3((unsigned)blocks), dim3(256), 0, ST, (const bf16_t*)g, n, acc);
+extern "C" int pz_sumsq(const void* g, int64_t n, float* parts, void* stream) {
+  PZ_CHECK_ARG(g && parts && n >= 0 && PZ_ALIGNED(g, 16), "sumsq: bad args (16-byte alignment)");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(PZ_SUMSQ_PARTS), dim3(256), 0, ST, (const bf16_t*)g, n, parts);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
 
-extern "C" int pz_clip_coef(const float* acc, float* coef, float* norm_out, float max_norm, void* stream) {
-  PZ_CHECK_ARG(acc && coef, "clip_coef: bad args");
-  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, ST, acc, coef, norm_out, max_norm);
+extern "C" int pz_clip_coef(const float* parts, int64_t nparts, float* coef, float* norm_out, float max_norm,
+                            void* stream) {
+  PZ_CHECK_ARG(parts && coef && nparts > 0, "clip_coef: bad args");
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, ST, parts, nparts, coef, norm_out, max_norm);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

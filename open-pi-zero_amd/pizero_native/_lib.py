@@ -12,9 +12,10 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 6  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 8  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
+PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
 
 i64, i32, f32, vp = C.c_int64, C.c_int32, C.c_float, C.c_void_p
 fp = C.POINTER(C.c_float)
@@ -77,6 +78,16 @@ class FlashArgs(C.Structure):
     ]
 
 
+class AdamW8Args(C.Structure):
+    _fields_ = [
+        ("p", vp), ("g", vp), ("s1", vp), ("s2", vp), ("absmax1", vp), ("absmax2", vp),
+        ("m32", vp), ("v32", vp), ("seg", vp), ("nseg", i64), ("nblocks", i64),
+        ("qmap1", vp), ("qmap2", vp),
+        ("beta1", f32), ("beta2", f32), ("omb1", f32), ("omb2", f32), ("step", f32), ("epsc", f32),
+        ("decay", f32), ("gscale", vp),
+    ]
+
+
 # name -> argtypes (restype int unless listed in _RESTYPE)
 SIGNATURES = {
     "pz_gemm": [C.POINTER(GemmArgs), vp],
@@ -101,7 +112,7 @@ SIGNATURES = {
     "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],
     "pz_embed_merge": [vp, vp, i64, vp, vp, i64, i64, i64, i64, i64, i64, f32, f32, vp],
     "pz_embed_merge_bwd": [vp, vp, vp, i64, i64, i64, i64, i64, f32, vp],
-    "pz_time_embed": [vp, vp, i64, i64, f32, vp],
+    "pz_time_embed": [vp, vp, i64, i64, f32, i32, vp],
     "pz_concat_time": [vp, vp, vp, i64, i64, i64, vp],
     "pz_split_time_grad": [vp, vp, i64, i64, vp],
     "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
@@ -112,8 +123,9 @@ SIGNATURES = {
     "pz_geglu_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, vp],
     "pz_act_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, vp],
     "pz_adamw": [vp, vp, vp, vp, i64, f32, f32, f32, f32, f32, f32, f32, vp, vp],
+    "pz_adamw8bit": [C.POINTER(AdamW8Args), vp],
     "pz_sumsq": [vp, i64, vp, vp],
-    "pz_clip_coef": [vp, vp, vp, f32, vp],
+    "pz_clip_coef": [vp, i64, vp, vp, f32, vp],
     "pz_fill_uniform": [vp, i32, i64, C.c_uint64, f32, f32, vp],
     "pz_cast_f32_bf16": [vp, vp, i64, vp],
     "pz_cast_bf16_f32": [vp, vp, i64, vp],

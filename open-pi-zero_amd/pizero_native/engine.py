@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -78,6 +79,7 @@ class Dims:
     sig_min: float
     steps: int
     clip: float | None
+    time_bf16: bool = False  # pz_time_embed mode 1: the reference's bf16 arithmetic (see modules.py)
 
     @staticmethod
     def from_cfg(cfg):
@@ -106,6 +108,7 @@ class Dims:
             p_theta=float(_cfg(mix, "proprio.rope_theta", _cfg(mix, "action.rope_theta", 10000.0))),
             tmax=float(_cfg(cfg, "time_max_period", 10000.0)), sig_min=float(_cfg(cfg, "flow_sig_min", 0.001)),
             steps=int(_cfg(cfg, "num_inference_steps")), clip=None if clip is None else float(clip),
+            time_bf16=bool(_cfg(cfg, "time_embed_bf16_reference", False)),
         )
 
     @property
@@ -119,6 +122,31 @@ class Dims:
     @property
     def kcols(self):
         return (3 * self.ps * self.ps + 31) // 32 * 32
+
+
+class _Token:
+    """Lifetime marker of the forward state that borrows the engine's joint K/V buffers."""
+
+
+class GeneralMask:
+    """A caller attention mask that is NOT the Pi0 block pattern (pizero.py:271-306).
+
+    The reference adds any additive mask to the soft-capped logits (joint_model.py:261-287); such a
+    mask is applied here by the GEMM + softmax path (pz_attn_softmax mask_mode 2, fp32 additive),
+    never by the fused kernels, which generate the block mask from per-sample prefix counts.
+    ``full``: fp32 [B, L, L] (training); ``itp``: fp32 [B, P+C, P+C] and ``act``: fp32 [B, H, L]
+    (inference, pizero.py:326-336 split)."""
+
+    def __init__(self, full=None, itp=None, act=None):
+        self.full, self.itp, self.act = full, itp, act
+
+
+def _mask_kw(d, cnt, which):
+    """pz_attn_softmax mask arguments: block mask from cnt, or the general additive mask."""
+    if isinstance(cnt, GeneralMask):
+        m = getattr(cnt, which)
+        return dict(mask_mode=2, mask=m, ldm=m.shape[2], mask_bstride=m.shape[1] * m.shape[2])
+    return dict(mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C)
 
 
 class Group:
@@ -137,6 +165,7 @@ class Engine:
         self.d = Dims.from_cfg(model.cfg)
         self._tables = {}
         self._ws = {}
+        self._jkv_holder = None
         # joint attention kernel: "gemm" = MFMA GEMMs around the soft-cap/block-mask softmax (default:
         # faster today), "flash" = the fused pz_flash kernels (no L x L tensors)
         self.joint_flash = os.environ.get("PZ_JOINT_ATTN", "gemm") == "flash"
@@ -388,7 +417,7 @@ class Engine:
         e1 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
         ops.small_linear(psi_bf, self.w("action_encoder.linear_1.weight"), e1, bias=self.w("action_encoder.linear_1.bias"))
         temb = torch.empty(B, d.aH, device=dev, dtype=BF16)
-        ops.time_embed(t, temb, d.tmax)
+        ops.time_embed(t, temb, d.tmax, ref_bf16=d.time_bf16)
         cat = torch.empty(rows, 2 * d.aH, device=dev, dtype=BF16)
         ops.concat_time(temb, e1, cat, B, rows // B, d.aH)
         pre = torch.empty(rows, d.aH, device=dev, dtype=BF16)
@@ -415,6 +444,27 @@ class Engine:
             mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh,
             dgroups=None if dO is None else [dO[g.name] for g in gs], delta=delta, dq=dq, dk=dk, dv=dv)
 
+    def _joint_kv(self, B, Lp, dev, save):
+        """Joint K/V buffers [nL, B, Lp, hd] for one training forward.  The engine owns one zeroed set
+        (the Lp - L pad rows stay zero for the GEMM path; rows < L are rewritten by every forward) and
+        lends it to the forward whose saved state (``save``) holds the token; while that state is alive
+        (its backward has not run and its graph still exists) another forward gets fresh buffers, so
+        interleaved forwards never share saved K/V."""
+        holder = self._jkv_holder() if self._jkv_holder is not None else None
+        if holder is not None:
+            k = torch.zeros(self.d.nL, B, Lp, self.d.hd, device=dev, dtype=BF16)
+            return k, torch.zeros_like(k)
+        key = ("jkv", B, Lp, dev)
+        kv = self._ws.get(key)
+        if kv is None:
+            self._ws = {k: v for k, v in self._ws.items() if k[0] != "jkv"}  # one shape at a time
+            k = torch.zeros(self.d.nL, B, Lp, self.d.hd, device=dev, dtype=BF16)
+            kv = self._ws[key] = (k, torch.zeros_like(k))
+        tok = _Token()
+        save["_jkv_token"] = tok
+        self._jkv_holder = weakref.ref(tok)
+        return kv
+
     def _joint_layers_train(self, groups, X, pos, cnt, B, save):
         """joint_model.py:24-304 x nL for the training pass (all mixtures active)."""
         d = self.d
@@ -422,11 +472,11 @@ class Engine:
         L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
         S = None
         layers = []
+        Kall, Vall = self._joint_kv(B, Lp, dev, save)
         for l in range(d.nL):
             last = l == d.nL - 1
             Qj = torch.empty(B, L, nh * hd, device=dev, dtype=BF16)
-            Kj = torch.zeros(B, Lp, hd, device=dev, dtype=BF16)
-            Vj = torch.zeros(B, Lp, hd, device=dev, dtype=BF16)
+            Kj, Vj = Kall[l], Vall[l]
             st = {"Q": Qj, "K": Kj, "V": Vj, "g": {}}
             for g in groups:
                 p = f"{g.prefix}{l}."
@@ -442,7 +492,7 @@ class Engine:
                                    Lp, g.off)
                 st["g"][g.name] = {"x": x, "h": h, "r": r}
             Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
-            if self.joint_flash:
+            if self.joint_flash and not isinstance(cnt, GeneralMask):
                 # fused joint attention (joint_model.py:259-292): soft-cap, block mask from cnt, O rows
                 # scattered into each mixture's o_proj input; one fp32 log-sum-exp per (token, head) row
                 lse = torch.empty(B, L * nh, device=dev, dtype=F32)
@@ -456,8 +506,8 @@ class Engine:
                          sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
                 Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
                 tc = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
-                ops.attn_softmax(S, Lp, Pm, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), cap=50.0, tcap=tc, mask_mode=1,
-                                 rows_per_batch=L * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
+                ops.attn_softmax(S, Lp, Pm, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), cap=50.0, tcap=tc,
+                                 rows_per_batch=L * nh, heads=nh, qoff=0, **_mask_kw(d, cnt, "full"))
                 st["P"], st["tc"] = Pm, tc
                 for g in groups:
                     if not (last and g.skip_last):
@@ -601,6 +651,7 @@ class Engine:
                 self._norm_grads(p + "input_layernorm.", part, None, beta)
                 dX[g.name] = dxn
             self._notify("joint", l)
+        sv.pop("_jkv_token", None)  # the joint K/V buffers are free for the next forward
         return dX
 
     # ============================================================ training ==
@@ -818,7 +869,7 @@ class Engine:
                 hs[g.name] = h
             if last:
                 break
-            if self.infer_flash:  # fused attention over the L1 prefix keys (no L1 x L1 tensor)
+            if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over the L1 prefix keys
                 Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
                 ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, g.T, Os[g.name]) for g in groups], L1, L1, 0,
                                                      cnt, B))
@@ -831,8 +882,8 @@ class Engine:
                 Pm = torch.empty(B, L1 * nh, Lp, device=dev, dtype=BF16)
             ops.gemm(L1 * nh, L1, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(L1 * nh * hd, 0),
                      sB=(Lp * hd, 0), sC=(L1 * nh * Lp, 0))
-            ops.attn_softmax(S, Lp, Pm, Lp, B * L1 * nh, L1, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,
-                             rows_per_batch=L1 * nh, heads=nh, qoff=0, cnt=cnt, prefix=d.P, cond=d.C)
+            ops.attn_softmax(S, Lp, Pm, Lp, B * L1 * nh, L1, 1.0 / math.sqrt(hd), cap=50.0,
+                             rows_per_batch=L1 * nh, heads=nh, qoff=0, **_mask_kw(d, cnt, "itp"))
             for g in groups:
                 p = f"{g.prefix}{l}."
                 x = X[g.name]
@@ -915,7 +966,7 @@ class Engine:
                 ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
                 ops.linear(h, self.qkv_w(p), qkv)
             ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
-            if self.infer_flash:  # fused attention of the action queries over every cached key
+            if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over every cached key
                 if O is None:
                     O = torch.empty(B * d.H, nh * hd, device=dev, dtype=BF16)
                 ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, d.H, O)], d.H, L, g.off, cnt, B))
@@ -926,8 +977,8 @@ class Engine:
                 Pm = torch.empty(B, d.H * nh, Lp, device=dev, dtype=BF16)
             ops.gemm(d.H * nh, L, hd, Q, hd, True, Kj, hd, True, S, Lp, batch=B, sA=(d.H * nh * hd, 0),
                      sB=(Lp * hd, 0), sC=(d.H * nh * Lp, 0))
-            ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=1,
-                             rows_per_batch=d.H * nh, heads=nh, qoff=d.P + d.C, cnt=cnt, prefix=d.P, cond=d.C)
+            ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0,
+                             rows_per_batch=d.H * nh, heads=nh, qoff=d.P + d.C, **_mask_kw(d, cnt, "act"))
             x = self._post_attn(g, p, x, Pm, Vj, B, d.H, Lp, qrow0=0)
         y = torch.empty_like(x)
         ops.rmsnorm(x, self.w("joint_model.mixtures.action.norm.weight"), y, None, d.rms_eps)

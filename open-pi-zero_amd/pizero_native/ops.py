@@ -19,6 +19,8 @@ from ._lib import (
     PZ_EPI_GELU,
     PZ_EPI_NONE,
     PZ_EPI_SILU,
+    PZ_SUMSQ_PARTS,
+    AdamW8Args,
     FlashArgs,
     GemmArgs,
     SmallGemmArgs,
@@ -377,9 +379,9 @@ def embed_merge_bwd(ids, dout, dimg, n_img, image_token, img_scale):
          _st())
 
 
-def time_embed(t, out, max_period):
+def time_embed(t, out, max_period, ref_bf16=False):
     B, D = out.shape
-    call("pz_time_embed", _p(t), _p(out), B, D, float(max_period), _st())
+    call("pz_time_embed", _p(t), _p(out), B, D, float(max_period), int(bool(ref_bf16)), _st())
 
 
 def concat_time(temb, e1, out, B, H, D):
@@ -428,12 +430,39 @@ def adamw(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, gscale=None):
          float(wd), float(bc1), float(bc2), _p(gscale), _st())
 
 
-def sumsq(g, acc):
-    call("pz_sumsq", _p(g), g.numel(), _p(acc), _st())
+def adamw8bit(run, g, qmap1, qmap2, lr, b1, b2, eps, wd, t, gscale=None):
+    """One bnb-style 8-bit AdamW step over a contiguous run (optim.FusedAdamW._prepare_8bit layout).
+    Host precomputes the float32 constants exactly as oracle/adamw8bit.py does."""
+    import numpy as np
+
+    f = np.float32
+    c1 = f(1.0 - b1 ** t)
+    c2 = f(np.sqrt(1.0 - b2 ** t))
+    a = AdamW8Args()
+    a.p, a.g = _p(run["flat"]), _p(g)
+    a.s1, a.s2 = _p(run["s1"]), _p(run["s2"])
+    a.absmax1, a.absmax2 = _p(run["absmax1"]), _p(run["absmax2"])
+    a.m32, a.v32 = _p(run["m32"]), _p(run["v32"])
+    a.seg, a.nseg, a.nblocks = _p(run["seg"]), run["nseg"], run["nblocks"]
+    a.qmap1, a.qmap2 = _p(qmap1), _p(qmap2)
+    a.beta1, a.beta2 = float(f(b1)), float(f(b2))
+    a.omb1, a.omb2 = float(f(1.0 - b1)), float(f(1.0 - b2))
+    a.step = float(f(f(-lr) * c2 / c1))
+    a.epsc = float(f(f(eps) * c2))
+    a.decay = float(f(1.0 - lr * wd)) if wd > 0 else 1.0
+    a.gscale = _p(gscale)
+    call("pz_adamw8bit", C.byref(a), _st())
 
 
-def clip_coef(acc, coef, norm_out, max_norm):
-    call("pz_clip_coef", _p(acc), _p(coef), _p(norm_out), float(max_norm), _st())
+def sumsq(g, parts):
+    """writes PZ_SUMSQ_PARTS fp32 partial sums of g*g into parts[0:PZ_SUMSQ_PARTS]"""
+    assert parts.dtype == torch.float32 and parts.numel() >= PZ_SUMSQ_PARTS
+    call("pz_sumsq", _p(g), g.numel(), _p(parts), _st())
+
+
+def clip_coef(parts, coef, norm_out, max_norm):
+    """norm = sqrt(sum(parts)) (fixed order), coef = min(1, max_norm / (norm + 1e-6))"""
+    call("pz_clip_coef", _p(parts), parts.numel(), _p(coef), _p(norm_out), float(max_norm), _st())
 
 
 def fill_uniform(x, seed, off, scale):

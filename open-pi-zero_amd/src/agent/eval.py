@@ -56,10 +56,10 @@ class EvalAgent:
         g = self._graphs.get(B)
         if g is None:
             g = self._graphs[B] = InferenceGraph(m, B)
-            g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m._prefix_counts(itp.to(dev)),
+            g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m.block_prefix_counts(itp, amask),
                    vpos.to(dev), ppos.to(dev), apos.to(dev), proprios.to(dev, torch.float32), noise)
             g.capture()
-        g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m._prefix_counts(itp.to(dev)), vpos.to(dev),
+        g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m.block_prefix_counts(itp, amask), vpos.to(dev),
                ppos.to(dev), apos.to(dev), proprios.to(dev, torch.float32), noise)
         return g.replay().to(self.dtype)
 

@@ -10,8 +10,9 @@ Same structure and semantics as shroglck/open-pi-zero's TrainAgent:
   * checkpoints with the reference's keys (cnt_update, cnt_batch, model,
     action_optimizer, vlm_optimizer, *_lr_scheduler, wandb_id, n_averaged).
 MI355X-native pieces: pizero_native.ddp.PiZeroDDP (RCCL bucketed all-reduce
-overlapped with backward), pizero_native.optim.FusedAdamW (flat fused AdamW;
-bitsandbytes AdamW8bit is not available -- parity unpinned).
+overlapped with backward), pizero_native.optim.FusedAdamW (flat fused AdamW; by default
+with the reference's blockwise 8-bit state, ``optimizer_state_bits: 8`` -- the algorithm of
+bitsandbytes' AdamW8bit restated, bitsandbytes itself absent: parity with it unpinned).
 Data: the OXE/RLDS TensorFlow pipeline is out of scope; the
 agent consumes any iterable of reference-format batches, by default
 ``SyntheticBridgeDataset`` (bridge-shaped random batches, already tokenized).
@@ -29,6 +30,16 @@ import torch
 from src.utils.config import cfg_get
 
 log = logging.getLogger(__name__)
+
+
+def sample_fm_time(bsz, flow_sampling="beta", beta_dist=None, t_max=1 - 0.001):
+    """train.py:239-247: beta -> t = t_max * (1 - Beta(alpha, beta)); uniform -> stratified
+    (U + arange(B)/B) mod (1 - 1e-5).  Same torch RNG calls as the reference (seeded parity)."""
+    if flow_sampling == "uniform":
+        return (torch.rand(1) + torch.arange(bsz) / bsz) % (1 - 1e-5)
+    if flow_sampling != "beta":
+        raise ValueError(f"Invalid flow matching timestep sampling mode: {flow_sampling}")
+    return t_max * (1 - beta_dist.sample((bsz,)))
 
 
 class SyntheticBridgeDataset(torch.utils.data.IterableDataset):
@@ -88,14 +99,18 @@ class TrainAgent:
         self.log_dir = cfg_get(cfg, "log_dir", "") or "."
         self.checkpoint_dir = os.path.join(self.log_dir, "checkpoint")
 
+        self.cnt_update = 0
+        self.cnt_batch = 0
+        self.wandb_id = None
         model = PiZero(cfg, use_ddp=self.multi_gpu, device=self.device, dtype=self.dtype, init="default")
-        if cfg_get(cfg, "resume_checkpoint_path"):
-            self._load_model(model, cfg_get(cfg, "resume_checkpoint_path"))
+        self.model = model
+        resume = cfg_get(cfg, "resume_checkpoint_path")
+        if resume:
+            self.load_checkpoint(resume)
         elif cfg_get(cfg, "load_pretrained_weights", False):
             model.load_pretrained_weights()
         model.tie_action_proprio_weights()
         model.freeze_unused_weights()
-        self.model = model
         self.model_meta = PiZeroDDP(model) if self.multi_gpu else model
 
         per_dev = int(cfg_get(cfg, "per_device_batch_size"))
@@ -103,8 +118,11 @@ class TrainAgent:
         self.train_dataloader = dataset if dataset is not None else SyntheticBridgeDataset(cfg, per_dev, seed=self.rank)
 
         self.train_vlm = bool(cfg_get(cfg, "train_vlm", True))
+        # the reference's bnb AdamW8bit (train.py:171-175): blockwise 8-bit state by default
+        self.state_bits = int(cfg_get(cfg, "optimizer_state_bits", 8))
         self.action_optimizer = FusedAdamW(model.action_expert_parameters, lr=cfg_get(cfg, "action_lr"),
-                                           weight_decay=cfg_get(cfg, "action_weight_decay", 0.0))
+                                           weight_decay=cfg_get(cfg, "action_weight_decay", 0.0),
+                                           state_bits=self.state_bits)
         sch = lambda opt, key, lr: CosineAnnealingWarmupRestarts(  # noqa: E731
             opt, first_cycle_steps=cfg_get(cfg, f"{key}.first_cycle_steps"), cycle_mult=1.0, max_lr=lr,
             min_lr=cfg_get(cfg, f"{key}.min_lr"), warmup_steps=cfg_get(cfg, f"{key}.warmup_steps"), gamma=1.0)
@@ -112,7 +130,8 @@ class TrainAgent:
         self.optimizers = [self.action_optimizer]
         if self.train_vlm:
             self.vlm_optimizer = FusedAdamW(model.trainable_vlm_parameters, lr=cfg_get(cfg, "vlm_lr"),
-                                            weight_decay=cfg_get(cfg, "vlm_weight_decay", 0.0))
+                                            weight_decay=cfg_get(cfg, "vlm_weight_decay", 0.0),
+                                            state_bits=self.state_bits)
             self.vlm_lr_scheduler = sch(self.vlm_optimizer, "vlm_lr_scheduler", cfg_get(cfg, "vlm_lr"))
             self.optimizers.append(self.vlm_optimizer)
         else:
@@ -122,32 +141,38 @@ class TrainAgent:
         self.flow_t_max = 1 - float(cfg_get(cfg, "flow_sig_min", 0.001))
         self.flow_beta_dist = torch.distributions.Beta(float(cfg_get(cfg, "flow_alpha", 1.5)),
                                                        float(cfg_get(cfg, "flow_beta", 1)))
-        self.cnt_update = 0
-        self.cnt_batch = 0
+        if resume:
+            self.load_optimizer(resume)
 
     def sample_fm_time(self, bsz):
         """train.py:239-247."""
-        if self.flow_sampling == "uniform":
-            return (torch.rand(1) + torch.arange(bsz) / bsz) % (1 - 1e-5)
-        return self.flow_t_max * (1 - self.flow_beta_dist.sample((bsz,)))
+        return sample_fm_time(bsz, self.flow_sampling, self.flow_beta_dist, self.flow_t_max)
 
     def preprocess_batch(self, batch, split_mask=False, sample_fm_time=True):
-        """train.py:271-314 (pixel normalisation of vla/processing.py:109-114 included)."""
+        """train.py:271-314 with the per-batch work on the device: the raw batch
+        (int64 ids / attention mask, uint8 pixels, fp32 proprio / actions) is copied once, then the
+        block mask + positions (vectorised builder, pizero.py:271-324) and the pixel normalisation
+        (x/255 - 0.5)/0.5 (vla/processing.py:109-114) are computed on the GPU -- no per-sample host
+        loop, and 1 byte per pixel crosses PCIe instead of 2."""
         m = self.model
-        mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids(batch["attention_mask"], self.dtype)
-        pix = batch["pixel_values"]
+        dev = self.device
+        nb = dict(non_blocking=True)
+        am = batch["attention_mask"].to(dev, **nb)
+        mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids(am, self.dtype)
+        pix = batch["pixel_values"].to(dev, **nb)
         if pix.dtype == torch.uint8:
-            pix = (pix.float() / 255.0 - 0.5) / 0.5
-        inputs = {"input_ids": batch["input_ids"], "pixel_values": pix.to(self.dtype), "vlm_position_ids": vpos,
-                  "proprio_position_ids": ppos, "action_position_ids": apos,
-                  "proprios": batch["proprio"].to(self.dtype), "actions": batch["action"].to(self.dtype)}
+            pix = (pix.to(torch.float32) / 255.0 - 0.5) / 0.5
+        inputs = {"input_ids": batch["input_ids"].to(dev, **nb), "pixel_values": pix.to(self.dtype),
+                  "vlm_position_ids": vpos, "proprio_position_ids": ppos, "action_position_ids": apos,
+                  "proprios": batch["proprio"].to(dev, **nb).to(self.dtype),
+                  "actions": batch["action"].to(dev, **nb).to(self.dtype)}
         if split_mask:
             inputs["image_text_proprio_mask"], inputs["action_mask"] = m.split_full_mask_into_submasks(mask)
         else:
             inputs["causal_mask"] = mask
         if sample_fm_time:
-            inputs["t"] = self.sample_fm_time(len(batch["input_ids"])).to(self.dtype)
-        return {k: v.to(self.device, non_blocking=True) for k, v in inputs.items()}
+            inputs["t"] = self.sample_fm_time(len(batch["input_ids"])).to(dev, **nb).to(self.dtype)
+        return inputs
 
     def run(self):
         from pizero_native.optim import clip_grad_norm_
@@ -204,9 +229,23 @@ class TrainAgent:
         torch.save(data, path)
         return path
 
-    @staticmethod
-    def _load_model(model, path):
+    def load_checkpoint(self, path):
+        """train.py:531-544: counters + weights (strict, ``_orig_mod.`` prefix of compiled saves stripped)."""
         data = torch.load(path, weights_only=True, map_location="cpu")
+        self.cnt_update = int(data["cnt_update"])
+        self.cnt_batch = int(data["cnt_batch"])
+        self.wandb_id = data.get("wandb_id")
         sd = {k.replace("_orig_mod.", ""): v for k, v in data["model"].items()}
-        model.load_state_dict(sd, strict=True)
+        self.model.load_state_dict(sd, strict=True)
+        log.info("Loaded model from %s at update %d batch %d", path, self.cnt_update, self.cnt_batch)
         return data
+
+    def load_optimizer(self, path):
+        """train.py:546-560: optimizer moments/steps and scheduler states."""
+        data = torch.load(path, weights_only=True, map_location="cpu")
+        self.action_optimizer.load_state_dict(data["action_optimizer"])
+        self.action_lr_scheduler.load_state_dict(data["action_lr_scheduler"])
+        if self.train_vlm:
+            self.vlm_optimizer.load_state_dict(data["vlm_optimizer"])
+            self.vlm_lr_scheduler.load_state_dict(data["vlm_lr_scheduler"])
+        log.info("Loaded optimizer and scheduler states from %s", path)

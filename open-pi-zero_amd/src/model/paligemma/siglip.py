@@ -5,9 +5,10 @@ reference (src/model/paligemma/siglip.py:9-320) so hydra-style ``_target_``
 configs resolve and checkpoints load with strict=True.  The computation is
 not done by these modules: the owning ``PiZero`` packs every weight into its
 flat arena and runs the tower with HIP kernels (pizero_native.engine:
-patchify + MFMA patch GEMM, 27x [LayerNorm, fused QKV GEMM, batched
-attention GEMMs + softmax, out-proj+residual GEMM, LayerNorm, fc1+GELU GEMM,
-fc2+residual GEMM], post-LN, projector GEMM).  Modules are created on the meta
+patchify + MFMA patch GEMM, 27x [LayerNorm, fused QKV GEMM, fused head_dim-72
+attention (flash_fwd_res_kernel<72>: LDS-resident keys, no [B, 16, 256, 256] tensor),
+out-proj+residual GEMM, LayerNorm, fc1+GELU GEMM, fc2+residual GEMM], post-LN,
+projector GEMM).  Modules are created on the meta
 device and materialised by the arena.
 """
 
@@ -21,7 +22,7 @@ from src.utils.config import cfg_get
 def _native_only(name):
     raise RuntimeError(
         f"{name}.forward is executed by the native Pi0 engine; call PiZero.forward / "
-        "PiZero.infer_action (or PiZero.siglip_features) instead")
+        "PiZero.infer_action instead")
 
 
 class PaliGemmaMultiModalProjector(nn.Module):

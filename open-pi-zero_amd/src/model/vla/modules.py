@@ -1,8 +1,12 @@
 """Action/time encoders (vla/modules.py:9-53) as parameter containers.
 
-SinusoidalPosEmb -> pz_time_embed (fp32 t, fp32 frequencies; the reference's
-bf16 ``arange`` rounding above 256 is not reproduced: parity is stated
-against the fp32 oracle).  ActionEncoder -> pz_gemm_small (K=7) +
+SinusoidalPosEmb -> pz_time_embed.  Default (mode 0): fp32 t and fp32 frequencies
+= the reference module in fp32 (the fp32 oracle's semantics).  The reference in a
+bf16 model computes it in bf16 (t cast to bf16 at train.py:311, ``arange`` in t.dtype
+so odd indices above 256 round, every op rounded): that arithmetic is mode 1, selected
+with the config key ``time_embed_bf16_reference: true``.  Measured size of the
+difference (reference fp32 vs reference bf16, 1024 wide, tests/golden/time_embed.npz):
+max |d| 5.3e-3, mean 2.3-4.6e-4; tests/test_kernels_gpu.py pins both modes.  ActionEncoder -> pz_gemm_small (K=7) +
 pz_concat_time + MFMA GEMM with SiLU epilogue + MFMA GEMM.
 """
 

@@ -338,16 +338,93 @@ class PiZero(nn.Module, NoSyncBase):
         vpos = torch.arange(1, P + 1, device=dev).repeat(bsz, 1)
         ppos = torch.arange(1, C + 1, device=dev).repeat(bsz, 1)
         apos = torch.arange(C + 1, C + H + 1, device=dev).repeat(bsz, 1)
+        # built here from cnt: known block pattern (finfo.min absorbs), so forward() skips validation
+        if torch.finfo(dtype).min <= -1e30:
+            self._mask_remember([mask], cnt.to(torch.int32).contiguous())
         return mask, vpos, ppos, apos
 
     def split_full_mask_into_submasks(self, causal_mask):
+        """pizero.py:326-336 (views); a validated full mask passes its prefix counts on to the pair."""
         n = self.max_image_text_tokens + self.num_proprio_tokens
-        return causal_mask[..., :n, :n], causal_mask[..., -self.num_action_tokens:, :]
+        itp, am = causal_mask[..., :n, :n], causal_mask[..., -self.num_action_tokens:, :]
+        spec = self._mask_lookup([causal_mask])
+        if spec is not None:
+            self._mask_remember([itp, am], spec)
+        return itp, am
 
     def _prefix_counts(self, mask):
         """Per-sample image+text token count from the proprio row of the block mask."""
         P = self.max_image_text_tokens
         return (mask[:, 0, P, :P] == 0).sum(-1).to(torch.int32).contiguous()
+
+    def _block_allowed(self, cnt, rows, ncols):
+        """[B, len(rows), ncols] bool: the Pi0 block pattern of pizero.py:271-306 for prefix counts cnt."""
+        P, C = self.max_image_text_tokens, self.num_proprio_tokens
+        i = rows.view(1, -1, 1)
+        j = torch.arange(ncols, device=cnt.device).view(1, 1, -1)
+        c = cnt.view(-1, 1, 1).to(torch.int64)
+        return torch.where(i < P, (i < c) & (j < c),
+                           torch.where(i < P + C, (j < c) | ((j >= P) & (j < P + C)), (j < c) | (j >= P)))
+
+    @staticmethod
+    def _is_block(mask, allowed):
+        """mask == 0 where allowed and <= -1e30 elsewhere (finfo.min of bf16/fp32, which absorbs any
+        logit exactly like the block kernels' 'excluded' -- a fully masked row is then uniform)."""
+        m = mask[:, 0]
+        return bool(torch.where(allowed, m == 0, m <= -1e30).all())
+
+    def _mask_spec(self, masks, rows_list):
+        """Validate the caller's additive mask(s) once per new tensor: the Pi0 block
+        pattern -> int32 per-sample prefix counts (the fused kernels regenerate the mask from them);
+        anything else -> engine.GeneralMask (the GEMM+softmax path adds it like joint_model.py:271).
+        The cache holds the mask tensors themselves (identity + version), so a freed-and-reused address
+        can never alias a stale entry."""
+        from pizero_native.engine import GeneralMask
+
+        hit = self._mask_lookup(masks)
+        if hit is not None:
+            return hit
+        itp = masks[0]
+        P = self.max_image_text_tokens
+        cnt = self._prefix_counts(itp) if itp.shape[2] > P else None
+        ok = cnt is not None
+        if ok:
+            for m, rows in zip(masks, rows_list):
+                if not self._is_block(m, self._block_allowed(cnt, rows, m.shape[-1])):
+                    ok = False
+                    break
+        if ok:
+            spec = cnt
+        else:
+            f = [m[:, 0].to(torch.float32).contiguous() for m in masks]
+            spec = GeneralMask(full=f[0]) if len(f) == 1 else GeneralMask(itp=f[0], act=f[1])
+            log.warning("attention mask is not the Pi0 block pattern: using the general additive-mask path")
+        self._mask_remember(masks, spec)
+        return spec
+
+    _MASK_CACHE = 6
+
+    def _mask_lookup(self, masks):
+        for ms, vers, spec in self.__dict__.get("_mask_cache", ()):
+            if len(ms) == len(masks) and all(a is b and a._version == v for a, b, v in zip(ms, masks, vers)):
+                return spec
+        return None
+
+    def _mask_remember(self, masks, spec):
+        cache = [e for e in self.__dict__.get("_mask_cache", []) if not all(a is b for a, b in zip(e[0], masks))]
+        cache.append((tuple(masks), tuple(m._version for m in masks), spec))
+        self.__dict__["_mask_cache"] = cache[-self._MASK_CACHE:]
+
+    def block_prefix_counts(self, image_text_proprio_mask, action_mask):
+        """int32 prefix counts for the static hipGraph path, which supports the Pi0 block mask only."""
+        dev = self._dev()
+        itp, am = image_text_proprio_mask.to(dev), action_mask.to(dev)
+        L1 = itp.shape[2]
+        spec = self._mask_spec([itp, am], [torch.arange(L1, device=dev), torch.arange(L1, L1 + am.shape[2], device=dev)])
+        if not isinstance(spec, torch.Tensor):
+            raise ValueError("the hipGraph inference path needs the Pi0 block mask (pizero.py:271-306); "
+                             "call infer_action eagerly for a general mask")
+        return spec
 
     def _dev(self):
         return self._arena.data.device
@@ -369,6 +446,7 @@ class PiZero(nn.Module, NoSyncBase):
             raise RuntimeError("the native path computes in bf16: call model.to(torch.bfloat16)")
         x1 = actions.to(dev, torch.float32).contiguous()
         x0 = (torch.randn_like(x1) if noise is None else noise.to(dev, torch.float32)).contiguous()
+        cm = causal_mask.to(dev)
         tied = self._tied
         pos = {"vlm": vlm_position_ids.to(dev, torch.int64).contiguous()}
         if tied:
@@ -378,14 +456,30 @@ class PiZero(nn.Module, NoSyncBase):
             pos["action"] = action_position_ids.to(dev, torch.int64).contiguous()
         batch = dict(ids=input_ids.to(dev, torch.int64).contiguous(),
                      pix=pixel_values.to(dev, torch.bfloat16).contiguous(),
-                     cnt=self._prefix_counts(causal_mask.to(dev)), pos=pos,
+                     cnt=self._mask_spec([cm], [torch.arange(cm.shape[2], device=dev)]), pos=pos,
                      proprios=proprios.to(dev, torch.float32).contiguous(), actions=x1,
                      t=t.to(dev, torch.float32).contiguous(), x0=x0)
         anchor = next((self._param(n) for n in self._trainable_names()), None)
+        if anchor is not None and torch.is_grad_enabled():
+            self._check_ddp_wrapper()
         if anchor is None or not torch.is_grad_enabled():
             save = {}
             return self._engine().train_forward(save=save, **batch).view(())
         return _PiZeroLoss.apply(anchor, self, batch)
+
+    def _check_ddp_wrapper(self):
+        """torch DDP (train.py:121-126) cannot reduce this model's gradients: the native backward writes
+        them into the flat arena, so no per-parameter autograd hook ever fires and DDP would either skip
+        the all-reduce or fail on the next step.  Multi-rank training must use PiZeroDDP."""
+        import torch.distributed as dist
+
+        if (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+                and getattr(self, "_ddp_wrapper", None) is None):
+            raise RuntimeError(
+                "PiZero's native backward does not fire torch.nn.parallel.DistributedDataParallel's "
+                "per-parameter hooks: wrap the model with pizero_native.ddp.PiZeroDDP (same .module / "
+                "no_sync() / forward surface, bucketed RCCL all-reduce overlapped with the backward) "
+                "instead of DistributedDataParallel (reference train.py:121-126)")
 
     # ============================================================ inference ==
     def _kv_buffers(self, B):
@@ -408,9 +502,13 @@ class PiZero(nn.Module, NoSyncBase):
         if noise is None:
             noise = torch.randn(B, self.horizon_steps, self.action_dim, device=dev, dtype=torch.float32)
         k, v = self._kv_buffers(B)
+        itp, am = image_text_proprio_mask.to(dev), action_mask.to(dev)
+        L1 = itp.shape[2]
+        spec = self._mask_spec([itp, am], [torch.arange(L1, device=dev),
+                                           torch.arange(L1, L1 + am.shape[2], device=dev)])
         a = self._engine().infer_action(
             input_ids.to(dev, torch.int64).contiguous(), pixel_values.to(dev, torch.bfloat16).contiguous(),
-            self._prefix_counts(image_text_proprio_mask.to(dev)), vlm_position_ids.to(dev, torch.int64).contiguous(),
+            spec, vlm_position_ids.to(dev, torch.int64).contiguous(),
             proprio_position_ids.to(dev, torch.int64).contiguous(), action_position_ids.to(dev, torch.int64).contiguous(),
             proprios.to(dev, torch.float32).contiguous(), noise.to(dev, torch.float32).contiguous(), k, v,
             clip=clip and self.final_action_clip_value is not None)

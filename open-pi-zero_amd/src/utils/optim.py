@@ -71,10 +71,28 @@ class CosineAnnealingWarmupRestarts:
         return [g["lr"] for g in self.optimizer.param_groups]
 
     def state_dict(self):
-        return {k: v for k, v in self.__dict__.items() if k != "optimizer"}
+        """The reference's keys (utils/optim.py:56-60 dumps its __dict__ minus the optimizer):
+        first_cycle_steps, cycle_mult, base_max_lr, max_lr, min_lr, warmup_steps, gamma,
+        cur_cycle_steps, cycle, step_in_cycle, last_epoch, base_lrs."""
+        c, s, length = self._cycle_of(self.last_epoch) if self.last_epoch >= 0 else (0, -1, self.first_cycle_steps)
+        return {
+            "first_cycle_steps": self.first_cycle_steps, "cycle_mult": self.cycle_mult,
+            "base_max_lr": self.base_max_lr, "max_lr": self.base_max_lr * self.gamma ** c, "min_lr": self.min_lr,
+            "warmup_steps": self.warmup_steps, "gamma": self.gamma, "cur_cycle_steps": length, "cycle": c,
+            "step_in_cycle": s, "last_epoch": self.last_epoch,
+            "base_lrs": [self.min_lr] * len(self.optimizer.param_groups),
+        }
 
     def load_state_dict(self, state):
-        self.__dict__.update(state)
+        """Restores from this class's or the reference's state_dict (the closed-form schedule needs the
+        constants and last_epoch only) and writes the lr of that step into the optimizer."""
+        for k in ("first_cycle_steps", "warmup_steps", "last_epoch"):
+            if k in state:
+                setattr(self, k, int(state[k]))
+        for k in ("cycle_mult", "base_max_lr", "min_lr", "gamma"):
+            if k in state:
+                setattr(self, k, float(state[k]))
+        self._set(self.lr_at(self.last_epoch))
 
 
 def get_num_params_in_billions(optimizer):

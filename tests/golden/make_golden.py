@@ -13,8 +13,13 @@ What it does
     ``infer_action`` and ``infer_action_naive`` (noise patched) in fp32, and
     the same in bf16 (weights + inputs cast, CPU) to record the reference's
     own bf16-vs-fp32 deviation, which sets the GPU tolerances;
-  * writes tests/golden/<name>.npz (inputs are regenerated from seeds, only
+  * summarises EVERY parameter gradient with tests/golden/gradprobe.py (norm, ~4096
+    seeded samples incl. tile tails, 2 whole-tensor Rademacher projections) and
+    writes tests/golden/<name>.npz (inputs are regenerated from seeds, only
     outputs and small input tensors are stored).
+
+Fixtures: tiny (2+2 layers at full widths... see oracle TINY_DIMS, B=3), full (bridge
+dims, B=2, + actions), b16 (bridge dims, B=16 = config C2's micro-batch, chunked).
 
 Nothing under /root/reference is copied; this script only imports it.
 """
@@ -34,6 +39,7 @@ REF = "/root/reference"
 
 from oracle.pizero_oracle import FULL_DIMS, TINY_DIMS, param_shapes, synth_weights  # noqa: E402
 from oracle.synth import synth_inputs  # noqa: E402
+from tests.golden.gradprobe import N_SAMPLE, probe  # noqa: E402
 
 
 class AttrDict(dict):
@@ -152,7 +158,14 @@ def ref_cfg(d):
     return to_attr(c)
 
 
-def run_reference(d, bsz, ragged, dtype, W, inp, grad_names):
+def run_reference(d, bsz, ragged, dtype, W, inp, grad_names, chunk=None, infer=True, n_sample=N_SAMPLE):
+    """Reference forward/backward (+ infer_action) at batch ``bsz``.
+
+    ``chunk``: run the training pass over sub-batches of that size and accumulate
+    ``loss_c * (b_c / bsz)`` -- the batch loss is a mean over samples and nothing in the
+    forward crosses samples, so this is the same gradient (train.py:350-368 accumulates
+    micro-batches the same way); it keeps a B=16 full-size fp32 run inside host memory.
+    """
     from src.model.vla import pizero as pz
 
     cfg = ref_cfg(d)
@@ -166,22 +179,28 @@ def run_reference(d, bsz, ragged, dtype, W, inp, grad_names):
         assert tuple(v.shape) == tuple(param_shapes(d)[k]), k
     model.load_state_dict({k: W[k] for k in sd}, strict=True)
     model.to(dtype)
-    t = lambda a: torch.from_numpy(a).to(dtype)  # noqa: E731
-    ids = torch.from_numpy(inp["input_ids"])
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    ids_all = torch.from_numpy(inp["input_ids"])
     am = torch.from_numpy(inp["attention_mask"])
-    mask, vpos, ppos, apos = model.build_causal_mask_and_position_ids(am, dtype)
-    itp, amask = model.split_full_mask_into_submasks(mask)
-    x0 = t(inp["x0"])
-    noise = t(inp["noise"])
+    mask_all, vpos_all, ppos_all, apos_all = model.build_causal_mask_and_position_ids(am, dtype)
     orig_randn_like, orig_randn = torch.randn_like, torch.randn
     out = {}
+    chunk = chunk or bsz
     try:
-        torch.randn_like = lambda *a, **k: x0.clone()
-        loss = model(input_ids=ids, pixel_values=t(inp["pixel_values"]), causal_mask=mask,
-                     vlm_position_ids=vpos, proprio_position_ids=ppos, action_position_ids=apos,
-                     proprios=t(inp["proprios"]), actions=t(inp["actions"]), t=t(inp["t"]))
-        loss.backward()
-        out["loss"] = np.float64(loss.detach().float().item())
+        total = 0.0
+        for s0 in range(0, bsz, chunk):
+            sl = slice(s0, min(bsz, s0 + chunk))
+            bc = sl.stop - sl.start
+            x0 = t(inp["x0"][sl])
+            torch.randn_like = lambda *a, **k: x0.clone()
+            loss = model(input_ids=ids_all[sl], pixel_values=t(inp["pixel_values"][sl]), causal_mask=mask_all[sl],
+                         vlm_position_ids=vpos_all[sl], proprio_position_ids=ppos_all[sl],
+                         action_position_ids=apos_all[sl], proprios=t(inp["proprios"][sl]),
+                         actions=t(inp["actions"][sl]), t=t(inp["t"][sl]))
+            (loss * (bc / bsz)).backward()
+            total += loss.detach().double().item() * bc / bsz
+            print(f"  chunk {sl.start}:{sl.stop} loss {loss.item():.6f}", flush=True)
+        out["loss"] = np.float64(total)
         named = dict(model.named_parameters())
         for n in grad_names:
             p = named[n]
@@ -189,91 +208,90 @@ def run_reference(d, bsz, ragged, dtype, W, inp, grad_names):
             if g is None:
                 out["gradnorm/" + n] = np.float64(-1.0)
                 continue
-            gf = g.detach().double()
-            out["gradnorm/" + n] = np.float64(gf.norm().item())
-            out["gradhead/" + n] = gf.flatten()[:64].numpy().astype(np.float64)
+            pr = probe(n, g, n_sample)
+            out["gradnorm/" + n] = np.float64(pr["norm"])
+            out["gsamp/" + n] = pr["sample"].numpy()
+            out["gproj/" + n] = pr["proj"].numpy()
         model.zero_grad(set_to_none=True)
-        model.eval()
-        with torch.inference_mode():
-            torch.randn = lambda *a, **k: noise.clone()
-            cv = model.final_action_clip_value
-            model.final_action_clip_value = None
-            a1 = model.infer_action(input_ids=ids, pixel_values=t(inp["pixel_values"]),
-                                    image_text_proprio_mask=itp, action_mask=amask,
-                                    vlm_position_ids=vpos, proprio_position_ids=ppos,
-                                    action_position_ids=apos, proprios=t(inp["proprios"]))
-            a2 = model.infer_action_naive(input_ids=ids, pixel_values=t(inp["pixel_values"]),
-                                          causal_mask=mask, vlm_position_ids=vpos,
-                                          proprio_position_ids=ppos, action_position_ids=apos,
-                                          proprios=t(inp["proprios"]))
-            model.final_action_clip_value = cv
-            a3 = model.infer_action(input_ids=ids, pixel_values=t(inp["pixel_values"]),
-                                    image_text_proprio_mask=itp, action_mask=amask,
-                                    vlm_position_ids=vpos, proprio_position_ids=ppos,
-                                    action_position_ids=apos, proprios=t(inp["proprios"]))
-        out["actions_unclipped"] = a1.float().numpy()
-        out["actions_naive_unclipped"] = a2.float().numpy()
-        out["actions_clipped"] = a3.float().numpy()
-        out["mask"] = mask[:, 0].float().numpy() if d is TINY_DIMS else np.zeros(1)
+        if infer:
+            ids, itp_amask = ids_all, model.split_full_mask_into_submasks(mask_all)
+            itp, amask = itp_amask
+            vpos, ppos, apos, mask = vpos_all, ppos_all, apos_all, mask_all
+            noise = t(inp["noise"])
+            model.eval()
+            with torch.inference_mode():
+                torch.randn = lambda *a, **k: noise.clone()
+                cv = model.final_action_clip_value
+                model.final_action_clip_value = None
+                a1 = model.infer_action(input_ids=ids, pixel_values=t(inp["pixel_values"]),
+                                        image_text_proprio_mask=itp, action_mask=amask,
+                                        vlm_position_ids=vpos, proprio_position_ids=ppos,
+                                        action_position_ids=apos, proprios=t(inp["proprios"]))
+                a2 = model.infer_action_naive(input_ids=ids, pixel_values=t(inp["pixel_values"]),
+                                              causal_mask=mask, vlm_position_ids=vpos,
+                                              proprio_position_ids=ppos, action_position_ids=apos,
+                                              proprios=t(inp["proprios"]))
+                model.final_action_clip_value = cv
+                a3 = model.infer_action(input_ids=ids, pixel_values=t(inp["pixel_values"]),
+                                        image_text_proprio_mask=itp, action_mask=amask,
+                                        vlm_position_ids=vpos, proprio_position_ids=ppos,
+                                        action_position_ids=apos, proprios=t(inp["proprios"]))
+            out["actions_unclipped"] = a1.float().numpy()
+            out["actions_naive_unclipped"] = a2.float().numpy()
+            out["actions_clipped"] = a3.float().numpy()
+        out["mask"] = mask_all[:, 0].float().numpy() if d is TINY_DIMS else np.zeros(1)
     finally:
         torch.randn_like, torch.randn = orig_randn_like, orig_randn
     return out
 
 
-def grad_name_subset(d):
-    """A representative set of trained parameters (every kind, first/last layers)."""
-    names = []
-    vt = "vision_tower.vision_model."
-    Lv, Lj = d["vis_layers"] - 1, d["n_layers"] - 1
-    names += [vt + "embeddings.patch_embedding.weight", vt + "embeddings.patch_embedding.bias",
-              vt + "embeddings.position_embedding.weight", vt + "post_layernorm.weight"]
-    for i in sorted({0, Lv}):
-        p = f"{vt}encoder.layers.{i}."
-        names += [p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight",
-                  p + "self_attn.v_proj.weight", p + "self_attn.out_proj.weight",
-                  p + "self_attn.q_proj.bias", p + "layer_norm1.weight", p + "layer_norm2.bias",
-                  p + "mlp.fc1.weight", p + "mlp.fc1.bias", p + "mlp.fc2.weight"]
-    names += ["multi_modal_projector.linear.weight", "multi_modal_projector.linear.bias"]
-    for mix in ("vlm", "action"):
-        for i in sorted({0, Lj // 2, Lj}):
-            p = f"joint_model.mixtures.{mix}.layers.{i}."
-            names += [p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight",
-                      p + "self_attn.o_proj.weight", p + "mlp.gate_proj.weight",
-                      p + "mlp.up_proj.weight", p + "mlp.down_proj.weight",
-                      p + "input_layernorm.weight", p + "post_attention_layernorm.weight"]
-            if not (mix == "vlm" and i == Lj):
-                names += [p + "self_attn.v_proj.weight"]
-    names += ["joint_model.mixtures.action.norm.weight"]
-    names += ["action_encoder.linear_1.weight", "action_encoder.linear_2.weight",
-              "action_encoder.linear_3.bias", "proprio_encoder.weight", "proprio_encoder.bias",
-              "action_decoder.weight", "action_decoder.bias"]
-    # mixtures.proprio.* alias mixtures.action.* after the tie; named_parameters
-    # reports the shared tensor once, under the first registered name (proprio)
-    return [n.replace(".mixtures.action.layers", ".mixtures.proprio.layers")
-            .replace(".mixtures.action.norm", ".mixtures.proprio.norm") for n in names]
+def all_grad_names(d):
+    """Every parameter name the reference's named_parameters() reports (after the tie the
+    shared expert tensors appear once, under mixtures.proprio.*, registered first)."""
+    from src.model.vla import pizero as pz
+
+    with torch.device("meta"):
+        model = pz.PiZero(ref_cfg(d))
+    model.tie_action_proprio_weights()
+    model.freeze_unused_weights()
+    return [n for n, _ in model.named_parameters()]
 
 
-def make(name, d, bsz, ragged):
+def make(name, d, bsz, ragged, chunk=None, infer=True, n_sample=N_SAMPLE, tags=("fp32", "bf16")):
     install_stubs()
     if REF not in sys.path:
         sys.path.insert(0, REF)
     torch.set_num_threads(os.cpu_count() or 8)
     W = synth_weights(d, seed=0)
     inp = synth_inputs(d, bsz, seed=0, ragged=ragged)
-    gnames = grad_name_subset(d)
+    gnames = all_grad_names(d)
     res = {}
-    for tag, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+    for tag in tags:
+        dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[tag]
         print(f"[{name}] reference run {tag} ...", flush=True)
-        o = run_reference(d, bsz, ragged, dt, W, inp, gnames)
+        o = run_reference(d, bsz, ragged, dt, W, inp, gnames, chunk=chunk, infer=infer, n_sample=n_sample)
         for k, v in o.items():
             res[f"{tag}/{k}"] = v
+        del o
+    if "bf16" in tags:
+        # the reference's own bf16-vs-fp32 deviation per tensor (sets the GPU tolerances)
+        for n in gnames:
+            a, b = res.get(f"bf16/gsamp/{n}"), res.get(f"fp32/gsamp/{n}")
+            if a is None or b is None:
+                continue
+            a64, b64 = a.astype(np.float64), b.astype(np.float64)
+            nb = np.linalg.norm(b64)
+            res[f"bf16/grel/{n}"] = np.float64(np.linalg.norm(a64 - b64) / max(nb, 1e-30))
+            res[f"bf16/gcos/{n}"] = np.float64(a64 @ b64 / max(np.linalg.norm(a64) * nb, 1e-30))
+            del res[f"bf16/gsamp/{n}"]
     for k in ("input_ids", "attention_mask", "t"):
         res["in/" + k] = inp[k]
     res["grad_names"] = np.array(gnames)
     res["bsz"] = np.int64(bsz)
+    res["n_sample"] = np.int64(n_sample)
     path = os.path.join(ROOT, "tests", "golden", f"{name}.npz")
     np.savez_compressed(path, **res)
-    print("wrote", path, "loss fp32", res["fp32/loss"], "bf16", res["bf16/loss"])
+    print("wrote", path, "loss fp32", res.get("fp32/loss"), "bf16", res.get("bf16/loss"))
 
 
 if __name__ == "__main__":
@@ -282,6 +300,9 @@ if __name__ == "__main__":
         make("tiny", TINY_DIMS, 3, ragged=True)
     if which in ("full", "all"):
         make("full", FULL_DIMS, 2, ragged=True)
+    if which in ("b16", "all"):
+        # config C2's micro-batch (bridge, B=16), fp32 + bf16, accumulated over chunks of 2
+        make("b16", FULL_DIMS, 16, ragged=True, chunk=2, infer=False, n_sample=2048)
 
 
 def make_lr():
@@ -290,7 +311,7 @@ def make_lr():
         sys.path.insert(0, REF)
     from src.utils.optim import CosineAnnealingWarmupRestarts
 
-    out = {}
+    out, states = {}, {}
     for name, (first, mult, mx, mn, warm, gamma) in {
         "bridge": (10000000, 1.0, 5e-5, 1e-8, 200, 1.0),
         "restarts": (50, 1.0, 1e-3, 1e-6, 10, 0.5),
@@ -301,14 +322,69 @@ def make_lr():
         s = CosineAnnealingWarmupRestarts(opt, first_cycle_steps=first, cycle_mult=mult, max_lr=mx, min_lr=mn,
                                           warmup_steps=warm, gamma=gamma)
         lrs = [opt.param_groups[0]["lr"]]
-        for _ in range(300):
+        for i in range(300):
             s.step()
             lrs.append(opt.param_groups[0]["lr"])
+            if i + 1 == 137:  # the reference's own state_dict mid-schedule (resume format, optim.py:56-60)
+                states[name] = {k: v for k, v in s.state_dict().items()}
         out[name] = np.array(lrs, dtype=np.float64)
         out[name + "_args"] = np.array([first, mult, mx, mn, warm, gamma], dtype=np.float64)
     np.savez_compressed(os.path.join(ROOT, "tests", "golden", "lr_schedule.npz"), **out)
+    import json
+
+    with open(os.path.join(ROOT, "tests", "golden", "lr_state.json"), "w") as f:
+        json.dump(states, f, indent=1, sort_keys=True)
     print("wrote lr_schedule.npz")
+
+
+def make_fm_time():
+    """Seeded draws of the reference's TrainAgent.sample_fm_time (train.py:216-247), beta and uniform."""
+    import types as _t
+
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_ref_train", os.path.join(REF, "src", "agent", "train.py"))
+    src_txt = open(spec.origin).read()
+    # compile only the sample_fm_time method (the module imports tensorflow/wandb, absent here)
+    import ast
+
+    tree = ast.parse(src_txt)
+    fn = next(n for c in tree.body if isinstance(c, ast.ClassDef) for n in c.body
+              if isinstance(n, ast.FunctionDef) and n.name == "sample_fm_time")
+    mod = ast.Module(body=[fn], type_ignores=[])
+    ns = {"torch": torch}
+    exec(compile(mod, "reference:train.py:sample_fm_time", "exec"), ns)
+    out = {}
+    for mode in ("beta", "uniform"):
+        obj = _t.SimpleNamespace(flow_sampling=mode, flow_t_max=1 - 0.001,
+                                 flow_beta_dist=torch.distributions.Beta(1.5, 1))
+        torch.manual_seed(1234)
+        out[mode] = np.concatenate([ns["sample_fm_time"](obj, b).numpy() for b in (16, 7, 64)])
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "fm_time.npz"), **out)
+    print("wrote fm_time.npz")
+
+
+def make_time_embed():
+    """The reference SinusoidalPosEmb (vla/modules.py:9-22) in fp32 and in bf16 (t in bf16 as in bf16
+    training, train.py:311: arange and every op in bf16) for the bridge width / both max periods."""
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from src.model.vla.modules import SinusoidalPosEmb
+
+    t = torch.linspace(0.0, 0.999, 37)
+    out = {"t": t.numpy()}
+    for P in (100.0, 10000.0):
+        m = SinusoidalPosEmb(1024, P)
+        out[f"fp32_{int(P)}"] = m(t).numpy()
+        out[f"bf16_{int(P)}"] = m(t.to(torch.bfloat16)).float().numpy()
+        out[f"t_bf16_{int(P)}"] = t.to(torch.bfloat16).float().numpy()
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "time_embed.npz"), **out)
+    print("wrote time_embed.npz")
 
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lr":
     make_lr()
+    make_fm_time()
+    make_time_embed()

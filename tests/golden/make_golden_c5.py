@@ -9,9 +9,10 @@ level: the reference's own ``JointModel`` (joint_model.py:307-383,
 bridge.yaml joint config at full Gemma-2B / action-expert dims, proprio mixture tied to action
 weights as pizero.py:262-264 does) runs forward + backward on generator-defined embeddings,
 with the reference's own block mask / positions (pizero.py:271-324, 8 pad text tokens).  Loss =
-sum(action_hidden * R) for a generator-defined R.  Stored: the action hidden states, the input
-embedding gradients (norm + first 64 values) and ~30 parameter gradients (norm + first 64), in
-fp32 and in bf16 (the reference's own bf16-vs-fp32 deviation sets the GPU tolerance).
+sum(action_hidden * R) for a generator-defined R.  Stored: the action hidden states and, for the
+input-embedding gradients and EVERY JointModel parameter gradient, the tests/golden/gradprobe.py
+summary (norm, seeded samples incl. tile tails, whole-tensor projections) in fp32, plus the
+reference's own bf16-vs-fp32 deviation (sets the GPU tolerance).
 Inputs are regenerated from seeds on both sides (oracle/synth.py; pz_fill_uniform on device).
 Nothing under /root/reference is copied; this script only imports it.
 """
@@ -31,6 +32,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 REF = "/root/reference"
 
+from gradprobe import probe  # noqa: E402
 from make_golden import install_stubs, ref_cfg  # noqa: E402
 from oracle.pizero_oracle import FULL_DIMS, synth_weights  # noqa: E402
 from oracle.synth import synth_tensor  # noqa: E402
@@ -45,17 +47,9 @@ C5_INPUTS = {  # name -> (shape, scale) of the generator-defined inputs (offset 
 }
 
 
-def c5_grad_names():
-    names = []
-    for mix in ("vlm", "action"):
-        for i in (0, 9, 17):
-            p = f"mixtures.{mix}.layers.{i}."
-            names += [p + "self_attn.q_proj.weight", p + "self_attn.k_proj.weight", p + "self_attn.o_proj.weight",
-                      p + "mlp.gate_proj.weight", p + "mlp.down_proj.weight", p + "input_layernorm.weight"]
-            if not (mix == "vlm" and i == 17):
-                names += [p + "self_attn.v_proj.weight", p + "post_attention_layernorm.weight"]
-    names += ["mixtures.action.norm.weight"]
-    return names
+def c5_grad_names(joint):
+    """Every JointModel parameter (after the tie the shared expert tensors appear once, as proprio)."""
+    return [n for n, _ in joint.named_parameters()]
 
 
 def run(dtype):
@@ -87,18 +81,22 @@ def run(dtype):
     loss.backward()
     res = {"action_hidden": ya.detach().float().numpy()}
     for n, lf in leaves.items():
-        g = lf.grad.detach().double()
-        res[f"dembeds/{n}/norm"] = np.float64(g.norm().item())
-        res[f"dembeds/{n}/head"] = g.flatten()[:64].numpy()
+        pr = probe("dembeds." + n, lf.grad)
+        res[f"gradnorm/dembeds.{n}"] = np.float64(pr["norm"])
+        res[f"gsamp/dembeds.{n}"] = pr["sample"].numpy()
+        res[f"gproj/dembeds.{n}"] = pr["proj"].numpy()
+    names = c5_grad_names(joint)
     named = dict(joint.named_parameters())
-    for n in c5_grad_names():
-        p = named.get(n) if n in named else named.get(n.replace("mixtures.action.", "mixtures.proprio."))
-        if p is None or p.grad is None:
+    for n in names:
+        p = named[n]
+        if p.grad is None:
             res[f"gradnorm/{n}"] = np.float64(-1.0)
             continue
-        g = p.grad.detach().double()
-        res[f"gradnorm/{n}"] = np.float64(g.norm().item())
-        res[f"gradhead/{n}"] = g.flatten()[:64].numpy()
+        pr = probe(n, p.grad)
+        res[f"gradnorm/{n}"] = np.float64(pr["norm"])
+        res[f"gsamp/{n}"] = pr["sample"].numpy()
+        res[f"gproj/{n}"] = pr["proj"].numpy()
+    res["_names"] = names
     return res
 
 
@@ -106,13 +104,24 @@ def main():
     install_stubs()
     sys.path.insert(0, REF)
     torch.set_num_threads(os.cpu_count() or 8)
-    out = {"cnt": np.int64(C5_CNT), "grad_names": np.array(c5_grad_names())}
+    out = {"cnt": np.int64(C5_CNT)}
     for tag, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
         t0 = time.time()
         r = run(dt)
         print(f"{tag}: {time.time() - t0:.1f}s", flush=True)
+        names = r.pop("_names")
+        out["grad_names"] = np.array(["dembeds." + n for n in ("vlm", "proprio", "action")] + names)
         for k, v in r.items():
             out[f"{tag}/{k}"] = v
+    for n in [str(x) for x in out["grad_names"]]:  # the reference's own bf16-vs-fp32 deviation
+        a, b = out.get(f"bf16/gsamp/{n}"), out.get(f"fp32/gsamp/{n}")
+        if a is None or b is None:
+            continue
+        a64, b64 = a.astype(np.float64), b.astype(np.float64)
+        nb = np.linalg.norm(b64)
+        out[f"bf16/grel/{n}"] = np.float64(np.linalg.norm(a64 - b64) / max(nb, 1e-30))
+        del out[f"bf16/gsamp/{n}"]
+    out["n_sample"] = np.int64(4096)
     path = os.path.join(ROOT, "tests", "golden", "c5.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")

@@ -34,7 +34,9 @@ def frozen(d, name):
     return False
 
 
-def oracle_run(d, bsz, ragged, want_grads=True):
+def oracle_run(d, bsz, ragged, want_grads=True, mask_fn=None):
+    """fp32 oracle loss (+ grads) and action chunks on the fixture inputs; ``mask_fn`` edits the
+    additive [B,1,L,L] mask before use (general-mask tests)."""
     W = O.synth_weights(d, seed=0)
     leaves = {}
     for k, v in W.items():
@@ -43,10 +45,13 @@ def oracle_run(d, bsz, ragged, want_grads=True):
     inp = synth_inputs(d, bsz, seed=0, ragged=ragged)
     ids = torch.from_numpy(inp["input_ids"])
     mask, vpos, ppos, apos = O.build_mask_and_positions(d, torch.from_numpy(inp["attention_mask"]))
+    if mask_fn is not None:
+        mask = mask_fn(mask)
+    out_mask = mask
     T = lambda a: torch.from_numpy(a)  # noqa: E731
     loss = O.pizero_loss(W, d, ids, T(inp["pixel_values"]), mask, vpos, ppos, apos,
                          T(inp["proprios"]), T(inp["actions"]), T(inp["t"]), T(inp["x0"]))
-    out = {"loss": loss.item()}
+    out = {"loss": loss.item(), "mask": out_mask}
     if want_grads:
         loss.backward()
         out["grads"] = {k: (None if v.grad is None else v.grad.detach().clone()) for k, v in W.items()}

@@ -26,7 +26,11 @@ def test_library_exports_all_declared_symbols():
     for s in declared_symbols():
         assert hasattr(L, s), s
         assert s in SIGNATURES, f"{s} has no ctypes signature"
-    assert L.pz_abi_version() == 6
+    from pizero_native._lib import ABI_VERSION
+
+    hdr = open(os.path.join(ROOT, "include", "pz_abi.h")).read()
+    assert f"#define PZ_ABI_VERSION {ABI_VERSION}" in hdr
+    assert L.pz_abi_version() == ABI_VERSION
 
 
 def test_error_path_without_gpu():

@@ -53,3 +53,51 @@ def test_eval_agent_graph_matches_eager():
     a_eager = ag.infer_chunk(b["input_ids"], b["attention_mask"], pix, b["proprio"], noise=noise)
     assert a_graph.shape == (2, 4, 7)
     assert torch.allclose(a_graph.float(), a_eager.float(), atol=1e-2)
+
+
+def _one_update(agent, batch, seed):
+    from pizero_native.optim import clip_grad_norm_
+
+    torch.manual_seed(seed)
+    inputs = agent.preprocess_batch(batch)
+    loss = agent.model(**inputs, noise=torch.zeros(inputs["actions"].shape, device="cuda"))
+    loss.backward()
+    clip_grad_norm_(agent.optimizers, agent.max_grad_norm)
+    for o in agent.optimizers:
+        o.step()
+        o.zero_grad(set_to_none=True)
+    agent.action_lr_scheduler.step()
+    agent.vlm_lr_scheduler.step()
+
+
+def test_save_resume_roundtrip(tmp_path):
+    """train.py:497-560: save_training -> TrainAgent(resume_checkpoint_path) restores weights, counters,
+    both optimizers' moments/steps and both schedulers; the next update is bitwise identical."""
+    from src.agent.train import SyntheticBridgeDataset, TrainAgent
+
+    c = _cfg()
+    c.update(dict(log_dir=str(tmp_path), n_updates=2, save_model_freq=2))
+    a = TrainAgent(c).run()
+    path = tmp_path / "checkpoint" / "step2.pt"
+    assert path.exists()
+    c2 = _cfg()
+    c2.update(dict(resume_checkpoint_path=str(path)))
+    b = TrainAgent(c2)
+    assert (b.cnt_update, b.cnt_batch) == (2, a.cnt_batch - 1)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)
+    for oa, ob in ((a.action_optimizer, b.action_optimizer), (a.vlm_optimizer, b.vlm_optimizer)):
+        da, db = oa.state_dict(), ob.state_dict()
+        assert da["param_groups"][0]["step"] == db["param_groups"][0]["step"] == 2
+        assert da["param_groups"][0]["lr"] == db["param_groups"][0]["lr"]
+        assert set(da["state"]) == set(db["state"]) and da["state"]
+        for i in da["state"]:  # 8-bit state by default: codes, absmax, qmaps (fp32 for small tensors)
+            for k, v in da["state"][i].items():
+                if isinstance(v, torch.Tensor):
+                    assert torch.equal(v, db["state"][i][k]), (i, k)
+    assert a.action_lr_scheduler.last_epoch == b.action_lr_scheduler.last_epoch == 1  # 2 steps from -1
+    batch = next(iter(SyntheticBridgeDataset(c, 4, seed=9)))
+    _one_update(a, batch, 5)
+    _one_update(b, batch, 5)
+    sa, sb = a.model.state_dict(), b.model.state_dict()
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)

@@ -7,17 +7,20 @@ full Gemma-2B / action-expert dims (proprio tied to action) on generator-defined
 the reference block mask (8 pad text tokens) and loss = sum(action_hidden * R), in fp32 and bf16.
 Here the native engine runs the same JointModel forward + backward (``Engine.joint_train``) on the
 same embeddings (pz_fill_uniform reproduces oracle/synth.py bit-exactly) in bf16 on the GPU.
-Tolerance = max(3x the reference's own bf16-vs-fp32 deviation, a floor): action hidden rel-L2
-<= 3e-2; gradient norms rel <= max(3*dev, 0.05), gradient-head cosine >= 0.97.
+Tolerance: action hidden rel-L2 <= max(3x the reference's own bf16-vs-fp32 deviation, 3e-2); the
+input-embedding gradients and EVERY JointModel parameter gradient pass the probe gate of
+tests/pizero_gpu_helpers.py (sample rel-L2 <= 8 %, cosine >= 0.995, whole-tensor projections).
 Precision: bf16 (the fp8 variant of C5 is not built).  Both joint-attention kernels are checked.
 """
+
+import types
 
 import numpy as np
 import pytest
 import torch
 
 from tests.oracle_helpers import O, load_golden
-from tests.pizero_gpu_helpers import build_gpu_model
+from tests.pizero_gpu_helpers import build_gpu_model, check_grads_probe
 
 pytestmark = pytest.mark.gpu
 
@@ -72,40 +75,12 @@ def test_c5_joint_model_forward_backward(c5, joint_attn):
     mine = out.float().cpu().numpy()
     tol = max(3 * _rel(refb, ref), 3e-2)
     assert _rel(mine, ref) <= tol, (_rel(mine, ref), _rel(refb, ref))
-    bad = []
+    params = {n: p for n, p in m.named_parameters()}
     for n in ("vlm", "proprio", "action"):
-        gd = demb[n].double()
-        r, rb = float(g[f"fp32/dembeds/{n}/norm"]), float(g[f"bf16/dembeds/{n}/norm"])
-        t = max(3 * abs(rb - r) / r, 0.05)
-        head = gd.flatten()[:64].cpu().numpy()
-        rh = g[f"fp32/dembeds/{n}/head"]
-        cos = float(np.dot(head, rh) / (np.linalg.norm(head) * np.linalg.norm(rh) + 1e-30))
-        if abs(gd.norm().item() - r) > t * r or cos < 0.97:
-            bad.append(("dembeds/" + n, gd.norm().item(), r, rb, cos))
-    params = dict(m.named_parameters())
-    for n in [str(x) for x in g["grad_names"]]:
-        r = float(g[f"fp32/gradnorm/{n}"])
-        full = "joint_model." + n
-        p = params.get(full)
-        if p is None:
-            p = params.get(full.replace("mixtures.action.", "mixtures.proprio."))
-        if r < 0:
-            assert p is None or p.grad is None or not p.requires_grad, n
-            continue
-        if r == 0 and (p is None or p.grad is None or not p.requires_grad):
-            continue  # reachable but gradient exactly 0 in the reference (frozen/unused here)
-        if p is None or p.grad is None:
-            bad.append((n, None, r))
-            continue
-        gg = p.grad.double()
-        mine_n = gg.norm().item()
-        rb = float(g[f"bf16/gradnorm/{n}"])
-        t = max(3 * abs(rb - r) / max(r, 1e-30), 0.05)
-        head = gg.flatten()[:64].cpu().numpy()
-        rh = g[f"fp32/gradhead/{n}"]
-        cos = float(np.dot(head, rh) / (np.linalg.norm(head) * np.linalg.norm(rh) + 1e-30))
-        ok = (r == 0 and mine_n == 0) or (abs(mine_n - r) <= t * r and
-                                         (np.linalg.norm(rh) < 1e-12 * r or cos >= 0.97))
-        if not ok:
-            bad.append((n, mine_n, r, rb, cos))
-    assert not bad, "\n".join(map(str, bad))
+        params["dembeds." + n] = types.SimpleNamespace(grad=demb[n], requires_grad=True)
+
+    def name_map(n):
+        return n if n.startswith("dembeds.") else "joint_model." + n
+
+    # (the last vlm layer's v_proj is frozen by freeze_unused_weights, pizero.py:224-256: skipped)
+    check_grads_probe(g, params, name_map=name_map, label=f"C5 {joint_attn}", skip_frozen=True)

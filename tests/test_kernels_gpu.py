@@ -524,9 +524,9 @@ def test_adamw_matches_torch():
         opt.step()
         ops.adamw(p, g, m, v, 1e-2, 0.9, 0.999, 1e-8, 0.01, 1 - 0.9 ** step, 1 - 0.999 ** step)
     close(p, pr.detach(), atol=1e-2)
-    acc = torch.zeros(1, device=dev)
-    ops.sumsq(g, acc)
-    assert abs(acc.item() - (g.float() ** 2).sum().item()) < 1e-3 * acc.item()
+    parts = torch.empty(ops.PZ_SUMSQ_PARTS, device=dev)
+    ops.sumsq(g, parts)
+    assert abs(parts.sum().item() - (g.float() ** 2).sum().item()) < 1e-3 * parts.sum().item()
 
 
 def test_wgrad_split_k_matches_single_pass():
@@ -541,3 +541,28 @@ def test_wgrad_split_k_matches_single_pass():
     close(dW, ref, atol=0.05 * math.sqrt(M) / 16)
     ops.linear_wgrad(dy, x, dW, beta=True)
     close(dW, 2 * ref, atol=0.1 * math.sqrt(M) / 16)
+
+
+def test_time_embed_modes_match_reference():
+    """pz_time_embed mode 0 = the reference SinusoidalPosEmb in fp32; mode 1 = the reference's bf16
+    arithmetic (bf16 arange rounds odd indices above 256, every op rounded; vla/modules.py:15-22)
+    -- both against the reference's own outputs (tests/golden/time_embed.npz)."""
+    from pizero_native import ops
+    from tests.oracle_helpers import load_golden
+
+    g = load_golden("time_embed")
+    for P in (100, 10000):
+        for mode, key, tkey in ((0, f"fp32_{P}", "t"), (1, f"bf16_{P}", f"t_bf16_{P}")):
+            t = torch.from_numpy(g[tkey]).to(dev)
+            out = torch.empty(t.numel(), 1024, device=dev, dtype=torch.bfloat16)
+            ops.time_embed(t, out, float(P), ref_bf16=bool(mode))
+            err = (out.float().cpu() - torch.from_numpy(g[key])).abs()
+            assert err.max().item() <= 8e-3 and err.mean().item() <= 6e-4, (P, mode, err.max().item(), err.mean().item())
+        # mode 1 tracks the bf16 reference more closely than the fp32 kernel does
+        t = torch.from_numpy(g[f"t_bf16_{P}"]).to(dev)
+        outs = []
+        for mode in (0, 1):
+            o = torch.empty(t.numel(), 1024, device=dev, dtype=torch.bfloat16)
+            ops.time_embed(t, o, float(P), ref_bf16=bool(mode))
+            outs.append((o.float().cpu() - torch.from_numpy(g[f"bf16_{P}"])).abs().mean().item())
+        assert outs[1] < outs[0], outs

@@ -87,3 +87,40 @@ def test_dtype_conversion_keeps_arena_binding(tiny_model):
 def test_cpu_execution_fails_loudly(tiny_model):
     with pytest.raises(RuntimeError, match="MI355X HIP path only"):
         tiny_model._engine()
+
+
+def test_mask_contract_block_vs_general(tiny_model):
+    """the reference builder's mask -> per-sample prefix counts (block kernels); any other
+    additive mask -> GeneralMask (GEMM + additive softmax path).  Validated once per tensor."""
+    from pizero_native.engine import GeneralMask
+
+    am = torch.tensor([[1] * 10 + [0] * 14, [1] * 7 + [0] * 17], dtype=torch.int64)
+    for dt in (torch.bfloat16, torch.float32):
+        m, *_ = tiny_model.build_causal_mask_and_position_ids(am, dt)
+        L = m.shape[-1]
+        spec = tiny_model._mask_spec([m], [torch.arange(L)])
+        assert isinstance(spec, torch.Tensor) and spec.tolist() == [10, 7]
+        assert tiny_model._mask_spec([m], [torch.arange(L)]) is spec  # cached by identity + version
+        itp, amask = tiny_model.split_full_mask_into_submasks(m)
+        L1 = itp.shape[-1]
+        s2 = tiny_model._mask_spec([itp, amask], [torch.arange(L1), torch.arange(L1, L1 + amask.shape[2])])
+        assert isinstance(s2, torch.Tensor) and s2.tolist() == [10, 7]
+    m, *_ = tiny_model.build_causal_mask_and_position_ids(am, torch.bfloat16)
+    L = m.shape[-1]
+    # action rows blind to the proprio token: not the block pattern
+    m2 = m.clone()
+    m2[:, :, -4:, 24] = torch.finfo(torch.bfloat16).min
+    assert isinstance(tiny_model._mask_spec([m2], [torch.arange(L)]), GeneralMask)
+    # in-place edit of a validated tensor bumps its version -> re-validated
+    spec = tiny_model._mask_spec([m], [torch.arange(L)])
+    assert isinstance(spec, torch.Tensor)
+    m[:, :, 0, 0] = -2.0
+    g = tiny_model._mask_spec([m], [torch.arange(L)])
+    assert isinstance(g, GeneralMask) and g.full.dtype == torch.float32 and g.full.shape == (2, L, L)
+    # fp16-style "-65504" masking does not absorb the logits like finfo.min: general path
+    m3, *_ = tiny_model.build_causal_mask_and_position_ids(am, torch.float32)
+    m3 = torch.where(m3 < 0, torch.full_like(m3, -65504.0), m3)
+    assert isinstance(tiny_model._mask_spec([m3], [torch.arange(L)]), GeneralMask)
+    with pytest.raises(ValueError, match="block mask"):
+        itp, amask = tiny_model.split_full_mask_into_submasks(m2)
+        tiny_model.block_prefix_counts(itp, amask)

@@ -43,6 +43,9 @@ def test_loss(tiny):
 
 
 def test_grads(tiny):
+    """every parameter: the oracle's gradient probe (norm, seeded samples, projections) = the reference's"""
+    from tests.golden.gradprobe import compare, probe
+
     g, out, _ = tiny
     names = [str(n) for n in g["grad_names"]]
     assert len(names) > 30
@@ -53,9 +56,13 @@ def test_grads(tiny):
             assert mine is None, n
             continue
         assert mine is not None, n
-        assert abs(mine.double().norm().item() - ref_norm) <= 1e-4 * ref_norm + 1e-9, n
-        head = mine.double().flatten()[:64].numpy()
-        np.testing.assert_allclose(head, g["fp32/gradhead/" + n], rtol=1e-3, atol=1e-6 * max(ref_norm, 1e-3))
+        if ref_norm == 0.0:
+            assert float(mine.abs().max()) == 0.0, n
+            continue
+        ref = {"norm": ref_norm, "sample": torch.from_numpy(g["fp32/gsamp/" + n]),
+               "proj": torch.from_numpy(g["fp32/gproj/" + n])}
+        c = compare(probe(n, mine, int(g["n_sample"])), ref)
+        assert c["rel"] <= 1e-4 and c["norm_rel"] <= 1e-4 and c["proj_err"] <= 1e-4, (n, c)
 
 
 def test_actions_cached_and_naive(tiny):

@@ -1,13 +1,22 @@
 """End-to-end parity of the native MI355X PiZero against the reference fixtures.
 
-The fixtures (tests/golden/{tiny,full}.npz) hold the REFERENCE's own fp32
-outputs (loss, gradient norms + first 64 gradient values of ~70 parameters,
-cached and naive action chunks) and its bf16 outputs for the same inputs.
-The HIP path runs in bf16 (fp32 accumulation); it is compared with the fp32
-reference with a tolerance of max(3x the reference's own bf16-vs-fp32
-deviation, a floor):  loss rel <= max(3*dev, 1e-2); gradient norm rel <=
-max(3*dev, 0.05) and gradient-head cosine >= 0.97 (0.9 for params whose head
-is tiny); actions mean|d| <= max(3*dev, 5e-3), max|d| <= max(3*dev, 3e-2).
+The fixtures (tests/golden/{tiny,full,b16}.npz, written by tests/golden/make_golden.py, which
+imports and runs the REFERENCE) hold its fp32 loss, cached and naive action chunks and, for EVERY
+parameter, a gradient summary (tests/golden/gradprobe.py: norm, ~4096 seeded samples incl. the
+last row / last column tile tails, 2 whole-tensor Rademacher projections), plus the reference's own
+bf16-vs-fp32 deviation for the same inputs.
+
+The HIP path runs in bf16 (fp32 accumulation) and is held to SURVEY 8(c)'s gate against the fp32
+reference:
+  * loss:    |d| <= max(3x the reference's own bf16 deviation, 1e-2 rel);
+  * grads:   per tensor sample rel-L2 <= 8 % and cosine >= 0.995, |norm| rel <= 8 %, projections
+             within 5 x 8 % of |g| -- widened to 2x the reference's own bf16 deviation for the few
+             tensors where that is larger (pizero_gpu_helpers.grad_tolerance);
+  * actions: mean|d| <= max(3x dev, 5e-3), max|d| <= max(3x dev, 3e-2).
+Shapes: tiny (B=3), bridge B=2 (full), bridge B=16 (config C2's micro-batch) and the benched
+micro-batch 64 (the 16 fixture samples x 4: the batch mean makes its loss and gradients equal to
+the B=16 fixture's, so the bench's M = 17664-row GEMM instantiations and split tails are checked
+end to end).
 """
 
 import numpy as np
@@ -15,7 +24,7 @@ import pytest
 import torch
 
 from tests.oracle_helpers import O, load_golden
-from tests.pizero_gpu_helpers import build_gpu_model, gpu_inputs, run_infer, run_loss
+from tests.pizero_gpu_helpers import build_gpu_model, check_grads_probe, gpu_inputs, run_infer, run_loss
 
 pytestmark = pytest.mark.gpu
 
@@ -32,30 +41,8 @@ def _check_loss(g, loss):
     assert abs(loss - ref) <= tol, (loss, ref, rb)
 
 
-def _check_grads(g, m):
-    params = dict(m.named_parameters())
-    names = [str(n) for n in g["grad_names"]]
-    bad = []
-    for n in names:
-        ref = float(g["fp32/gradnorm/" + n])
-        p = params[n]
-        if ref < 0:
-            assert p.grad is None or not p.requires_grad, n
-            continue
-        assert p.grad is not None, n
-        gg = p.grad.double()
-        mine = gg.norm().item()
-        refb = float(g["bf16/gradnorm/" + n])
-        tol = max(3 * abs(refb - ref) / max(ref, 1e-30), 0.05)
-        head = gg.flatten()[:64].cpu().numpy()
-        rh = g["fp32/gradhead/" + n]
-        cos = float(np.dot(head, rh) / (np.linalg.norm(head) * np.linalg.norm(rh) + 1e-30))
-        ok_norm = ref == 0 and mine == 0 or abs(mine - ref) <= tol * ref
-        ok_cos = (ref == 0 and mine == 0) or np.linalg.norm(rh) < 1e-12 * ref or \
-            cos >= (0.97 if np.linalg.norm(rh) > 1e-3 * ref else 0.9)
-        if not (ok_norm and ok_cos):
-            bad.append((n, mine, ref, refb, cos))
-    assert not bad, "\n".join(map(str, bad))
+def _check_grads(g, m, label):
+    return check_grads_probe(g, dict(m.named_parameters()), label=label)
 
 
 def _check_actions(g, a, key):
@@ -81,7 +68,7 @@ def test_tiny_loss_and_grads(tiny):
     d, g, m, gi = tiny
     loss = run_loss(m, gi)
     _check_loss(g, loss.item())
-    _check_grads(g, m)
+    _check_grads(g, m, "tiny")
 
 
 def test_tiny_grad_accumulation_and_zero(tiny):
@@ -109,19 +96,23 @@ def test_tiny_actions(tiny):
 
 
 @pytest.fixture(scope="module")
-def full():
+def full_model():
+    return build_gpu_model(O.FULL_DIMS)
+
+
+@pytest.fixture(scope="module")
+def full(full_model):
     d = O.FULL_DIMS
     g = load_golden("full")
-    m = build_gpu_model(d)
-    gi = gpu_inputs(m, d, int(g["bsz"]))
-    return d, g, m, gi
+    gi = gpu_inputs(full_model, d, int(g["bsz"]))
+    return d, g, full_model, gi
 
 
 def test_full_loss_and_grads(full):
     d, g, m, gi = full
     loss = run_loss(m, gi)
     _check_loss(g, loss.item())
-    _check_grads(g, m)
+    _check_grads(g, m, "full B=2")
 
 
 def test_full_actions(full):
@@ -132,15 +123,95 @@ def test_full_actions(full):
     np.testing.assert_allclose(a3.float().cpu().numpy(), np.clip(a.float().cpu().numpy(), -1, 1), atol=1e-2)
 
 
+def test_full_actions_hipgraph(full):
+    """The hipGraph-captured chunk (pizero_native/graph.py) at bridge size against the reference."""
+    from pizero_native.graph import InferenceGraph
+
+    d, g, m, gi = full
+    B = int(g["bsz"])
+    ig = InferenceGraph(m, B, clip=False)
+    ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"], gi["ppos"], gi["apos"],
+            gi["proprios"].float(), gi["noise"])
+    ig.capture()
+    for _ in range(3):  # replays are idempotent (static inputs, KV rewritten by each prefill)
+        a = ig.replay()
+    torch.cuda.synchronize()
+    _check_actions(g, a.clone(), "actions_unclipped")
+    eager = run_infer(m, gi, clip=False)
+    assert torch.equal(a.float(), eager.float()), float((a.float() - eager.float()).abs().max())
+
+
+@pytest.fixture(scope="module")
+def b16(full_model):
+    d = O.FULL_DIMS
+    g = load_golden("b16")
+    assert int(g["bsz"]) == 16
+    return d, g, full_model
+
+
+def test_b16_loss_and_grads(b16):
+    """config C2's micro-batch (bridge, B=16) against the reference."""
+    d, g, m = b16
+    gi = gpu_inputs(m, d, 16)
+    loss = run_loss(m, gi)
+    _check_loss(g, loss.item())
+    _check_grads(g, m, "bridge B=16")
+
+
+def test_microbatch64_batch_invariance(b16):
+    """The bench's micro-batch 64 = the 16 fixture samples x 4: same loss / gradients as B=16."""
+    d, g, m = b16
+    gi = gpu_inputs(m, d, 16, repeat=4)
+    assert gi["input_ids"].shape[0] == 64
+    loss = run_loss(m, gi)
+    _check_loss(g, loss.item())
+    _check_grads(g, m, "micro-batch 64")
+
+
 @pytest.mark.parametrize("which", ["tiny", "full"])
 def test_loss_and_grads_fused_joint_attention(which, request):
-    """the fused (flash) joint attention path (PZ_JOINT_ATTN=flash) against the same fixtures"""
+    """the fused (flash) joint attention path against the same fixtures"""
     d, g, m, gi = request.getfixturevalue(which)
     eng = m._engine()
+    prev = eng.joint_flash
     eng.joint_flash = True
     try:
         loss = run_loss(m, gi)
         _check_loss(g, loss.item())
-        _check_grads(g, m)
+        _check_grads(g, m, f"{which} flash")
     finally:
-        eng.joint_flash = False
+        eng.joint_flash = prev
+
+
+@pytest.mark.parametrize("which", ["tiny", "full"])
+def test_loss_and_grads_gemm_joint_attention(which, request):
+    """the GEMM + softmax joint attention path against the same fixtures"""
+    d, g, m, gi = request.getfixturevalue(which)
+    eng = m._engine()
+    prev = eng.joint_flash
+    eng.joint_flash = False
+    try:
+        loss = run_loss(m, gi)
+        _check_loss(g, loss.item())
+        _check_grads(g, m, f"{which} gemm")
+    finally:
+        eng.joint_flash = prev
+
+
+def test_interleaved_forwards_keep_their_saved_state(tiny):
+    """two forwards before one backward (autograd semantics): each keeps its own saved K/V, so the
+    gradient of loss(A) + loss(B) equals the sum of the separate gradients"""
+    d, g, m, gi = tiny
+    gj = gpu_inputs(m, d, 3)
+    gj["x0"] = -gj["x0"]
+    gj["t32"] = 1.0 - gj["t32"]
+    run_loss(m, gi)
+    ga = m.action_decoder.weight.grad.float().clone()
+    run_loss(m, gj)
+    gb = m.action_decoder.weight.grad.float().clone()
+    m.zero_grad(set_to_none=True)
+    la = run_loss(m, gi, backward=False)
+    lb = run_loss(m, gj, backward=False)
+    (la + lb).backward()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(m.action_decoder.weight.grad.float(), ga + gb, rtol=2e-2, atol=2e-3)

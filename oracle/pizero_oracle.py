@@ -203,7 +203,7 @@ def embed_siglip_and_text(W, d, input_ids, pixel_values):
     out = torch.where(text[..., None], emb, out)
     for b in range(input_ids.shape[0]):
         idx = (input_ids[b] == d["image_token_index"]).nonzero(as_tuple=True)[0]
-        out[b, idx] = img[b, : len(idx)]
+        out[b, idx] = img[b, : len(idx)].to(out.dtype)  # (autocast: img may be bf16)
     return out
 
 

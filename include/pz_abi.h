@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 8
+#define PZ_ABI_VERSION 10
 
 enum {
   PZ_OK = 0,
@@ -127,6 +127,22 @@ int pz_rope_table(float* cs, int64_t max_pos, int64_t head_dim, float theta, voi
 int pz_qkv_rope_split(const void* qkv, const int64_t* pos, const float* cs, void* q_out, void* k_out,
                       void* v_out, int64_t B, int64_t T, int64_t nh, int64_t nkv, int64_t hd,
                       int64_t Lq, int64_t qoff, int64_t Lk, int64_t koff, void* stream);
+/* q|k|v projection of few rows (M <= 8) with the fused Gemma RMSNorm of x (norm_w NULL: none) and
+ * RoPE + scatter as its epilogue (mixture.py:162-215, joint_model.py:170-257, utils.py:4-16): the
+ * projection x[M, K] . W[N = (nh + 2) * hd, K]^T is rounded to bf16 like pz_gemm + pz_qkv_rope_split
+ * would, then row r = b*T + t is rotated with the table cs at pos[r] and written to
+ * q_out[b][qoff + t][nh*hd] (Lq rows per sample), k_out / v_out[b][koff + t][hd] (Lk rows).  One
+ * launch for the denoise step's q|k|v (pizero.py:461-481), K % 512 == 0. */
+typedef struct pz_qkv_rope_args {
+  const void* x; int64_t ldx;
+  const void* W; int64_t ldw;
+  int64_t M, N, K;
+  const void* norm_w; float norm_eps;
+  const int64_t* pos; const float* cs;
+  void* q_out; void* k_out; void* v_out;
+  int64_t T, nh, hd, Lq, qoff, Lk, koff;
+} pz_qkv_rope_args;
+int pz_gemv_qkv_rope(const pz_qkv_rope_args* a, void* stream);
 /* backward of the above: writes d(qkv) (un-rotates dQ/dK, copies dV).  dq NULL -> zero dQ part */
 int pz_qkv_rope_split_bwd(const void* dq, const void* dk, const void* dv, const int64_t* pos,
                           const float* cs, void* dqkv, int64_t B, int64_t T, int64_t nh, int64_t nkv,
@@ -196,6 +212,25 @@ int pz_flash_fwd(const pz_flash_args* a, void* stream);
 int pz_flash_bwd_prep(const pz_flash_args* a, void* stream);
 /* dQ and delta (query-parallel), then dK, dV (key-parallel over all query rows of the unit); overwrite */
 int pz_flash_bwd(const pz_flash_args* a, void* stream);
+
+/* Decode-shaped joint attention (denoise steps, pizero.py:461-481; joint_model.py:259-292): for each
+ * sample b, the T query tokens x nh heads (T*nh <= 32 rows, MQA) q[(b*Lq + qoff + t)*ldq + h*256 ..]
+ * against the nk cached keys/values k/v[b*k_bstride + j*256 ..] (head_dim 256): logits
+ * cap*tanh(scale*q.k/cap), the Pi0 block mask for joint query token qtok0 + t (prefix counts cnt[b],
+ * prefix / cond sizes; NULL cnt: no mask), fp32 softmax, O[(b*T + t)*ldo + h*256 ..] bf16.  Two
+ * launches: per 32-key chunk partial (m, l, O) into the fp32 workspace ws (pz_decode_attn_ws_bytes),
+ * then a fixed-order merge.  Deterministic. */
+typedef struct pz_decode_attn_args {
+  const void* q; int64_t ldq, Lq, qoff;
+  const void* k; const void* v; int64_t k_bstride, v_bstride;
+  void* o; int64_t ldo;
+  int64_t B, nh, T, nk, head_dim;
+  float scale, cap;
+  const int32_t* cnt; int64_t prefix, cond, qtok0;
+  float* ws; int64_t ws_bytes;
+} pz_decode_attn_args;
+int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t nk);
+int pz_decode_attn(const pz_decode_attn_args* a, void* stream);
 
 /* SigLIP patch embed im2col (siglip.py:42-48,69-74): pixels bf16 [B,3,H,W] -> cols bf16
  * [B*(H/ps)*(W/ps), ldc] with k = c*ps*ps + ky*ps + kx, zero pad k in [3*ps*ps, ldc) */

@@ -77,6 +77,10 @@ __device__ __forceinline__ float silu_grad(float x) {
   return s * (1.f + x * (1.f - s));
 }
 
+// ---- few-row GEMV path (pz_gemv.hip), chosen by pz_gemm's planner ------------------
+bool pz_gemv_supported(const pz_gemm_args* a);
+int pz_gemv_launch(const pz_gemm_args* a, hipStream_t st);
+
 // ---- host side error plumbing -------------------------------------------------
 void pz_set_error(const char* fmt, ...);
 #define PZ_CHECK_ARG(cond, ...)          \

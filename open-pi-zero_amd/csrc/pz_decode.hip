@@ -1,0 +1,187 @@
+// Decode-shaped joint attention for the denoise steps (pizero.py:461-481 with joint_model.py:130-304):
+// the H action tokens of one sample x nh query heads (MQA: one K/V head of 256 shared by all heads,
+// so every (token, head) is a query row of the same keys) against every cached key (vlm + proprio +
+// the action tokens themselves).
+//
+// Two launches, each short and wide:
+//   decode_attn_part: one workgroup per 32-key chunk of one sample, ALL query rows (T x nh <= 32):
+//     S^T = K Q^T on the MFMA (16 keys x 16 rows tiles, one tile per wave, K and Q fragments loaded
+//     straight from global memory), soft-cap + Pi0 block mask, chunk-local softmax stats (m, l),
+//     partial O = P V on the VALU (each thread 8 head dims x 4 query rows, its 16-byte V loads issued
+//     before the S phase), written as fp32 partials to the caller's workspace;
+//   decode_attn_combine: one workgroup per query row merges the chunks' (m, l, O) in fixed order.
+// The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of once per head.
+// Deterministic (no atomics).
+#include "pz_common.h"
+
+namespace {
+
+constexpr int DA_KC = 32;    // keys per chunk (workgroup)
+constexpr int DA_R = 32;     // max query rows per sample (tokens x heads)
+constexpr int DA_HD = 256;   // head dim (Gemma)
+constexpr int DA_RS = DA_HD + 4;  // workspace row: O[256], m, l (16-byte aligned rows)
+
+__device__ __forceinline__ bool da_allowed(int t, int j, int nk, int cnt, int P, int C) {
+  if (j >= nk) return false;
+  if (t < P) return t < cnt && j < cnt;
+  if (t < P + C) return j < cnt || (j >= P && j < P + C);
+  return j < cnt || j >= P;
+}
+
+// grid (nchunks, B), 256 threads = 4 waves: wave w computes key tile (w & 1) x row tile (w >> 1)
+__global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
+  __shared__ float S[DA_R][DA_KC + 1];  // logits -> probabilities, [row][key]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
+  const int cnt = a.cnt ? a.cnt[b] : nk;
+  const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
+  const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
+  const int j0 = c * DA_KC;
+  // P.V ownership: thread = 8 head dims (dg) x 4 query rows (rg); its V loads (16 keys x 16 B, 128 B
+  // contiguous per 8 lanes) are issued before the S phase so their latency overlaps it
+  const int dg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  u32x4 vv[DA_KC / 2];
+#pragma unroll
+  for (int u = 0; u < DA_KC / 2; ++u)
+    vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + u, nk - 1) * DA_HD + 8 * dg);
+  {
+    const int kt = wave & 1, rt = wave >> 1;
+    const int g = lane >> 4;
+    const int key = min(j0 + kt * 16 + (lane & 15), nk - 1);
+    const int row = rt * 16 + (lane & 15);  // query row = t * nh + h
+    const bool rok = row < R;
+    const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
+    const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
+    const bf16_t* qp = (const bf16_t*)a.q + ((int64_t)b * a.Lq + a.qoff + t) * a.ldq + (int64_t)h * DA_HD + 8 * g;
+    bf16x8 kf[8], qf[8];
+#pragma unroll
+    for (int dc = 0; dc < 8; ++dc) {
+      kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
+      qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dc = 0; dc < 8; ++dc) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], acc, 0, 0, 0);
+    // lane holds S^T[key = kt*16 + 4g + e][row = rt*16 + (lane & 15)]
+    const int qt = (int)a.qtok0 + t;
+    const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int kl = kt * 16 + 4 * g + e;
+      float x = acc[e] * a.scale;
+      if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
+      const bool ok = rok && da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond);
+      S[row][kl] = ok ? x : -INFINITY;
+    }
+  }
+  __syncthreads();
+  // chunk-local softmax stats per row (thread r < 32): m, l; S <- p
+  float* ws = a.ws + ((int64_t)b * gridDim.x + c) * DA_R * DA_RS;
+  if (threadIdx.x < DA_R) {
+    const int r = threadIdx.x;
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
+    float l = 0.f;
+#pragma unroll
+    for (int k = 0; k < DA_KC; ++k) {
+      const float p = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
+      S[r][k] = p;
+      l += p;
+    }
+    ws[r * DA_RS + DA_HD] = m;
+    ws[r * DA_RS + DA_HD + 1] = l;
+  }
+  __syncthreads();
+  // partial O[row][d] = sum_k p[row][k] V[k][d]: 4 rows x 8 dims per thread, two halves of 16 keys
+  float o[4][8];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[r][e] = 0.f;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (half == 1) {
+#pragma unroll
+      for (int u = 0; u < DA_KC / 2; ++u)
+        vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + DA_KC / 2 + u, nk - 1) * DA_HD + 8 * dg);
+    }
+#pragma unroll
+    for (int u4 = 0; u4 < DA_KC / 8; ++u4) {
+      float pr[4][4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * rg + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pr[r][q] = S[row][half * (DA_KC / 2) + 4 * u4 + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float vf[8];
+        const u32x4 vr = vv[4 * u4 + q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          vf[2 * e] = __uint_as_float(vr[e] << 16);
+          vf[2 * e + 1] = __uint_as_float(vr[e] & 0xffff0000u);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[r][e] += pr[r][q] * vf[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = 4 * rg + r;
+    if (row < R) {
+      float4* dst = reinterpret_cast<float4*>(ws + row * DA_RS + 8 * dg);
+      dst[0] = float4{o[r][0], o[r][1], o[r][2], o[r][3]};
+      dst[1] = float4{o[r][4], o[r][5], o[r][6], o[r][7]};
+    }
+  }
+}
+
+// grid (R, B), 256 threads: thread = head dim; merges the chunks in order 0..nchunks-1
+__global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a, int nchunks) {
+  const int r = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
+  const int nh = (int)a.nh, t = r / nh, h = r % nh;
+  const float* ws = a.ws + (int64_t)b * nchunks * DA_R * DA_RS + r * DA_RS;
+  float M = -INFINITY;
+  for (int c = 0; c < nchunks; ++c) M = fmaxf(M, ws[(int64_t)c * DA_R * DA_RS + DA_HD]);
+  float o = 0.f, l = 0.f;
+  for (int c = 0; c < nchunks; ++c) {
+    const float* w = ws + (int64_t)c * DA_R * DA_RS;
+    const float mc = w[DA_HD];
+    const float s = mc == -INFINITY ? 0.f : __expf(mc - M);
+    o += s * w[d];
+    l += s * w[DA_HD + 1];
+  }
+  bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + t) * a.ldo + (int64_t)h * DA_HD + d;
+  *out = f2bf(l > 0.f ? o / l : 0.f);
+}
+
+}  // namespace
+
+extern "C" int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t nk) {
+  return B * ((nk + DA_KC - 1) / DA_KC) * DA_R * DA_RS * (int64_t)sizeof(float);
+}
+
+extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->ws && a->B > 0 && a->nh > 0, "decode_attn: bad args");
+  PZ_CHECK_ARG(a->head_dim == DA_HD && a->T >= 1 && a->T * a->nh <= DA_R && a->nk >= 1,
+               "decode_attn: head_dim 256 and tokens x heads <= 32 query rows per sample");
+  PZ_CHECK_ARG(a->ws_bytes >= pz_decode_attn_ws_bytes(a->B, a->nk), "decode_attn: workspace too small");
+  PZ_CHECK_ARG(PZ_ALIGNED(a->q, 16) && PZ_ALIGNED(a->k, 16) && PZ_ALIGNED(a->v, 16) && PZ_ALIGNED(a->o, 2) &&
+                   PZ_ALIGNED(a->ws, 16) && a->ldq % 8 == 0 && a->k_bstride % 8 == 0 && a->v_bstride % 8 == 0,
+               "decode_attn: alignment");
+  const int nchunks = (int)((a->nk + DA_KC - 1) / DA_KC);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)nchunks, (unsigned)a->B), dim3(256), 0, st, *a);
+  PZ_CHECK_LAUNCH();
+  hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
+                     nchunks);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

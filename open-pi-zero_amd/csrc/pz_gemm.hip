@@ -1932,7 +1932,7 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
@@ -1989,6 +1989,12 @@ Plan make_plan(const pz_gemm_args* a) {
   pl.bkc = a->b_kcontig != 0;
   pl.geglu = a->epilogue == PZ_EPI_GEGLU;
   const int64_t ncols = pl.geglu ? a->geglu_inter : a->N;
+  // GEMV path (M <= 8, K % 512 == 0: the B = 1..2 denoise rows): every CU streams its weight slice
+  // (pz_gemv.hip); PZ_GEMV=0 falls back to the MFMA skinny kernel below
+  if (pz_gemv_supported(a)) {
+    pl.kind = PATH_GEMV;
+    return pl;
+  }
   // skinny path: few rows, weights streamed once (inference denoise / proprio rows)
   if (a->M <= 16 && pl.akc && pl.bkc && a->K % 32 == 0 && !a->c_fp32 && a->epilogue < PZ_EPI_DGELU) {
     const int64_t kch = a->K / 32;
@@ -2060,6 +2066,9 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   switch (pl.kind) {
     case PATH_SKINNY:
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
+      break;
+    case PATH_GEMV:
+      snprintf(buf, sizeof(buf), "gemv_kernel<M<=%d>", a->M <= 4 ? 4 : 8);
       break;
     case PATH_256:
       if (use_8phase() && pl.tail_s)
@@ -2218,6 +2227,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
 
   const Plan pl = make_plan(a);
+  if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
   if (a->norm_w)
     PZ_CHECK_ARG(pl.kind == PATH_SKINNY && PZ_ALIGNED(a->norm_w, 16),
                  "pz_gemm: fused RMSNorm needs the few-row path (M <= 16, k-contiguous A/B, K %% 32 == 0) "

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 8  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 10  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -88,6 +88,23 @@ class AdamW8Args(C.Structure):
     ]
 
 
+class QkvRopeArgs(C.Structure):
+    _fields_ = [
+        ("x", vp), ("ldx", i64), ("W", vp), ("ldw", i64), ("M", i64), ("N", i64), ("K", i64),
+        ("norm_w", vp), ("norm_eps", f32), ("pos", vp), ("cs", vp), ("q_out", vp), ("k_out", vp), ("v_out", vp),
+        ("T", i64), ("nh", i64), ("hd", i64), ("Lq", i64), ("qoff", i64), ("Lk", i64), ("koff", i64),
+    ]
+
+
+class DecodeAttnArgs(C.Structure):
+    _fields_ = [
+        ("q", vp), ("ldq", i64), ("Lq", i64), ("qoff", i64), ("k", vp), ("v", vp), ("k_bstride", i64),
+        ("v_bstride", i64), ("o", vp), ("ldo", i64), ("B", i64), ("nh", i64), ("T", i64), ("nk", i64),
+        ("head_dim", i64), ("scale", f32), ("cap", f32), ("cnt", vp), ("prefix", i64), ("cond", i64),
+        ("qtok0", i64), ("ws", vp), ("ws_bytes", i64),
+    ]
+
+
 # name -> argtypes (restype int unless listed in _RESTYPE)
 SIGNATURES = {
     "pz_gemm": [C.POINTER(GemmArgs), vp],
@@ -104,6 +121,9 @@ SIGNATURES = {
     "pz_rope_table": [vp, i64, i64, f32, vp],
     "pz_qkv_rope_split": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
     "pz_qkv_rope_split_bwd": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
+    "pz_gemv_qkv_rope": [C.POINTER(QkvRopeArgs), vp],
+    "pz_decode_attn": [C.POINTER(DecodeAttnArgs), vp],
+    "pz_decode_attn_ws_bytes": [i64, i64],
     "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],
     "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
     "pz_flash_fwd": [C.POINTER(FlashArgs), vp],
@@ -132,7 +152,8 @@ SIGNATURES = {
     "pz_last_error": [],
     "pz_abi_version": [],
 }
-_RESTYPE = {"pz_last_error": C.c_char_p, "pz_gemm_kernel_name": C.c_char_p, "pz_norm_rows_per_part": i64}
+_RESTYPE = {"pz_last_error": C.c_char_p, "pz_gemm_kernel_name": C.c_char_p, "pz_norm_rows_per_part": i64,
+            "pz_decode_attn_ws_bytes": i64}
 
 _lib = None
 

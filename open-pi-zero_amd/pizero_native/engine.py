@@ -821,6 +821,16 @@ class Engine:
         return out, {"vlm": dEv, "proprio": dEp, "action": dEa}
 
     # ============================================================ inference ==
+    def decode_attn_ok(self):
+        """pz_decode_attn for the denoise attention (H x nh <= 32 query rows per sample, head_dim 256);
+        PZ_DECODE_ATTN=0 uses the key-split flash kernel + combine"""
+        d = self.d
+        return d.H * d.nh <= 32 and d.hd == 256 and os.environ.get("PZ_DECODE_ATTN", "1") != "0"
+
+    def gemv_ok(self, M, K):
+        """few-row GEMV kernels (pz_gemv.hip): M <= 8 rows, K % 512 == 0 (PZ_GEMV=0 disables)"""
+        return M <= 8 and K % 512 == 0 and os.environ.get("PZ_GEMV", "1") != "0"
+
     def prefill(self, ids, pix, cnt, vpos, ppos, proprios, kcache, vcache):
         """pizero.py:430-451: SigLIP + prefix pass over {vlm, proprio}; writes post-RoPE K/V caches."""
         d = self.d
@@ -852,6 +862,14 @@ class Engine:
                 p = f"{g.prefix}{l}."
                 x = X[g.name]
                 M = x.shape[0]
+                if self.gemv_ok(M, x.shape[1]):  # few rows (the proprio token): one fused launch
+                    if last:
+                        self._kv_only_gemv(x, p, pos[g.pos_key], g, Kj, Vj, L1, Lp)
+                    else:
+                        ops.gemv_qkv_rope(x, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, g.T, nh,
+                                          hd, L1, g.off, Lp, g.off,
+                                          norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                    continue
                 h = torch.empty_like(x)
                 ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
                 if last:  # only K/V are consumed downstream (pizero.py:451, skipped post-attn)
@@ -889,6 +907,13 @@ class Engine:
                 x = X[g.name]
                 X[g.name] = self._post_attn(g, p, x, Pm, Vj, B, L1, Lp)
         return kcache, vcache
+
+    def _kv_only_gemv(self, x, p, pos, g, Kj, Vj, L1, Lp):
+        """last prefill layer, few rows: only the k|v projection (+RoPE on k) is consumed"""
+        d = self.d
+        ops.gemv_qkv_rope(x, self.ar.span(p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"), pos,
+                          self.rope(g.theta), None, Kj, Vj, g.T, 0, d.hd, L1, g.off, Lp, g.off,
+                          norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
 
     def _attn_flash_infer(self, Q, K, V, outs, Lq, nk, tok0, cnt, B):
         """pz_flash_args for the inference attention: queries = Lq tokens starting at joint token tok0
@@ -958,18 +983,26 @@ class Engine:
             p = f"{g.prefix}{l}."
             Kj, Vj = kcache[l], vcache[l]
             M = x.shape[0]
-            qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
-            if M <= 16:  # RMSNorm fused into the q|k|v GEMM
-                ops.linear(x, self.qkv_w(p), qkv, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+            if self.gemv_ok(M, d.aH):  # one launch: RMSNorm + q|k|v GEMV + RoPE + Q / K-cache / V-cache scatter
+                ops.gemv_qkv_rope(x, self.qkv_w(p), apos, self.rope(g.theta), Q, Kj, Vj, d.H, nh, hd, d.H, 0, Lp,
+                                  g.off, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
             else:
-                h = torch.empty_like(x)
-                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
-                ops.linear(h, self.qkv_w(p), qkv)
-            ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
+                qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
+                if M <= 16:  # RMSNorm fused into the q|k|v GEMM
+                    ops.linear(x, self.qkv_w(p), qkv, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                else:
+                    h = torch.empty_like(x)
+                    ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
+                    ops.linear(h, self.qkv_w(p), qkv)
+                ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
             if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over every cached key
                 if O is None:
                     O = torch.empty(B * d.H, nh * hd, device=dev, dtype=BF16)
-                ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, d.H, O)], d.H, L, g.off, cnt, B))
+                if self.decode_attn_ok():  # one workgroup per (head, sample), no key split / combine launch
+                    ops.decode_attn(Q, d.H, 0, Kj, Vj, O, B, nh, d.H, L, 1.0 / math.sqrt(hd), 50.0, cnt, d.P, d.C,
+                                    g.off)
+                else:
+                    ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, d.H, O)], d.H, L, g.off, cnt, B))
                 x = self._post_attn_O(g, p, x, O)
                 continue
             if S is None:

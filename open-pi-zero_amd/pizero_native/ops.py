@@ -21,6 +21,8 @@ from ._lib import (
     PZ_EPI_SILU,
     PZ_SUMSQ_PARTS,
     AdamW8Args,
+    QkvRopeArgs,
+    DecodeAttnArgs,
     FlashArgs,
     GemmArgs,
     SmallGemmArgs,
@@ -278,6 +280,37 @@ def qkv_rope_split(qkv, pos, cs, q_out, k_out, v_out, B, T, nh, nkv, hd, Lq, qof
 def qkv_rope_split_bwd(dq, dk, dv, pos, cs, dqkv, B, T, nh, nkv, hd, Lq, qoff, Lk, koff):
     call("pz_qkv_rope_split_bwd", _p(dq), _p(dk), _p(dv), _p(pos), _p(cs), _p(dqkv), B, T, nh, nkv, hd, Lq,
          qoff, Lk, koff, _st())
+
+
+def gemv_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, koff, norm=None):
+    """Few-row q|k|v projection (+ fused RMSNorm) with RoPE and the Q / K / V scatter as its epilogue."""
+    a = QkvRopeArgs()
+    a.x, a.ldx = _p(x), x.stride(0)
+    a.W, a.ldw = _p(W), W.stride(0)
+    a.M, a.N, a.K = x.shape[0], W.shape[0], x.shape[1]
+    if norm is not None:
+        a.norm_w, a.norm_eps = _p(norm[0]), float(norm[1])
+    a.pos, a.cs = _p(pos), _p(cs)
+    a.q_out, a.k_out, a.v_out = _p(q_out), _p(k_out), _p(v_out)
+    a.T, a.nh, a.hd, a.Lq, a.qoff, a.Lk, a.koff = T, nh, hd, Lq, qoff, Lk, koff
+    call("pz_gemv_qkv_rope", C.byref(a), _st())
+
+
+def decode_attn(q, Lq, qoff, k, v, o, B, nh, T, nk, scale, cap, cnt, prefix, cond, qtok0):
+    """Few-query joint attention (denoise): q [B, Lq, nh*hd] rows qoff.., k/v [B, Lk, hd], o [B*T, nh*hd]."""
+    a = DecodeAttnArgs()
+    a.q, a.ldq, a.Lq, a.qoff = _p(q), q.shape[-1], Lq, qoff
+    a.k, a.v = _p(k), _p(v)
+    a.k_bstride, a.v_bstride = k.stride(0), v.stride(0)
+    a.o, a.ldo = _p(o), o.stride(0)
+    a.B, a.nh, a.T, a.nk, a.head_dim = B, nh, T, nk, k.shape[-1]
+    a.scale, a.cap = float(scale), float(cap)
+    a.cnt, a.prefix, a.cond, a.qtok0 = _p(cnt), prefix, cond, qtok0
+    need = lib().pz_decode_attn_ws_bytes(B, nk)
+    ws = workspace(o.device)  # the GEMM split-K scratch: stream-ordered, not in use between kernels
+    assert ws.numel() * 4 >= need
+    a.ws, a.ws_bytes = _p(ws), ws.numel() * 4
+    call("pz_decode_attn", C.byref(a), _st())
 
 
 def attn_softmax(S, lds, P, ldp, R, N, scale, cap=0.0, tcap=None, mask_mode=0, rows_per_batch=1, heads=1,

@@ -259,10 +259,11 @@ def test_split_k_forward_epilogues(M, N, K):
 
 
 @pytest.mark.parametrize("K", [96, 1024, 2048, 4096, 4128])
-def test_skinny_widths(K):
-    """M <= 16 rows: W = 4/8/16 waves per block, 8/4/1-chunk unroll tails."""
+def test_skinny_widths(K, monkeypatch):
+    """M <= 16 rows: W = 4/8/16 waves per block, 8/4/1-chunk unroll tails (MFMA skinny kernel)."""
     from pizero_native import ops
 
+    monkeypatch.setenv("PZ_GEMV", "0")
     for M in (1, 4, 16):
         x, W, b = bf(M, K), bf(1040, K, scale=K ** -0.5), bf(1040)
         out = torch.empty(M, 1040, device=dev, dtype=torch.bfloat16)
@@ -278,6 +279,7 @@ def test_skinny_column_blocks(N, min_nc, monkeypatch):
     from pizero_native import ops
 
     monkeypatch.setenv("PZ_SKINNY_MINNC", min_nc)
+    monkeypatch.setenv("PZ_GEMV", "0")
     K = 2048
     for M in (1, 4, 16):
         x, W, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(M, N)
@@ -294,12 +296,14 @@ def _rms_ref(x, w, eps):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * (1 + w.float())).to(torch.bfloat16)
 
 
+@pytest.mark.parametrize("gemv", ["1", "0"])
 @pytest.mark.parametrize("K,N", [(1024, 2560), (2048, 1024)])
-def test_skinny_fused_rmsnorm(K, N):
+def test_skinny_fused_rmsnorm(K, N, gemv, monkeypatch):
     """Gemma RMSNorm fused into the few-row GEMM (inference denoise q|k|v and gate|up) vs
     rmsnorm -> GEMM in fp32; also the GeGLU epilogue."""
     from pizero_native import ops
 
+    monkeypatch.setenv("PZ_GEMV", gemv)
     eps = 1e-6
     for M in (1, 4, 16):
         x = bf(M, K, scale=3.0)
@@ -318,6 +322,68 @@ def test_skinny_fused_rmsnorm(K, N):
     with pytest.raises(RuntimeError):  # many rows: not the few-row path
         x = bf(64, K)
         ops.linear(x, W, torch.empty(64, N, device=dev, dtype=torch.bfloat16), norm=(w, eps))
+
+
+@pytest.mark.parametrize("K", [1024, 2048, 4096])
+def test_gemv_epilogues(K):
+    """few-row GEMV path (M <= 8, K % 512 == 0): every epilogue vs fp32 torch"""
+    from pizero_native import ops
+
+    F = torch.nn.functional
+    for M in (1, 4, 5, 8):
+        assert ops.gemm_kernel_name(M, 1024, K).startswith("gemv_kernel"), ops.gemm_kernel_name(M, 1024, K)
+        x = bf(M, K)
+        for N in (1024, 1040, 2560):
+            W, b, r = bf(N, K, scale=K ** -0.5), bf(N), bf(M, N)
+            ref = x.float() @ W.float().t()
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, out, bias=b, resid=r)
+            close(out, ref + b.float() + r.float())
+            aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, out, bias=b, epi=ops.PZ_EPI_GELU, aux=aux)
+            close(aux, ref + b.float())
+            close(out, F.gelu(ref + b.float(), approximate="tanh"))
+            ops.linear(x, W, out, epi=ops.PZ_EPI_SILU)
+            close(out, F.silu(ref))
+            o32 = torch.zeros(M, N, device=dev)
+            ops.gemm(M, N, K, x, K, True, W, K, True, o32, N, beta=True)
+            ops.gemm(M, N, K, x, K, True, W, K, True, o32, N, beta=True)
+            close(o32, 2 * ref, rtol=1e-3, atol=1e-3)
+        I = 4096
+        Wg = bf(2 * I, K, scale=K ** -0.5)
+        raw = x.float() @ Wg.float().t()
+        h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+        gu = torch.empty(M, 2 * I, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, Wg, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+        close(gu, raw)
+        close(h, F.gelu(raw[:, :I], approximate="tanh") * raw[:, I:], rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,T", [(4, 4), (8, 4), (1, 1)])
+def test_gemv_qkv_rope_matches_unfused(M, T):
+    """pz_gemv_qkv_rope == RMSNorm-fused q|k|v GEMM + pz_qkv_rope_split (same rounding points)"""
+    from pizero_native import ops
+
+    K, nh, hd = 1024, 8, 256
+    B = M // T
+    N = (nh + 2) * hd
+    x, W, w = bf(M, K, scale=2.0), bf(N, K, scale=K ** -0.5), bf(K, scale=0.3)
+    pos = torch.randint(0, 200, (B, T), device=dev, dtype=torch.int64)
+    cs = torch.empty(301 * hd, device=dev)
+    ops.rope_table(cs, 300, hd, 100.0)
+    Lq, Lk, qoff, koff = T + 2, 290, 1, 277
+    q1 = torch.zeros(B, Lq, nh * hd, device=dev, dtype=torch.bfloat16)
+    k1 = torch.zeros(B, Lk, hd, device=dev, dtype=torch.bfloat16)
+    v1 = torch.zeros_like(k1)
+    q2, k2, v2 = q1.clone(), k1.clone(), v1.clone()
+    ops.gemv_qkv_rope(x, W, pos, cs, q1, k1, v1, T, nh, hd, Lq, qoff, Lk, koff, norm=(w, 1e-6))
+    qkv = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, qkv, norm=(w, 1e-6))
+    ops.qkv_rope_split(qkv, pos, cs, q2, k2, v2, B, T, nh, 1, hd, Lq, qoff, Lk, koff)
+    close(q1, q2, rtol=2e-2, atol=2e-2)
+    close(k1, k2, rtol=2e-2, atol=2e-2)
+    close(v1, v2, rtol=2e-2, atol=2e-2)
+    assert q1[:, :qoff].abs().max() == 0 and k1[:, :koff].abs().max() == 0  # only the target rows written
 
 
 def test_small_gemm():
@@ -566,3 +632,27 @@ def test_time_embed_modes_match_reference():
             ops.time_embed(t, o, float(P), ref_bf16=bool(mode))
             outs.append((o.float().cpu() - torch.from_numpy(g[f"bf16_{P}"])).abs().mean().item())
         assert outs[1] < outs[0], outs
+
+
+@pytest.mark.parametrize("B,T,cnts", [(1, 4, [270]), (2, 4, [276, 259]), (1, 2, [100]), (2, 1, [5, 276])])
+def test_decode_attn_matches_reference(B, T, cnts):
+    """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
+    with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306)"""
+    from pizero_native import ops
+
+    P, C, nh, hd = 276, 1, 8, 256
+    nk = P + C + T
+    Lp = (nk + 7) // 8 * 8
+    q = bf(B, T, nh * hd)
+    k, v = bf(B, Lp, hd), bf(B, Lp, hd)
+    cnt = torch.tensor(cnts, device=dev, dtype=torch.int32)
+    o = torch.empty(B * T, nh * hd, device=dev, dtype=torch.bfloat16)
+    ops.decode_attn(q, T, 0, k, v, o, B, nh, T, nk, 1 / 16.0, 50.0, cnt, P, C, P + C)
+    qf = q.float().view(B, T, nh, hd)
+    s = torch.einsum("bthd,bjd->bhtj", qf, k.float()[:, :nk]) / 16.0
+    s = 50.0 * torch.tanh(s / 50.0)
+    j = torch.arange(nk, device=dev)
+    allowed = (j[None, :] < cnt[:, None]) | (j[None, :] >= P)  # action rows (pizero.py:296-306)
+    s = s.masked_fill(~allowed[:, None, None, :], float("-inf"))
+    ref = torch.einsum("bhtj,bjd->bthd", torch.softmax(s, -1), v.float()[:, :nk]).reshape(B * T, nh * hd)
+    close(o, ref, rtol=2e-2, atol=2e-2)

@@ -10,10 +10,10 @@ import sys
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if r.get("Start_Timestamp") and r.get("End_Timestamp")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "embed_merge" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "patchify" in r["Kernel_Name"]]  # first kernel of a chunk
     ch = rows[idx[-2]:idx[-1]]
     t0 = int(ch[0]["Start_Timestamp"])
-    te = [i for i, r in enumerate(ch) if "time_embed" in r["Kernel_Name"]]
+    te = [i for i, r in enumerate(ch) if "time_embed" in r["Kernel_Name"] or "denoise" in r["Kernel_Name"]]
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
     print(f"chunk: {len(ch)} kernels, wall {(int(ch[-1]['End_Timestamp']) - t0) / 1e3:.1f} us, "
           f"busy {sum(map(dur, ch)):.1f} us; prefill {te[0]} kernels, "

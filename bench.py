@@ -145,6 +145,57 @@ def cpu_baseline(seconds_budget=25.0):
                        "torch-CPU oracle/pizero_oracle.py")}
 
 
+def c5_inference(cfg, dev, iters):
+    """BASELINE.json configs[4] (the Pi0-paper shape): 3 images (768 image tokens) + 20 text + 1 proprio,
+    action chunk 50, B=1, bf16, prefill + 10 Euler steps in one hipGraph; against the 73 ms Pi0-paper
+    figure quoted in the reference README (README.md:80,84).  Random-init weights."""
+    import copy
+
+    from pizero_native.graph import InferenceGraph
+    from src.model.vla.pizero import PiZero
+
+    c = copy.deepcopy(cfg)
+    for key, val in (("num_images", 3), ("max_seq_len", 788), ("max_image_text_tokens", 788), ("horizon_steps", 50)):
+        c[key] = val
+    m = PiZero(c, device=dev, dtype=torch.bfloat16, init="default")
+    m.tie_action_proprio_weights()
+    m.freeze_all_weights()
+    m.eval()
+    d = m._engine().d
+    gen = torch.Generator().manual_seed(11)
+    ids = torch.full((1, d.P), 0, dtype=torch.int64)
+    ids[:, : d.n_img] = d.image_token
+    ids[:, d.n_img] = 2
+    ids[:, d.n_img + 1 : d.P - 1] = torch.randint(3, 256000, (1, d.P - d.n_img - 2), generator=gen)
+    ids[:, d.P - 1] = 108
+    mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids((ids != 0).long(), torch.bfloat16)
+    itp, amask = m.split_full_mask_into_submasks(mask)
+    pix = (torch.rand(1, 3, 3, d.img, d.img, generator=gen) * 2 - 1).to(dev, torch.bfloat16)
+    prop = (torch.rand(1, 1, d.Pd, generator=gen) * 2 - 1).to(dev)
+    noise = torch.randn(1, d.H, d.A, device=dev)
+    g = InferenceGraph(m, 1)
+    g.load(ids.to(dev), pix, m.block_prefix_counts(itp.to(dev), amask.to(dev)), vpos.to(dev), ppos.to(dev),
+           apos.to(dev), prop, noise)
+    g.capture()
+    for _ in range(3):
+        g.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    del g, m
+    torch.cuda.empty_cache()
+    return {"metric": "bf16 action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
+                      "1 proprio, chunk 50, B=1, prefill + 10 Euler steps)",
+            "graph_ms": ms, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
+            "baseline_source": "Pi0 paper figure quoted in the reference README.md:80,84 (other hardware)",
+            "vs_baseline": 73.0 / ms, "dtype": "bf16"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +207,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--optim-bits", type=int, default=8, choices=(8, 32))
+    ap.add_argument("--no-c5", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -288,6 +340,10 @@ def main():
                  "algorithmic_bytes": INFER_BYTES, "achieved_GBps": INFER_BYTES / (graph_ms * 1e-3) / 1e9,
                  "frac": INFER_BYTES / (graph_ms * 1e-3) / (PEAK_HBM_GBPS * 1e9)}
 
+    c5 = None
+    if not args.no_infer and not args.no_c5 and rank == 0:
+        c5 = c5_inference(cfg, dev, args.infer_iters)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
@@ -310,6 +366,7 @@ def main():
                          "frac": None if achieved is None else achieved / PEAK_BF16_TFLOPS,
                          **pmc_traffic(kname, [Mg, Ng, Kg])},
             "inference": infer,
+            "c5_inference": c5,
             "cpu_baseline": cpu,
             "loss_mean": float(loss_acc.item()) / (accum * args.steps * max(1, world)),
             "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else None,

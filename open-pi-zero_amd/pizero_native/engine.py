@@ -56,7 +56,7 @@ class Dims:
     pad_token: int
     img: int
     ps: int
-    n_img: int
+    n_img: int  # image tokens per sample (= img_tok x n_images)
     vH: int
     vI: int
     vL: int
@@ -80,6 +80,12 @@ class Dims:
     steps: int
     clip: float | None
     time_bf16: bool = False  # pz_time_embed mode 1: the reference's bf16 arithmetic (see modules.py)
+    n_images: int = 1  # images per sample (C5, the Pi0-paper shape: 3)
+
+    @property
+    def img_tok(self):
+        """SigLIP tokens per image"""
+        return (self.img // self.ps) ** 2
 
     @staticmethod
     def from_cfg(cfg):
@@ -93,7 +99,8 @@ class Dims:
             P=int(_cfg(cfg, "max_image_text_tokens", _cfg(cfg, "max_seq_len"))), C=int(_cfg(cfg, "cond_steps")),
             H=int(_cfg(cfg, "horizon_steps")), A=int(_cfg(cfg, "action_dim")), Pd=int(_cfg(cfg, "proprio_dim")),
             vocab=int(_cfg(cfg, "vocab_size")), image_token=int(_cfg(cfg, "image_token_index")),
-            pad_token=int(_cfg(cfg, "pad_token_id")), img=img, ps=ps, n_img=(img // ps) ** 2,
+            pad_token=int(_cfg(cfg, "pad_token_id")), img=img, ps=ps,
+            n_img=(img // ps) ** 2 * int(_cfg(cfg, "num_images", 1)),
             vH=int(_cfg(v, "hidden_size")), vI=int(_cfg(v, "intermediate_size")),
             vL=int(_cfg(v, "num_hidden_layers")), vheads=int(_cfg(v, "num_attention_heads")),
             ln_eps=float(_cfg(v, "layer_norm_eps", 1e-6)),
@@ -109,6 +116,7 @@ class Dims:
             tmax=float(_cfg(cfg, "time_max_period", 10000.0)), sig_min=float(_cfg(cfg, "flow_sig_min", 0.001)),
             steps=int(_cfg(cfg, "num_inference_steps")), clip=None if clip is None else float(clip),
             time_bf16=bool(_cfg(cfg, "time_embed_bf16_reference", False)),
+            n_images=int(_cfg(cfg, "num_images", 1)),
         )
 
     @property
@@ -236,10 +244,13 @@ class Engine:
 
     # ================================================================ SigLIP ==
     def siglip_forward(self, pix, save):
-        """siglip.py:34-300 + projector (siglip.py:9-31). pix bf16 [B,3,H,W] -> img [B*n_img, proj]."""
+        """siglip.py:34-300 + projector (siglip.py:9-31). pix bf16 [B,3,H,W] or [B,n_images,3,H,W] ->
+        img [B*n_img, proj] (a sample's images' tokens consecutive, in image order)."""
         d = self.d
-        B = pix.shape[0]
-        M = B * d.n_img
+        pix = pix.reshape(-1, 3, d.img, d.img)
+        B = pix.shape[0]  # images
+        Nt = d.img_tok
+        M = B * Nt
         dev = pix.device
         vt = "vision_tower.vision_model."
         kc = d.kcols
@@ -249,13 +260,13 @@ class Engine:
         wpatch = self.w(vt + "embeddings.patch_embedding.weight").view(d.vH, -1)
         ops.copy_rows(wpatch, wpatch.shape[1], 0, wpad, kc, 0, 1, d.vH, wpatch.shape[1])
         x = torch.empty(M, d.vH, device=dev, dtype=BF16)
-        ops.gemm(d.n_img, d.vH, kc, cols, kc, True, wpad, kc, True, x, d.vH, batch=B, sA=(d.n_img * kc, 0),
-                 sC=(d.n_img * d.vH, 0), bias=self.w(vt + "embeddings.patch_embedding.bias"),
+        ops.gemm(Nt, d.vH, kc, cols, kc, True, wpad, kc, True, x, d.vH, batch=B, sA=(Nt * kc, 0),
+                 sC=(Nt * d.vH, 0), bias=self.w(vt + "embeddings.patch_embedding.bias"),
                  resid=self.w(vt + "embeddings.position_embedding.weight"), ld_resid=d.vH, sR=(0, 0))
         if save is not None:
             save["cols"] = cols
         nh, hd = d.vheads, d.vH // d.vheads
-        Np = d.n_img
+        Np = Nt
         layers = []
         for i in range(d.vL):
             p = f"{vt}encoder.layers.{i}."
@@ -300,8 +311,8 @@ class Engine:
 
     def siglip_backward(self, sv, dimg, beta):
         d = self.d
-        B = sv["B"]
-        M = B * d.n_img
+        B = sv["B"]  # images
+        M = B * d.img_tok
         dev = dimg.device
         vt = "vision_tower.vision_model."
         rpp = ops.rows_per_part()
@@ -322,7 +333,7 @@ class Engine:
                           dw_part=pw, db_part=pb)
         self._norm_grads(vt + "post_layernorm.", pw, pb, beta)
         nh, hd = d.vheads, d.vH // d.vheads
-        Np = d.n_img
+        Np = d.img_tok
         W3 = 3 * d.vH
         dg = torch.empty(M, d.vI, device=dev, dtype=BF16)
         delta = torch.empty(B * nh, Np, device=dev, dtype=F32)
@@ -378,7 +389,8 @@ class Engine:
         # patch embedding + position embedding
         pe = vt + "embeddings."
         if self.rg(pe + "position_embedding.weight"):
-            ops.batch_sum(dx, B, d.n_img * d.vH, d.n_img * d.vH, self.gw(pe + "position_embedding.weight"), beta=beta)
+            ops.batch_sum(dx, B, d.img_tok * d.vH, d.img_tok * d.vH, self.gw(pe + "position_embedding.weight"),
+                          beta=beta)
         if self.rg(pe + "patch_embedding.bias"):
             ops.colsum(dx, self.gw(pe + "patch_embedding.bias"), ws, beta=beta)
         if self.rg(pe + "patch_embedding.weight"):

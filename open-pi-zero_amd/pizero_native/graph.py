@@ -24,7 +24,7 @@ class InferenceGraph:
         dev = model._dev()
         self.static = dict(
             ids=torch.zeros(bsz, d.P, device=dev, dtype=torch.int64),
-            pix=torch.zeros(bsz, 3, d.img, d.img, device=dev, dtype=torch.bfloat16),
+            pix=torch.zeros(bsz * d.n_images, 3, d.img, d.img, device=dev, dtype=torch.bfloat16),
             cnt=torch.full((bsz,), d.P, device=dev, dtype=torch.int32),
             vpos=torch.arange(1, d.P + 1, device=dev).repeat(bsz, 1),
             ppos=torch.arange(1, d.C + 1, device=dev).repeat(bsz, 1),
@@ -44,7 +44,7 @@ class InferenceGraph:
     def load(self, input_ids, pixel_values, cnt, vpos, ppos, apos, proprios, noise):
         s = self.static
         s["ids"].copy_(input_ids)
-        s["pix"].copy_(pixel_values)
+        s["pix"].copy_(pixel_values.reshape(s["pix"].shape))
         s["cnt"].copy_(cnt)
         s["vpos"].copy_(vpos)
         s["ppos"].copy_(ppos)

@@ -196,8 +196,14 @@ def siglip_forward(W, d, pixel_values):
 def embed_siglip_and_text(W, d, input_ids, pixel_values):
     """pizero.py:376-414: gather text rows, SigLIP+projector, /sqrt(hidden), merge."""
     emb = F.embedding(input_ids, W["embed_tokens.weight"])
-    img = siglip_forward(W, d, pixel_values)
+    # several images per sample (config C5, the Pi0-paper shape; the reference PiZero takes one image,
+    # pizero.py:389-413): SigLIP runs per image and the images' tokens are concatenated in image order
+    # into the sample's image-token slots -- an extension, pinned by composition, not by a reference run
+    B = input_ids.shape[0]
+    H = d["image_size"]
+    img = siglip_forward(W, d, pixel_values.reshape(-1, 3, H, H))
     img = linear(img, W, "multi_modal_projector.linear") / (d["vlm_hidden"] ** 0.5)
+    img = img.reshape(B, -1, img.shape[-1])
     out = torch.zeros_like(emb)
     text = (input_ids != d["image_token_index"]) & (input_ids != d["pad_token_id"])
     out = torch.where(text[..., None], emb, out)

@@ -114,7 +114,8 @@ def synth_inputs(cfg: dict, bsz: int, seed: int = 0, ragged: bool = False) -> di
         ids[b, n_img + n_text - 1] = 108 if vocab > 108 else 3
     attn = (ids != 0).astype(np.int64)
     H = cfg["image_size"]
-    pix = synth_tensor("pixel_values", (bsz, 3, H, H), 0.0, 1.0, seed)
+    n_images = cfg.get("num_images", 1)
+    pix = synth_tensor("pixel_values", (bsz, 3, H, H) if n_images == 1 else (bsz, n_images, 3, H, H), 0.0, 1.0, seed)
     prop = synth_tensor("proprios", (bsz, cfg["cond_steps"], cfg["proprio_dim"]), 0.0, 1.0, seed)
     act = synth_tensor("actions", (bsz, cfg["horizon_steps"], cfg["action_dim"]), 0.0, 1.0, seed)
     # x0 ~ approx N(0,1): sum of 4 uniforms scaled (deterministic, portable)

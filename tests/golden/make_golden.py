@@ -132,7 +132,7 @@ def ref_cfg(d):
         action_dim=d["action_dim"], proprio_dim=d["proprio_dim"],
         num_inference_steps=d["num_inference_steps"],
         final_action_clip_value=d["final_action_clip_value"],
-        flow_sig_min=d["flow_sig_min"], action_expert_adaptive_mode=None,
+        flow_sig_min=d["flow_sig_min"], action_expert_adaptive_mode=None, num_images=d.get("num_images", 1),
         time_hidden_size=256, time_max_period=d["time_max_period"],
         action_expert_rope_theta=d["act_theta"], mixture=mix,
         vision=dict(_target_="src.model.paligemma.siglip.SiglipVisionModel",

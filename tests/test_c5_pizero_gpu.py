@@ -1,0 +1,77 @@
+"""Config C5 at the PiZero level: several images per sample (the Pi0-paper shape: 3 images = 768 image
+tokens + text + 1 proprio + an action chunk of 50).
+
+The reference PiZero composes one image per sample (pizero.py:389-413), so a multi-image PiZero is an
+extension: SigLIP runs per image and each sample's images' tokens fill its image-token slots in image
+order.  Its parity is pinned by composition: (1) a tiny 3-image model against the fp32 oracle running
+the same composition (oracle/pizero_oracle.py embed_siglip_and_text), loss + every gradient (probe gate)
++ the action chunk; (2) the JointModel at the full C5 shape against the reference itself
+(tests/test_c5_gpu.py); (3) the full-size 3-image / chunk-50 inference path runs, in a hipGraph equal
+to eager.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from tests.oracle_helpers import O, oracle_run
+from tests.pizero_gpu_helpers import GRAD_COS, GRAD_REL, build_gpu_model, gpu_inputs, run_infer, run_loss
+
+pytestmark = pytest.mark.gpu
+
+TINY3 = dict(O.TINY_DIMS, num_images=3, num_image_tokens=48, max_seq_len=56, horizon_steps=6)
+C5_FULL = dict(O.FULL_DIMS, num_images=3, num_image_tokens=768, max_seq_len=788, horizon_steps=50)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def test_three_image_pizero_matches_oracle():
+    from tests.golden.gradprobe import compare, probe
+
+    d = TINY3
+    ref, _ = oracle_run(d, 2, ragged=True)
+    m = build_gpu_model(d)
+    gi = gpu_inputs(m, d, 2)
+    assert gi["pixel_values"].shape == (2, 3, 3, 56, 56)
+    loss = run_loss(m, gi).item()
+    assert abs(loss - ref["loss"]) <= 1e-2 * abs(ref["loss"]), (loss, ref["loss"])
+    params = dict(m.named_parameters())
+    bad = []
+    for n, gref in ref["grads"].items():
+        p = params.get(n)
+        if p is None or gref is None or not p.requires_grad or float(gref.norm()) == 0.0:
+            continue
+        if n.endswith("self_attn.k_proj.bias") and n.startswith("vision_tower"):
+            continue  # exact gradient 0 (softmax shift invariance): both sides are rounding noise
+        c = compare(probe(n, p.grad), probe(n, gref))
+        if c["rel"] > GRAD_REL or c["cos"] < GRAD_COS:
+            bad.append((n, c))
+    assert not bad, bad
+    a = run_infer(m, gi, clip=False).float().cpu().numpy()
+    err = np.abs(a - ref["actions"].numpy())
+    assert err.mean() <= 5e-3 and err.max() <= 3e-2, (err.mean(), err.max())
+
+
+def test_c5_full_shape_inference_graph_equals_eager():
+    """3 x 224^2 images (768 image tokens) + 20 text + 1 proprio, chunk 50, B=1, bf16: the hipGraph
+    replay equals the eager native path and the chunk is finite"""
+    from pizero_native.graph import InferenceGraph
+
+    d = C5_FULL
+    m = build_gpu_model(d)
+    m.eval()
+    gi = gpu_inputs(m, d, 1, ragged=False)
+    assert gi["input_ids"].shape == (1, 788) and gi["pixel_values"].shape[1] == 3
+    eager = run_infer(m, gi, clip=False)
+    assert eager.shape == (1, 50, 7) and torch.isfinite(eager.float()).all()
+    ig = InferenceGraph(m, 1, clip=False)
+    ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"],
+            gi["ppos"], gi["apos"], gi["proprios"].float(), gi["noise"])
+    ig.capture()
+    a = ig.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a.float(), eager.float())

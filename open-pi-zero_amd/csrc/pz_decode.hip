@@ -34,7 +34,8 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x, b = blockIdx.y;
   const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
-  const int cnt = a.cnt ? a.cnt[b] : nk;
+  const bool masked = a.cnt != nullptr;  // NULL: no mask (text generation, pizero.py:336-365)
+  const int cnt = masked ? a.cnt[b] : nk;
   const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
   const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
   const int j0 = c * DA_KC;
@@ -71,7 +72,7 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
       const int kl = kt * 16 + 4 * g + e;
       float x = acc[e] * a.scale;
       if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
-      const bool ok = rok && da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond);
+      const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
       S[row][kl] = ok ? x : -INFINITY;
     }
   }

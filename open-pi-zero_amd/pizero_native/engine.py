@@ -202,11 +202,17 @@ class Engine:
     def gu_w(self, p):
         return self.ar.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight")
 
-    def rope(self, theta):
+    def rope(self, theta, maxpos=None):
+        """fp32 cos|sin table for positions 0..maxpos (default L + 8: every training / action position);
+        text generation asks for longer tables (a new, power-of-two sized table: graphs captured on the
+        default one keep it)"""
         dev = self.ar.data.device
-        key = (float(theta), dev)
+        base = self.d.L + 8
+        if maxpos is not None and maxpos > base:
+            base = 1 << (int(maxpos) - 1).bit_length()
+        key = (float(theta), dev, base)
         if key not in self._tables:
-            maxpos = self.d.L + 8
+            maxpos = base
             cs = torch.empty((maxpos + 1) * self.d.hd, device=dev, dtype=F32)
             ops.rope_table(cs, maxpos, self.d.hd, theta)
             self._tables[key] = cs
@@ -919,6 +925,58 @@ class Engine:
                 x = X[g.name]
                 X[g.name] = self._post_attn(g, p, x, Pm, Vj, B, L1, Lp)
         return kcache, vcache
+
+    # ========================================================= text generation ==
+    def text_forward(self, ids, pix, pos, kc, vc, start, n_img, maxpos):
+        """PiZero.infer_text (pizero.py:559-593): the vlm mixture alone through all layers (cache_mode
+        "append", no last-layer skip, the all-zeros text mask of pizero.py:336-365 -> no masking), the
+        new tokens ids [B, q] written at cache rows [start, start + q) of kc / vc [nL, B, Lcap, hd] and
+        attending to rows [0, start + q); then the vlm final norm (if the mixture has one) and the
+        lm_head tied to embed_tokens (pizero.py:106-112).  pix / n_img: images of a prefill (None / 0
+        for decode steps).  maxpos: an upper bound of the positions (sizes the RoPE table).  Returns bf16
+        logits [B, q, vocab]."""
+        d = self.d
+        B, q = ids.shape
+        dev = ids.device
+        nh, hd = d.nh, d.hd
+        Lcap = kc.shape[2]
+        nk = start + q
+        table = self.w("embed_tokens.weight")
+        img = table if pix is None else self.siglip_forward(pix, None)
+        X = torch.empty(B * q, d.gH, device=dev, dtype=BF16)
+        ops.embed_merge(ids, table, img, X, n_img, d.image_token, d.pad_token, math.sqrt(d.gH), 1.0)
+        g = Group("vlm", "joint_model.mixtures.vlm.layers.", ["vlm"], q, 0, d.gH, d.gI, d.g_theta, False, "vlm")
+        Q = torch.empty(B, q, nh * hd, device=dev, dtype=BF16)
+        O = torch.empty(B * q, nh * hd, device=dev, dtype=BF16)
+        few = self.gemv_ok(B * q, d.gH) and q * nh <= 32
+        cs = self.rope(g.theta, maxpos)
+        x = X
+        for l in range(d.nL):
+            p = f"{g.prefix}{l}."
+            Kl, Vl = kc[l], vc[l]
+            if few:
+                ops.gemv_qkv_rope(x, self.qkv_w(p), pos, cs, Q, Kl, Vl, q, nh, hd, q, 0, Lcap, start,
+                                  norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                ops.decode_attn(Q, q, 0, Kl, Vl, O, B, nh, q, nk, 1.0 / math.sqrt(hd), 50.0, None, 0, 0, start)
+            else:
+                h = torch.empty_like(x)
+                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
+                qkv = torch.empty(B * q, (nh + 2) * hd, device=dev, dtype=BF16)
+                ops.linear(h, self.qkv_w(p), qkv)
+                ops.qkv_rope_split(qkv, pos, cs, Q, Kl, Vl, B, q, nh, 1, hd, q, 0, Lcap, start)
+                ops.flash_fwd(ops.flash_args(
+                    B, 1, q * nh, nk, hd, Q, (hd, q * nh * hd, 0), Kl, (hd, Lcap * hd, 0), Vl, (hd, Lcap * hd, 0),
+                    [(0, O, q * nh * hd, hd)], 0, None, 1.0 / math.sqrt(hd), cap=50.0, mask_mode=0,
+                    rows_per_token=nh, key_split=True))
+            x = self._post_attn_O(g, p, x, O)
+        nw = "joint_model.mixtures.vlm.norm.weight"
+        if nw in self.ar.slots:
+            y = torch.empty_like(x)
+            ops.rmsnorm(x, self.w(nw), y, None, d.rms_eps)
+            x = y
+        logits = torch.empty(B * q, table.shape[0], device=dev, dtype=BF16)
+        ops.linear(x, table, logits)
+        return logits.view(B, q, -1)
 
     def _kv_only_gemv(self, x, p, pos, g, Kj, Vj, L1, Lp):
         """last prefill layer, few rows: only the k|v projection (+RoPE on k) is consumed"""

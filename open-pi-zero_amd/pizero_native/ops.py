@@ -308,7 +308,8 @@ def decode_attn(q, Lq, qoff, k, v, o, B, nh, T, nk, scale, cap, cnt, prefix, con
     a.cnt, a.prefix, a.cond, a.qtok0 = _p(cnt), prefix, cond, qtok0
     need = lib().pz_decode_attn_ws_bytes(B, nk)
     ws = workspace(o.device)  # the GEMM split-K scratch: stream-ordered, not in use between kernels
-    assert ws.numel() * 4 >= need
+    if ws.numel() * 4 < need:
+        raise ValueError(f"decode_attn: {B} samples x {nk} keys need {need} B of workspace (> {ws.numel() * 4})")
     a.ws, a.ws_bytes = _p(ws), ws.numel() * 4
     call("pz_decode_attn", C.byref(a), _st())
 

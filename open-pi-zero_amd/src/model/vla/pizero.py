@@ -75,8 +75,6 @@ class PiZero(nn.Module, NoSyncBase):
         self.pad_token_id = cfg_get(cfg, "pad_token_id")
         self.image_token_index = cfg_get(cfg, "image_token_index")
         self.use_lm_head = cfg_get(cfg, "use_lm_head", False)
-        if self.use_lm_head:
-            raise NotImplementedError("use_lm_head / infer_text is out of scope this round (SURVEY 8(f) rank 4)")
         self.max_image_text_tokens = cfg_get(cfg, "max_image_text_tokens", cfg_get(cfg, "max_seq_len"))
         self.num_proprio_tokens = cfg_get(cfg, "cond_steps")
         self.num_action_tokens = cfg_get(cfg, "horizon_steps")
@@ -102,6 +100,8 @@ class PiZero(nn.Module, NoSyncBase):
             self.time_embedding = SinusoidalPosEmb(self.action_hidden_size, cfg_get(cfg, "time_max_period"))
             self.proprio_encoder = nn.Linear(self.proprio_dim, self.proprio_hidden_size)
             self.action_decoder = nn.Linear(self.action_hidden_size, self.action_dim)
+            if self.use_lm_head:  # optional text output (pizero.py:106-112), tied to embed_tokens
+                self.lm_head = nn.Linear(self.image_text_hidden_size, self.vocab_size, bias=False)
         self._tied = False
         self._eng = None
         self._kv = None
@@ -132,6 +132,8 @@ class PiZero(nn.Module, NoSyncBase):
                 gemma("proprio", l, "action")
         for n in ("action_encoder.linear_3", "action_encoder.linear_2", "action_encoder.linear_1", "proprio_encoder"):
             out += [(n + ".weight", "action"), (n + ".bias", "action")]
+        if hasattr(self.joint_model.mixtures["vlm"], "norm"):  # use_final_norm (text generation config)
+            out.append((mp + "vlm.norm.weight", "vlm"))
         for l in reversed(range(nL)):
             gemma("vlm", l, "vlm")
         out += [("multi_modal_projector.linear.weight", "vlm"), ("multi_modal_projector.linear.bias", "vlm")]
@@ -161,6 +163,7 @@ class PiZero(nn.Module, NoSyncBase):
             binds[name] = (mod, attr, p.requires_grad)
         self._arena = Arena(entries, device, dtype)
         self._arena.bind(binds)
+        self._tie_lm_head()
         self._pmap = {name: _resolve(self, name) for name, _ in self._layout()}
         if init == "default":
             self._init_weights()
@@ -201,9 +204,15 @@ class PiZero(nn.Module, NoSyncBase):
         rg = {n: self._pmap[n][0]._parameters[self._pmap[n][1]].requires_grad for n in self._pmap}
         self._arena.apply(fn)
         self._arena.bind({n: (m, a, rg[n]) for n, (m, a) in self._pmap.items()})
+        self._tie_lm_head()
         self._eng = None
         self._kv = None
         return self
+
+    def _tie_lm_head(self):
+        """pizero.py:112: lm_head.weight IS embed_tokens.weight (one arena tensor, two state_dict keys)"""
+        if getattr(self, "use_lm_head", False) and hasattr(self, "lm_head"):
+            self.lm_head._parameters["weight"] = self.embed_tokens._parameters["weight"]
 
     def _param(self, name):
         m, a = self._pmap[name]
@@ -524,8 +533,64 @@ class PiZero(nn.Module, NoSyncBase):
         return self.infer_action(input_ids, pixel_values, itp, amask, vlm_position_ids, proprio_position_ids,
                                  action_position_ids, proprios, noise=noise, clip=clip)
 
-    def infer_text(self, *args, **kwargs):
-        raise NotImplementedError("text generation (infer_text) is out of scope this round (SURVEY 8(f) rank 4)")
+    def build_causal_mask_and_position_ids_for_text(self, q_len, attention_mask, kv_cache=None):
+        """pizero.py:336-365: the all-zeros text mask (no masking: prefix-LM prefill, cached decode) and the
+        positions cumsum(attention_mask) (pads -> 1; a cached decode step takes the last one).  The
+        reference reads an undefined global ``bsz`` here; the batch size comes from attention_mask."""
+        bsz = attention_mask.shape[0]
+        dtype, device = attention_mask.dtype, attention_mask.device
+        if kv_cache is None or kv_cache.num_items() == 0:
+            mask = torch.zeros(bsz, q_len, q_len, dtype=dtype, device=device)
+        else:
+            if q_len != 1:
+                raise ValueError("Using KV cache so should only use one single token")
+            mask = torch.zeros(bsz, q_len, kv_cache.num_items() + q_len, dtype=dtype, device=device)
+        mask = mask.unsqueeze(1)
+        if kv_cache is not None and kv_cache.num_items() > 0:
+            pos = attention_mask.cumsum(-1)[:, -1:]
+        else:
+            pos = attention_mask.cumsum(-1).masked_fill_(attention_mask == 0, 1)
+        return mask, pos
+
+    @torch.no_grad()
+    def infer_text(self, input_ids, pixel_values, attention_mask, kv_cache: Optional[KVCache] = None):
+        """pizero.py:559-593: {"logits": [B, q_len, vocab]} (+ "kv_cache").  The prompt prefill runs the
+        vlm mixture over q_len tokens (image tokens merged from SigLIP); each later call feeds ONE new
+        token that attends to the cache.  ``kv_cache`` is this repo's static KVCache (rows appended in
+        place, grown when full); ``None`` -> a standalone prefill, like the reference."""
+        if not self.use_lm_head:
+            raise RuntimeError("infer_text needs use_lm_head: true (pizero.py:106-112)")
+        dev = self._dev()
+        ids = input_ids.to(dev, torch.int64).contiguous()
+        B, q = ids.shape
+        am = attention_mask.to(dev)
+        _, pos = self.build_causal_mask_and_position_ids_for_text(q, am, kv_cache)
+        eng = self._engine()
+        d = eng.d
+        cache = kv_cache if kv_cache is not None else KVCache()
+        start = cache.num_items()
+        if start == 0:
+            cap = (q + 256 + 7) // 8 * 8
+            cache.allocate(d.nL, B, cap, d.hd, dev)
+        elif start + q > cache.k.shape[2]:  # grow (amortised) keeping the cached rows
+            old_k, old_v = cache.k, cache.v
+            cache.k = torch.zeros(d.nL, B, (start + q + 256 + 7) // 8 * 8, d.hd, device=dev, dtype=old_k.dtype)
+            cache.v = torch.zeros_like(cache.k)
+            cache.k[:, :, :start].copy_(old_k[:, :, :start])
+            cache.v[:, :, :start].copy_(old_v[:, :, :start])
+        n_img = int((ids == self.image_token_index).sum(1).max().item()) if start == 0 else 0
+        pix = None
+        if n_img:
+            pix = pixel_values.to(dev, torch.bfloat16).contiguous()
+            n_img = d.n_img
+        # positions are cumsum(attention_mask) <= its length (pizero.py:363-371): bounds the RoPE table
+        logits = eng.text_forward(ids, pix, pos.to(torch.int64).contiguous(), cache.k, cache.v, start, n_img,
+                                  maxpos=am.shape[1])
+        cache.length = start + q
+        out = {"logits": logits}
+        if kv_cache is not None:
+            out["kv_cache"] = kv_cache
+        return out
 
 
 class PiZeroInference(PiZero):

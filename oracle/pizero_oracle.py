@@ -96,7 +96,7 @@ def param_shapes(d: dict) -> dict:
             s[p + "mlp.down_proj.weight"] = (hid, inter)
             s[p + "input_layernorm.weight"] = (hid,)
             s[p + "post_attention_layernorm.weight"] = (hid,)
-        if mix != "vlm":
+        if mix != "vlm" or d.get("vlm_final_norm"):
             s[f"joint_model.mixtures.{mix}.norm.weight"] = (hid,)
     A, Ah = d["action_dim"], d["act_hidden"]
     s["action_encoder.linear_1.weight"] = (Ah, A)
@@ -128,6 +128,8 @@ def synth_weights(d: dict, seed: int = 0) -> dict:
     for k in list(W):
         if ".mixtures.action." in k:
             W[k.replace(".mixtures.action.", ".mixtures.proprio.")] = W[k]
+    if d.get("use_lm_head"):
+        W["lm_head.weight"] = W["embed_tokens.weight"]  # tied (pizero.py:112)
     return W
 
 
@@ -410,3 +412,33 @@ def pizero_infer_naive(W, d, input_ids, pixel_values, causal_mask, vlm_pos,
         c = d["final_action_clip_value"]
         a = torch.clamp(a, -c, c)
     return a
+
+
+# ------------------------------------------------------ text generation ----
+
+
+def text_positions(attention_mask):
+    """pizero.py:336-365: positions cumsum(attention_mask), pads -> 1."""
+    return attention_mask.cumsum(-1).masked_fill(attention_mask == 0, 1)
+
+
+def pizero_infer_text(W, d, input_ids, pixel_values, attention_mask, new_tokens):
+    """pizero.py:559-593 with a KV cache, teacher-forced with ``new_tokens`` [B, n] (the tokens fed back
+    after the prefill).  The cached run's semantics as one masked pass: prompt tokens attend to the
+    whole prompt (the all-zeros prefill mask), generated token k to the prompt and generated tokens
+    <= k (what the cache holds when it is fed); positions cumsum(mask) for the prompt, count + 1 + k
+    for generated token k.  Returns logits [B, q + n, vocab] (rows q-1.. are the next-token logits)."""
+    B, q = input_ids.shape
+    n = new_tokens.shape[1]
+    emb = embed_siglip_and_text(W, d, input_ids, pixel_values)
+    gen = F.embedding(new_tokens, W["embed_tokens.weight"])
+    x = torch.cat([emb, gen], dim=1)
+    pos = torch.cat([text_positions(attention_mask),
+                     attention_mask.sum(-1, keepdim=True) + 1 + torch.arange(n)[None, :]], dim=1)
+    N = q + n
+    i = torch.arange(N)[:, None]
+    j = torch.arange(N)[None, :]
+    allowed = (j < q) & (i < q) | (i >= q) & ((j < q) | (j <= i))
+    mask = torch.where(allowed, 0.0, torch.finfo(torch.float32).min)[None, None].expand(B, 1, N, N)
+    h = joint_forward(W, d, {"vlm": x}, {"vlm": pos}, mask, skip_last=())["vlm"]
+    return F.linear(h, W["embed_tokens.weight"])

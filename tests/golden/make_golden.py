@@ -112,10 +112,11 @@ def install_stubs():
 
 
 def ref_cfg(d):
-    """bridge.yaml-shaped config (config/train/bridge.yaml:68-181) from dims."""
+    """bridge.yaml-shaped config (config/train/bridge.yaml:68-181) from dims (text generation:
+    use_lm_head + the vlm final norm, as pizero.py:712-714 sets them)."""
     mix = {
         "vlm": dict(hidden_size=d["vlm_hidden"], intermediate_size=d["vlm_inter"],
-                    use_final_norm=False, cache=True, use_quantize=False, use_lora=False,
+                    use_final_norm=bool(d.get("vlm_final_norm", False)), cache=True, use_quantize=False, use_lora=False,
                     adaptive_mode=None, rope_theta=d["vlm_theta"]),
         "proprio": dict(hidden_size=d["act_hidden"], intermediate_size=d["act_inter"],
                         use_final_norm=True, cache=True, use_quantize=False, use_lora=False,
@@ -126,7 +127,7 @@ def ref_cfg(d):
     }
     c = dict(
         vocab_size=d["vocab_size"], pad_token_id=d["pad_token_id"],
-        image_token_index=d["image_token_index"], use_lm_head=False,
+        image_token_index=d["image_token_index"], use_lm_head=bool(d.get("use_lm_head", False)),
         max_seq_len=d["max_seq_len"], max_image_text_tokens=d["max_seq_len"],
         cond_steps=d["cond_steps"], horizon_steps=d["horizon_steps"],
         action_dim=d["action_dim"], proprio_dim=d["proprio_dim"],
@@ -383,6 +384,65 @@ def make_time_embed():
     np.savez_compressed(os.path.join(ROOT, "tests", "golden", "time_embed.npz"), **out)
     print("wrote time_embed.npz")
 
+
+TEXT_NEW = 6  # tokens generated after the prefill
+
+
+def make_text():
+    """Greedy text generation through the reference's infer_text with its KV cache (the loop of
+    pizero.py:763-790, batched: B=2 ragged prompts, no stop token), TINY_DIMS + lm_head + vlm final
+    norm, fp32 and bf16.  Stores the prefill logits, every step's logits and the generated tokens.
+    The reference's build_causal_mask_and_position_ids_for_text reads a module-global ``bsz``
+    (pizero.py:349, set by its __main__ block); it is set here the same way."""
+    install_stubs()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    from src.model.vla import pizero as pz
+
+    d = dict(TINY_DIMS, use_lm_head=True, vlm_final_norm=True)
+    torch.set_num_threads(os.cpu_count() or 8)
+    W = synth_weights(d, seed=0)
+    B = 2
+    inp = synth_inputs(d, B, seed=3, ragged=True)
+    res = {}
+    for tag, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        torch.manual_seed(0)
+        model = pz.PiZero(ref_cfg(d))
+        model.tie_action_proprio_weights()
+        sd = model.state_dict()
+        assert set(sd) == set(param_shapes(d)) | {"lm_head.weight"}, set(sd) ^ set(param_shapes(d))
+        model.load_state_dict({k: W[k] for k in sd}, strict=True)
+        assert model.lm_head.weight is model.embed_tokens.weight
+        model.to(dt).eval()
+        pz.bsz = B
+        ids = torch.from_numpy(inp["input_ids"])
+        am = torch.from_numpy(inp["attention_mask"])
+        pix = torch.from_numpy(inp["pixel_values"]).to(dt)
+        cache = model.build_text_cache()
+        steps, toks = [], []
+        with torch.inference_mode():
+            for k in range(TEXT_NEW + 1):
+                o = model.infer_text(input_ids=ids, pixel_values=pix, attention_mask=am, kv_cache=cache)
+                lg = o["logits"].float()
+                if k == 0:
+                    res[f"{tag}/prefill_logits"] = lg.numpy()
+                else:
+                    steps.append(lg[:, -1].numpy())
+                nxt = lg[:, -1].argmax(-1, keepdim=True)
+                toks.append(nxt.numpy())
+                ids = nxt
+                am = torch.cat([am, torch.ones(B, 1, dtype=am.dtype)], dim=-1)
+        res[f"{tag}/step_logits"] = np.stack(steps, 1)
+        res[f"{tag}/tokens"] = np.concatenate(toks, 1)
+        print(f"[text] {tag} tokens", res[f"{tag}/tokens"].tolist(), flush=True)
+    res["in/input_ids"] = inp["input_ids"]
+    res["in/attention_mask"] = inp["attention_mask"]
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "text.npz"), **res)
+    print("wrote text.npz")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "text":
+    make_text()
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lr":
     make_lr()

@@ -74,3 +74,31 @@ def test_actions_cached_and_naive(tiny):
 def test_reference_bf16_deviation_recorded(tiny):
     g, _, _ = tiny
     assert abs(float(g["bf16/loss"]) - float(g["fp32/loss"])) < 0.05 * abs(float(g["fp32/loss"]))
+
+
+TEXT_DIMS = dict(O.TINY_DIMS, use_lm_head=True, vlm_final_norm=True)
+
+
+def test_infer_text_matches_reference():
+    """infer_text (pizero.py:559-593) with the reference's KV-cache greedy loop (tests/golden/text.npz):
+    the oracle's one-pass restatement, teacher-forced with the reference's tokens, gives the same
+    prefill logits and per-step logits, and greedy argmax reproduces the reference's tokens"""
+    from oracle.synth import synth_inputs
+
+    g = load_golden("text")
+    W = O.synth_weights(TEXT_DIMS, seed=0)
+    assert W["lm_head.weight"] is W["embed_tokens.weight"]
+    inp = synth_inputs(TEXT_DIMS, 2, seed=3, ragged=True)
+    np.testing.assert_array_equal(g["in/input_ids"], inp["input_ids"])
+    toks = torch.from_numpy(g["fp32/tokens"])
+    n = toks.shape[1] - 1
+    with torch.no_grad():
+        lg = O.pizero_infer_text(W, TEXT_DIMS, torch.from_numpy(inp["input_ids"]),
+                                 torch.from_numpy(inp["pixel_values"]), torch.from_numpy(inp["attention_mask"]),
+                                 toks[:, :n])
+    q = inp["input_ids"].shape[1]
+    pre, steps = g["fp32/prefill_logits"], g["fp32/step_logits"]
+    scale = np.abs(pre).max()
+    np.testing.assert_allclose(lg[:, :q].numpy(), pre, rtol=0, atol=1e-4 * scale)
+    np.testing.assert_allclose(lg[:, q:].numpy(), steps, rtol=0, atol=1e-4 * scale)
+    assert torch.equal(lg[:, q - 1:].argmax(-1), toks)

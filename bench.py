@@ -173,27 +173,36 @@ def c5_inference(cfg, dev, iters):
     pix = (torch.rand(1, 3, 3, d.img, d.img, generator=gen) * 2 - 1).to(dev, torch.bfloat16)
     prop = (torch.rand(1, 1, d.Pd, generator=gen) * 2 - 1).to(dev)
     noise = torch.randn(1, d.H, d.A, device=dev)
-    g = InferenceGraph(m, 1)
-    g.load(ids.to(dev), pix, m.block_prefix_counts(itp.to(dev), amask.to(dev)), vpos.to(dev), ppos.to(dev),
-           apos.to(dev), prop, noise)
-    g.capture()
-    for _ in range(3):
-        g.replay()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    e0.record()
-    for _ in range(iters):
-        g.replay()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    del g, m
+    def timed():
+        g = InferenceGraph(m, 1)
+        g.load(ids.to(dev), pix, m.block_prefix_counts(itp.to(dev), amask.to(dev)), vpos.to(dev), ppos.to(dev),
+               apos.to(dev), prop, noise)
+        g.capture()
+        for _ in range(3):
+            g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record()
+        for _ in range(iters):
+            a = g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / iters, a.float().clone()
+
+    ms, a16 = timed()
+    m.use_fp8_inference(True)  # BASELINE configs[4]: fp8 MFMA attention / MLP GEMMs
+    ms8, a8 = timed()
+    rel = float((a8 - a16).norm() / a16.norm())
+    del m
     torch.cuda.empty_cache()
-    return {"metric": "bf16 action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
+    return {"metric": "action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
                       "1 proprio, chunk 50, B=1, prefill + 10 Euler steps)",
-            "graph_ms": ms, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
+            "graph_ms": ms, "dtype": "bf16", "fp8_graph_ms": ms8,
+            "fp8": "e4m3 weights (per-tensor scales) for every SigLIP / vlm / action-expert Linear: prefill W8A8 "
+                   "on the fp8 MFMA (per-row activation scales), denoise W8A16",
+            "fp8_vs_bf16_chunk_rel_l2": rel, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
             "baseline_source": "Pi0 paper figure quoted in the reference README.md:80,84 (other hardware)",
-            "vs_baseline": 73.0 / ms, "dtype": "bf16"}
+            "vs_baseline": 73.0 / ms, "fp8_vs_baseline": 73.0 / ms8}
 
 
 def main():

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 10
+#define PZ_ABI_VERSION 11
 
 enum {
   PZ_OK = 0,
@@ -73,11 +73,31 @@ typedef struct pz_gemm_args {
   void* workspace; int64_t ws_bytes;
   /* optional fused Gemma RMSNorm of the A rows (paligemma/modules.py:7-21): A is the raw x and
    * the product uses x*rsqrt(mean_k(x^2)+norm_eps)*(1+norm_w[k]) (norm_w bf16 [K]).  Only for
-   * the few-row path (M <= 16, k-contiguous A and B, K % 32 == 0: inference denoise rows);
+   * the few-row paths (M <= 16 with K % 32 == 0, or 16 < M <= 64 with K % 64 == 0; k-contiguous
+   * A and B: inference denoise rows);
    * PZ_ERR_ARG otherwise.  NULL disables. */
   const void* norm_w; float norm_eps;
+  /* fp8 operands (OCP e4m3fn codes, one byte each; K, lda, ldb count codes):
+   *   0 = bf16 A and B;
+   *   1 = W8A8: fp8 A [M][K] and B [N][K], both k-contiguous, batch 1, K / lda / ldb % 16 == 0,
+   *       forward epilogues (none / GeGLU / GELU / SiLU, bias, resid), no fused norm; the product
+   *       is alpha * a_row_scale[m] * sum_k A*B (alpha = the weight scale; a_row_scale fp32 [M]
+   *       from pz_fp8_quant_rows, NULL = 1).  Runs the 256-tile 8-phase kernel at the fp8 MFMA rate;
+   *   2 = W8A16: bf16 A rows (M <= 64, optional fused RMSNorm), fp8 B [N][K] expanded to bf16 in
+   *       registers, product * alpha (= the weight scale); K % 64 == 0, ldb % 16 == 0. */
+  int32_t fp8_mode; const float* a_row_scale;
 } pz_gemm_args;
 int pz_gemm(const pz_gemm_args* args, void* stream);
+/* fp8 (OCP e4m3fn) quantisation for fp8_mode 1 / 2 (C5, BASELINE.json configs[4]):
+ * pz_fp8_quant_rows: per row r of bf16 x [R, D] (ldx): s = max_k |x[r,k]| / 448 (1 for an all-zero
+ *   row), q[r,k] = e4m3(x[r,k] / s) (round to nearest even), row_scale[r] = s.  D % 8 == 0, D <= 16384.
+ * pz_fp8_quant_tensor: q[i] = e4m3(x[i] * inv_scale) for n bf16 elements (n % 8 == 0): weights, with
+ *   the per-tensor scale max|W| / 448 from pz_fp8_absmax (PZ_ABSMAX_PARTS fp32 partial maxima). */
+#define PZ_ABSMAX_PARTS 1024
+int pz_fp8_quant_rows(const void* x, int64_t ldx, void* q, int64_t ldq, float* row_scale, int64_t R, int64_t D,
+                      void* stream);
+int pz_fp8_quant_tensor(const void* x, int64_t n, void* q, float inv_scale, void* stream);
+int pz_fp8_absmax(const void* x, int64_t n, float* parts, void* stream);
 /* name of the kernel pz_gemm would launch for args (profiling / bench labels); never fails */
 const char* pz_gemm_kernel_name(const pz_gemm_args* args);
 

@@ -50,7 +50,16 @@ struct GemmP {
   // fused Gemma RMSNorm of the A rows (skinny path only): bf16 (1 + w) weights [K] or NULL
   const bf16_t* nw;
   float neps;
+  // fp8 W8A8 (gemm8p_f8_kernel): per-row activation scales [M] or NULL
+  const float* rs;
 };
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+// two bf16-shaped fragments (8 x 16 bit each = 16 fp8 codes) -> one 32-code f8f6f4 operand
+__device__ __forceinline__ i32x8 cat_f8(const bf16x8& lo, const bf16x8& hi) {
+  const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
+  return i32x8{(int)a[0], (int)a[1], (int)a[2], (int)a[3], (int)b[0], (int)b[1], (int)b[2], (int)b[3]};
+}
 
 __device__ __forceinline__ int sw_tr(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
 
@@ -1230,8 +1239,16 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
   }
 }
 
-template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
-__global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
+// F8: fp8 (OCP e4m3) A and B, both k-contiguous, staged by the same byte-identical pipeline: the
+// caller passes K, lda, ldb in units of 2 codes ("bf16-sized" elements), so a 64-unit K-tile is 128
+// codes, and each (row block, column block) of a K-tile is ONE v_mfma_f32_16x16x128_f8f6f4 on the two
+// bf16-shaped fragments of that tile concatenated (lane group g: codes 16g..16g+15 and 64+16g..
+// 64+16g+15 of the tile on BOTH operands -- the same k set, so the sum is the plain dot product) at
+// twice the bf16 MFMA rate.  The per-row activation scale (p.rs) multiplies the accumulators after
+// the main loop (before the split-tail partials are written, so the tail sum stays linear); the
+// weight scale is alpha.
+template <bool AKC, bool BKC, bool GEGLU, bool KTAIL, bool F8>
+__device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
@@ -1338,14 +1355,24 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
   };
   auto mfma_quad = [&](int ah, int bh) {
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    if (F8) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[ah * 4 + i][bh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[bh][j][kk], af[i][kk], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+          acc[ah * 4 + i][bh * 2 + j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              cat_f8(bf[bh][j][0], bf[bh][j][1]), cat_f8(af[i][0], af[i][1]), acc[ah * 4 + i][bh * 2 + j], 0, 0, 0, 0,
+              0, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[ah * 4 + i][bh * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[bh][j][kk], af[i][kk], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -1440,6 +1467,15 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
     PZ_RAW_BARRIER();
   }
   if (wr == 0) PZ_RAW_BARRIER();
+  if (F8 && p.rs) {  // per-row activation scale: lane rows m0 + wr*128 + 16 rb + (lane & 15)
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      const int64_t row = min(m0 + wr * 128 + 16 * rb + (lane & 15), p.M - 1);
+      const float sr = p.rs[row];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[rb][cb] *= sr;
+    }
+  }
 
   if (piece >= 0) {  // split tail: raw partial sums, summed + epilogued by gemm8p_tail_epilogue
     f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)piece * (32 * NT2);
@@ -1450,6 +1486,17 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
     return;
   }
   epilogue8p<GEGLU>(p, zo * p.sCo + zi * p.sCi, zo * p.sRo + zi * p.sRi, m0, n0, wr, wc, lane, acc, smem);
+}
+
+template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
+__global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
+  gemm8p_body<AKC, BKC, GEGLU, KTAIL, false>(p);
+}
+
+// fp8 e4m3 x e4m3 (W8A8) instantiation of the 8-phase kernel (C5 prefill MLP GEMMs)
+template <bool GEGLU, bool KTAIL>
+__global__ void __launch_bounds__(NT2, 1) gemm8p_f8_kernel(GemmP p) {
+  gemm8p_body<true, true, GEGLU, KTAIL, true>(p);
 }
 
 // ---- k-half variant of the ping-pong kernel -----------------------------------
@@ -1818,6 +1865,199 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
 }
 
 // -------------------------------------------------------------------------
+// Skinny GEMM for 16 < M <= 64 rows, and for fp8 (OCP e4m3) weights at M <= 64 (W8A16): the C5
+// denoise steps (an action chunk of 50 rows per sample).  The scheme of gemm_skinny_kernel -- W waves
+// per NC output columns, K split into W contiguous ranges, weights streamed once into VGPRs, LDS
+// reduction -- with MB 16-row blocks sharing every weight fragment (MB MFMAs per fragment; the
+// activation rows are re-read from L2 by every block).  K is walked in 64-k chunks: lane group g
+// takes k = 64c + 16g + [0, 16) of A (two bf16x8) and of B (two bf16x8, or ONE 16-byte load of fp8
+// codes expanded in registers by v_cvt_scalef32_pk_bf16_fp8 -- exact, every e4m3 value is a bf16);
+// the chunk's two MFMAs sum over k = 64c + 16g + [0, 8) and [8, 16), g = 0..3: the same k set on
+// both operands, so the sum is the plain dot product.  The weight scale of fp8 codes is alpha.
+// Requires K % 64 == 0, k-contiguous A and B, batch 1.
+// -------------------------------------------------------------------------
+__device__ __forceinline__ void fp8x16_to_bf16(const u32x4 q, bf16x8& lo, bf16x8& hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 h[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[2 * e] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, false);
+    h[2 * e + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, true);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    lo[2 * e] = h[e][0];
+    lo[2 * e + 1] = h[e][1];
+    hi[2 * e] = h[4 + e][0];
+    hi[2 * e + 1] = h[4 + e][1];
+  }
+}
+
+template <int W, int NC, int MB, bool F8W>
+__global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
+  static_assert(W >= MB, "one wave per row block in the epilogue");
+  constexpr int U = MB >= 3 ? 2 : 4;  // 64-k chunks per load batch (register budget: A is MB x 8 VGPRs)
+  __shared__ f32x4 red[W][MB][64];
+  __shared__ float redn[W][MB][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const bool geglu = p.epi == PZ_EPI_GEGLU;
+  const bool nrm = p.nw != nullptr;
+  const int64_t ncols = geglu ? p.geglu_I : p.N;
+  const int64_t n0 = (int64_t)blockIdx.x * NC;
+  const int64_t nr = n0 + (lane & 15) % NC;
+  const bool nok = nr < ncols;
+  constexpr int ES = F8W ? 1 : 2;  // weight element bytes
+  const char* Bc = reinterpret_cast<const char*>(p.B);
+  const char* Brow = Bc + (nr * p.ldb + 16 * g) * ES;
+  const char* Brow2 = Bc + ((p.geglu_I + nr) * p.ldb + 16 * g) * ES;
+  const bf16_t* Arow[MB];
+  bool mok[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int64_t m = mb * 16 + (lane & 15);
+    mok[mb] = m < p.M;
+    Arow[mb] = p.A + m * p.lda + 16 * g;
+  }
+  const bf16_t* Wn = p.nw + 16 * g;
+  f32x4 acc[MB], acc2[MB];
+  float ss[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    acc[mb] = acc2[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ss[mb] = 0.f;
+  }
+  const int64_t kchunks = p.K / 64;
+  const int64_t per = (kchunks + W - 1) / W;
+  const int64_t kb = wave * per, ke = min(kchunks, kb + per);
+  auto load_b = [&](const char* row, int64_t c, bf16x8& lo, bf16x8& hi) {
+    if (!nok) {
+      lo = hi = bf16x8{};
+    } else if (F8W) {
+      fp8x16_to_bf16(*reinterpret_cast<const u32x4*>(row + c * 64), lo, hi);
+    } else {
+      lo = *reinterpret_cast<const bf16x8*>(row + c * 128);
+      hi = *reinterpret_cast<const bf16x8*>(row + c * 128 + 16);
+    }
+  };
+  int64_t kc = kb;
+  auto run = [&](auto U_) {
+    constexpr int UU = decltype(U_)::value;
+    for (; kc + UU <= ke; kc += UU) {
+      bf16x8 a[UU][MB][2], b[UU][2], b2[UU][2], wv[UU][2];
+      u32x4 braw[UU], braw2[UU];
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
+        if (F8W) {  // raw codes first (all loads in flight), expanded after the A loads are issued
+          braw[u] = nok ? *reinterpret_cast<const u32x4*>(Brow + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+          if (geglu) braw2[u] = nok ? *reinterpret_cast<const u32x4*>(Brow2 + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+        } else {
+          load_b(Brow, kc + u, b[u][0], b[u][1]);
+          if (geglu) load_b(Brow2, kc + u, b2[u][0], b2[u][1]);
+        }
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            a[u][mb][h] = mok[mb] ? *reinterpret_cast<const bf16x8*>(Arow[mb] + (kc + u) * 64 + 8 * h) : bf16x8{};
+        if (nrm)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) wv[u][h] = *reinterpret_cast<const bf16x8*>(Wn + (kc + u) * 64 + 8 * h);
+      }
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
+        if (F8W) {
+          fp8x16_to_bf16(braw[u], b[u][0], b[u][1]);
+          if (geglu) fp8x16_to_bf16(braw2[u], b2[u][0], b2[u][1]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            if (nrm) {  // sum of squares of the raw row; the product takes x * (1 + w), rsqrt applied after
+              const u32x4 xa = __builtin_bit_cast(u32x4, a[u][mb][h]), xw = __builtin_bit_cast(u32x4, wv[u][h]);
+              u32x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x0 = __uint_as_float(xa[e] << 16), x1 = __uint_as_float(xa[e] & 0xffff0000u);
+                const float w0 = __uint_as_float(xw[e] << 16), w1 = __uint_as_float(xw[e] & 0xffff0000u);
+                ss[mb] += x0 * x0 + x1 * x1;
+                o[e] = pack2bf(x0 * (1.f + w0), x1 * (1.f + w1));
+              }
+              a[u][mb][h] = __builtin_bit_cast(bf16x8, o);
+            }
+            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][h], a[u][mb][h], acc[mb], 0, 0, 0);
+            if (geglu) acc2[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[u][h], a[u][mb][h], acc2[mb], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+  run(std::integral_constant<int, U>{});
+  run(std::integral_constant<int, 1>{});
+  // D[n_local = 4g + r][m = mb*16 + (lane & 15)]; wave w < MB finishes row block w
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    red[wave][mb][lane] = acc[mb];
+    if (nrm) {
+      float t = ss[mb];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if (lane < 16) redn[wave][mb][lane] = t;
+    }
+  }
+  __syncthreads();
+  const int mb = wave;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f}, o2 = {0.f, 0.f, 0.f, 0.f};
+  if (mb < MB)
+    for (int w = 0; w < W; ++w) o += red[w][mb][lane];
+  if (geglu) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < MB; ++b) red[wave][b][lane] = acc2[b];
+    __syncthreads();
+    if (mb < MB)
+      for (int w = 0; w < W; ++w) o2 += red[w][mb][lane];
+  }
+  if (mb >= MB) return;
+  const int64_t mm = mb * 16 + (lane & 15);
+  if (mm >= p.M) return;
+  float scale = p.alpha;
+  if (nrm) {
+    float t = 0.f;
+    for (int w = 0; w < W; ++w) t += redn[w][mb][lane & 15];
+    scale *= rsqrtf(t / (float)p.K + p.neps);
+  }
+  const int64_t n = n0 + 4 * g;
+  for (int r = 0; r < 4; ++r) {
+    const int64_t nn = n + r;
+    if (4 * g + r >= NC || nn >= ncols) continue;
+    float x = o[r] * scale;
+    if (geglu) {
+      const float gg = x, u = o2[r] * scale;
+      if (p.aux) {
+        p.aux[mm * p.ld_aux + nn] = f2bf(gg);
+        p.aux[mm * p.ld_aux + p.geglu_I + nn] = f2bf(u);
+      }
+      x = gelu_tanh(gg) * u;
+    } else {
+      if (p.bias) x += bf2f(p.bias[nn]);
+      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+        if (p.aux) p.aux[mm * p.ld_aux + nn] = f2bf(x);
+        x = p.epi == PZ_EPI_GELU ? gelu_tanh(x) : silu(x);
+      }
+      if (p.resid) x += bf2f(p.resid[mm * p.ld_resid + nn]);
+    }
+    if (p.c_fp32) {
+      float* Cp = reinterpret_cast<float*>(p.C) + mm * p.ldc + nn;
+      *Cp = p.beta ? *Cp + x : x;
+    } else {
+      bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + mm * p.ldc + nn;
+      *Cp = f2bf(p.beta ? bf2f(*Cp) + x : x);
+    }
+  }
+}
+
+// -------------------------------------------------------------------------
 // Small strided fp32-accumulate GEMM for the K=7 / N=7 action/proprio linears
 // (SURVEY 2.2 "proprio enc / action dec": 0.03 GF).  One thread per output.
 // -------------------------------------------------------------------------
@@ -1932,11 +2172,11 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64 };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
-  int wm, tag, skinny_w, skinny_nc, splits;
+  int wm, tag, skinny_w, skinny_nc, skinny_mb, splits;
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
 };
@@ -1989,6 +2229,35 @@ Plan make_plan(const pz_gemm_args* a) {
   pl.bkc = a->b_kcontig != 0;
   pl.geglu = a->epilogue == PZ_EPI_GEGLU;
   const int64_t ncols = pl.geglu ? a->geglu_inter : a->N;
+  // fp8 W8A8: the 8-phase 256-tile kernel on code pairs (K, lda, ldb halved by the caller of make_plan)
+  if (a->fp8_mode == 1) {
+    pl.kind = PATH_256;
+    pl.tiles_m = (a->M + BT - 1) / BT;
+    pl.tiles_n = (ncols + (pl.geglu ? BT / 2 : BT) - 1) / (pl.geglu ? BT / 2 : BT);
+    plan_tail(pl, a);
+    return pl;
+  }
+  // skinny-64 path: 16 < M <= 64 rows (bf16), or any M <= 64 with fp8 weights (W8A16)
+  const bool sk64_ok = a->M <= 64 && pl.akc && pl.bkc && a->K % 64 == 0 && a->batch == 1 && !a->c_fp32 &&
+                       a->epilogue < PZ_EPI_DGELU;
+  if (a->fp8_mode == 2 || (sk64_ok && a->M > 16)) {
+    pl.kind = PATH_SKINNY64;
+    pl.skinny_mb = (int)((a->M + 15) / 16);
+    pl.skinny_mb = pl.skinny_mb == 3 ? 4 : pl.skinny_mb;
+    // 16 real columns per block, 8 waves: every block re-reads the (L2-resident) activation rows, so
+    // narrower blocks multiply that traffic -- measured at 50 rows (tools/skinny_bench.py): q|k|v
+    // 7.3 vs 16.8 us, gate|up 8.6 vs 25.6 us for 16 vs 4 columns; W = 8 never slower than 4
+    pl.skinny_w = a->K / 64 >= 8 ? 8 : 4;
+    pl.skinny_nc = 16;
+    {  // A/B overrides (read per call): PZ_SK64_NC = 4|8|16 columns per block, PZ_SK64_W = 4|8 waves
+      const char* e = getenv("PZ_SK64_NC");
+      if (e && (atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) pl.skinny_nc = atoi(e);
+      e = getenv("PZ_SK64_W");
+      if (e && (atoi(e) == 4 || atoi(e) == 8)) pl.skinny_w = atoi(e);
+    }
+    pl.tiles_n = (ncols + pl.skinny_nc - 1) / pl.skinny_nc;
+    return pl;
+  }
   // GEMV path (M <= 8, K % 512 == 0: the B = 1..2 denoise rows): every CU streams its weight slice
   // (pz_gemv.hip); PZ_GEMV=0 falls back to the MFMA skinny kernel below
   if (pz_gemv_supported(a)) {
@@ -2067,6 +2336,10 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
     case PATH_SKINNY:
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
       break;
+    case PATH_SKINNY64:
+      snprintf(buf, sizeof(buf), "gemm_skinny64_kernel<%d, %d, %d, %s>", pl.skinny_w, pl.skinny_nc, pl.skinny_mb,
+               bstr(a->fp8_mode == 2));
+      break;
     case PATH_GEMV:
       snprintf(buf, sizeof(buf), "gemv_kernel<M<=%d>", a->M <= 4 ? 4 : 8);
       break;
@@ -2091,6 +2364,55 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
   }
   return buf;
+}
+
+template <int W, int NC, int MB, bool F8W>
+static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n), dim3(W * 64), 0, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+template <int W, int MB, bool F8W>
+static int launch_sk64_nc(const GemmP& p, int nc, int64_t tiles_n, hipStream_t st) {
+  if (nc == 4) return launch_sk64<W, 4, MB, F8W>(p, tiles_n, st);
+  if (nc == 8) return launch_sk64<W, 8, MB, F8W>(p, tiles_n, st);
+  return launch_sk64<W, 16, MB, F8W>(p, tiles_n, st);
+}
+
+template <bool F8W>
+static int launch_sk64_any(const GemmP& p, const Plan& pl, hipStream_t st) {
+  const int nc = pl.skinny_nc;
+  const int64_t tn = pl.tiles_n;
+  if (pl.skinny_w == 8) {
+    if (pl.skinny_mb == 1) return launch_sk64_nc<8, 1, F8W>(p, nc, tn, st);
+    if (pl.skinny_mb == 2) return launch_sk64_nc<8, 2, F8W>(p, nc, tn, st);
+    return launch_sk64_nc<8, 4, F8W>(p, nc, tn, st);
+  }
+  if (pl.skinny_mb == 1) return launch_sk64_nc<4, 1, F8W>(p, nc, tn, st);
+  if (pl.skinny_mb == 2) return launch_sk64_nc<4, 2, F8W>(p, nc, tn, st);
+  return launch_sk64_nc<4, 4, F8W>(p, nc, tn, st);
+}
+
+template <bool GEGLU>
+static int launch8p_f8(const GemmP& p, hipStream_t st) {
+  const int smem = 2 * P8_BUF;
+  auto kern = p.K % 64 != 0 ? gemm8p_f8_kernel<GEGLU, true> : gemm8p_f8_kernel<GEGLU, false>;
+  static bool attr_set[2] = {false, false};
+  const int ix = p.K % 64 != 0;
+  if (!attr_set[ix]) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set[ix] = true;
+  }
+  const int T = p.tiles_m * p.tiles_n;
+  const int units = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
+  hipLaunchKernelGGL(kern, dim3(units, 1), dim3(NT2), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  if (p.tail_s) {
+    hipLaunchKernelGGL(gemm8p_tail_epilogue<GEGLU>, dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+    PZ_CHECK_LAUNCH();
+  }
+  return PZ_OK;
 }
 
 template <int W, int NC>
@@ -2201,6 +2523,24 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   }
   if (a->aux) PZ_CHECK_ARG(a->ld_aux % 4 == 0 && PZ_ALIGNED(a->aux, 8), "pz_gemm: aux alignment");
   PZ_CHECK_ARG(a->ws_bytes >= 0, "pz_gemm: negative ws_bytes");
+  PZ_CHECK_ARG(a->fp8_mode >= 0 && a->fp8_mode <= 2, "pz_gemm: fp8_mode %d", (int)a->fp8_mode);
+  pz_gemm_args a8;  // fp8 W8A8: K / lda / ldb in code pairs for the planner and the kernel
+  if (a->fp8_mode == 1) {
+    PZ_CHECK_ARG(a->a_kcontig && a->b_kcontig && a->batch == 1 && !a->norm_w && a->epilogue <= PZ_EPI_SILU &&
+                     a->K % 16 == 0 && a->lda % 16 == 0 && a->ldb % 16 == 0,
+                 "pz_gemm: fp8 W8A8 needs k-contiguous A [M][K] and B [N][K] codes, batch 1, K / lda / ldb "
+                 "%% 16 == 0, a forward epilogue and no fused norm");
+    a8 = *a;
+    a8.K = a->K / 2;
+    a8.lda = a->lda / 2;
+    a8.ldb = a->ldb / 2;
+    a = &a8;
+  }
+  if (a->fp8_mode == 2)
+    PZ_CHECK_ARG(a->M <= 64 && a->a_kcontig && a->b_kcontig && a->batch == 1 && a->K % 64 == 0 && !a->c_fp32 &&
+                     a->epilogue < PZ_EPI_DGELU && a->ldb % 16 == 0,
+                 "pz_gemm: fp8 weights with bf16 rows (W8A16) need M <= 64, k-contiguous A and B, batch 1, "
+                 "K %% 64 == 0, ldb %% 16 == 0, bf16 C and a forward epilogue");
 
   GemmP p;
   memset(&p, 0, sizeof(p));
@@ -2224,14 +2564,31 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.alpha = a->alpha;
   p.nw = (const bf16_t*)a->norm_w;
   p.neps = a->norm_eps;
+  p.rs = a->fp8_mode == 1 ? a->a_row_scale : nullptr;
   hipStream_t st = (hipStream_t)stream;
 
   const Plan pl = make_plan(a);
   if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
   if (a->norm_w)
-    PZ_CHECK_ARG(pl.kind == PATH_SKINNY && PZ_ALIGNED(a->norm_w, 16),
-                 "pz_gemm: fused RMSNorm needs the few-row path (M <= 16, k-contiguous A/B, K %% 32 == 0) "
-                 "and a 16-byte aligned weight");
+    PZ_CHECK_ARG((pl.kind == PATH_SKINNY || pl.kind == PATH_SKINNY64) && PZ_ALIGNED(a->norm_w, 16),
+                 "pz_gemm: fused RMSNorm needs the few-row paths (M <= 64, k-contiguous A/B, K %% 32 == 0 "
+                 "(M <= 16) or K %% 64 == 0) and a 16-byte aligned weight");
+  if (pl.kind == PATH_SKINNY64) {
+    p.tiles_n = (int)pl.tiles_n;
+    return a->fp8_mode == 2 ? launch_sk64_any<true>(p, pl, st) : launch_sk64_any<false>(p, pl, st);
+  }
+  if (a->fp8_mode == 1) {
+    p.tiles_m = (int)pl.tiles_m;
+    p.tiles_n = (int)pl.tiles_n;
+    PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31), "pz_gemm: grid too large");
+    if (pl.tail_s) {
+      p.ws = (float*)a->workspace;
+      p.dp_tiles = pl.dp_tiles;
+      p.tail_s = pl.tail_s;
+      p.tail_kt = pl.tail_kt;
+    }
+    return geglu ? launch8p_f8<true>(p, st) : launch8p_f8<false>(p, st);
+  }
   if (pl.kind == PATH_SKINNY) {
     PZ_CHECK_ARG(a->batch < 65536, "pz_gemm: batch too large");
     if (pl.skinny_w == 16) return launch_skinny<16>(p, pl.skinny_nc, pl.tiles_n, a->batch, st);

@@ -262,7 +262,7 @@ int launch_gemv(const GemvP& p, hipStream_t st) {
 
 // shape/epilogue support of the GEMV path (the planner in pz_gemm.hip asks before choosing it)
 bool pz_gemv_supported(const pz_gemm_args* a) {
-  if (a->M < 1 || a->M > 8 || a->batch != 1 || !a->a_kcontig || !a->b_kcontig) return false;
+  if (a->M < 1 || a->M > 8 || a->batch != 1 || !a->a_kcontig || !a->b_kcontig || a->fp8_mode) return false;
   if (a->K % 512 != 0 || a->epilogue > PZ_EPI_SILU) return false;
   if (a->epilogue == PZ_EPI_GEGLU && a->bias) return false;
   if (!PZ_ALIGNED(a->A, 16) || !PZ_ALIGNED(a->B, 16) || a->lda % 8 || a->ldb % 8) return false;

@@ -1,0 +1,135 @@
+// fp8 (OCP e4m3fn) quantisation for the C5 fp8 path (BASELINE.json configs[4]: "fp8 MFMA attention/MLP").
+//
+// Activations: per-row scales (one workgroup per row holds the row in registers: max|x| by a block
+// reduction, then every element divided by s = max/448 and converted with v_cvt_pk_fp8_f32 -- RNE,
+// in range by construction, so no saturation path is ever taken).  Weights: one per-tensor scale,
+// computed once at load from pz_fp8_absmax partials.  HBM-bound byte work: 2 B read + 1 B written
+// per element.
+#include "pz_common.h"
+
+namespace {
+
+constexpr float E4M3_MAX = 448.f;
+
+__device__ __forceinline__ unsigned enc4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+
+__device__ __forceinline__ void unpack8f(const u32x4& r, float (&f)[8]) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    f[2 * e] = __uint_as_float(r[e] << 16);
+    f[2 * e + 1] = __uint_as_float(r[e] & 0xffff0000u);
+  }
+}
+
+// one row per workgroup; thread t owns 8-element chunks t, t + 256, ... (CH of them, in registers)
+template <int CH>
+__global__ void __launch_bounds__(256) quant_rows_kernel(const bf16_t* __restrict__ x, int64_t ldx, uint8_t* q,
+                                                         int64_t ldq, float* row_scale, int64_t D) {
+  __shared__ float red[4];
+  const int64_t r = blockIdx.x;
+  const int t = threadIdx.x;
+  const int64_t nch = D / 8;
+  const bf16_t* xr = x + r * ldx;
+  u32x4 v[CH];
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t ch = t + (int64_t)c * 256;
+    v[c] = ch < nch ? *reinterpret_cast<const u32x4*>(xr + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+    float f[8];
+    unpack8f(v[c], f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
+  }
+  m = warp_max(m);
+  if ((t & 63) == 0) red[t >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float s = m > 0.f ? __fdiv_rn(m, E4M3_MAX) : 1.f;  // IEEE quotients (reproducible scales)
+  const float inv = __fdiv_rn(1.f, s);
+  if (t == 0) row_scale[r] = s;
+  uint8_t* qr = q + r * ldq;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int64_t ch = t + (int64_t)c * 256;
+    if (ch >= nch) break;
+    float f[8];
+    unpack8f(v[c], f);
+    // clamp guards the one rounding case x/s = 448 * (1 + ulp) (never above the max code)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fminf(fmaxf(f[e] * inv, -E4M3_MAX), E4M3_MAX);
+    *reinterpret_cast<u32x2*>(qr + ch * 8) = u32x2{enc4(f[0], f[1], f[2], f[3]), enc4(f[4], f[5], f[6], f[7])};
+  }
+}
+
+__global__ void __launch_bounds__(256) quant_tensor_kernel(const bf16_t* __restrict__ x, int64_t n8, uint8_t* q,
+                                                           float inv_scale) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n8) return;
+  float f[8];
+  unpack8f(*reinterpret_cast<const u32x4*>(x + i * 8), f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) f[e] = fminf(fmaxf(f[e] * inv_scale, -E4M3_MAX), E4M3_MAX);
+  *reinterpret_cast<u32x2*>(q + i * 8) = u32x2{enc4(f[0], f[1], f[2], f[3]), enc4(f[4], f[5], f[6], f[7])};
+}
+
+// max |x| partials: grid-stride over 8-element chunks, one partial per workgroup (fixed order)
+__global__ void __launch_bounds__(256) absmax_kernel(const bf16_t* __restrict__ x, int64_t n8, float* parts) {
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    float f[8];
+    unpack8f(*reinterpret_cast<const u32x4*>(x + i * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m = fmaxf(m, fabsf(f[e]));
+  }
+  m = warp_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+}  // namespace
+
+extern "C" int pz_fp8_quant_rows(const void* x, int64_t ldx, void* q, int64_t ldq, float* row_scale, int64_t R,
+                                 int64_t D, void* stream) {
+  PZ_CHECK_ARG(x && q && row_scale && R > 0 && D > 0 && D % 8 == 0 && D <= 8 * 256 * 8,
+               "fp8_quant_rows: bad args (D %% 8 == 0, D <= 16384)");
+  PZ_CHECK_ARG(PZ_ALIGNED(x, 16) && PZ_ALIGNED(q, 8) && ldx % 8 == 0 && ldq % 8 == 0 && R < (1LL << 31),
+               "fp8_quant_rows: alignment");
+  const int ch = (int)((D / 8 + 255) / 256);
+  hipStream_t st = (hipStream_t)stream;
+  const bf16_t* xb = (const bf16_t*)x;
+  uint8_t* qb = (uint8_t*)q;
+  switch (ch) {
+    case 1: hipLaunchKernelGGL(quant_rows_kernel<1>, dim3((unsigned)R), dim3(256), 0, st, xb, ldx, qb, ldq, row_scale, D); break;
+    case 2: hipLaunchKernelGGL(quant_rows_kernel<2>, dim3((unsigned)R), dim3(256), 0, st, xb, ldx, qb, ldq, row_scale, D); break;
+    case 3:
+    case 4: hipLaunchKernelGGL(quant_rows_kernel<4>, dim3((unsigned)R), dim3(256), 0, st, xb, ldx, qb, ldq, row_scale, D); break;
+    default: hipLaunchKernelGGL(quant_rows_kernel<8>, dim3((unsigned)R), dim3(256), 0, st, xb, ldx, qb, ldq, row_scale, D); break;
+  }
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_fp8_quant_tensor(const void* x, int64_t n, void* q, float inv_scale, void* stream) {
+  PZ_CHECK_ARG(x && q && n > 0 && n % 8 == 0 && PZ_ALIGNED(x, 16) && PZ_ALIGNED(q, 8) && inv_scale > 0.f,
+               "fp8_quant_tensor: bad args (n %% 8 == 0, aligned, inv_scale > 0)");
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(quant_tensor_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const bf16_t*)x, n8, (uint8_t*)q, inv_scale);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_fp8_absmax(const void* x, int64_t n, float* parts, void* stream) {
+  PZ_CHECK_ARG(x && parts && n > 0 && n % 8 == 0 && PZ_ALIGNED(x, 16), "fp8_absmax: bad args (n %% 8 == 0)");
+  hipLaunchKernelGGL(absmax_kernel, dim3(PZ_ABSMAX_PARTS), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)x,
+                     n / 8, parts);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 10  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 11  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -35,6 +35,7 @@ class GemmArgs(C.Structure):
         ("geglu_inter", i64),
         ("workspace", vp), ("ws_bytes", i64),
         ("norm_w", vp), ("norm_eps", f32),
+        ("fp8_mode", i32), ("a_row_scale", vp),
     ]
 
 
@@ -108,6 +109,9 @@ class DecodeAttnArgs(C.Structure):
 # name -> argtypes (restype int unless listed in _RESTYPE)
 SIGNATURES = {
     "pz_gemm": [C.POINTER(GemmArgs), vp],
+    "pz_fp8_quant_rows": [vp, i64, vp, i64, vp, i64, i64, vp],
+    "pz_fp8_quant_tensor": [vp, i64, vp, f32, vp],
+    "pz_fp8_absmax": [vp, i64, vp, vp],
     "pz_gemm_kernel_name": [C.POINTER(GemmArgs)],
     "pz_gemm_small": [C.POINTER(SmallGemmArgs), vp],
     "pz_rmsnorm_fwd": [vp, i64, vp, vp, i64, vp, i64, i64, f32, vp],

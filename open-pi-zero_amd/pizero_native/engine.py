@@ -32,7 +32,7 @@ from dataclasses import dataclass
 import torch
 
 from . import ops
-from .ops import PZ_EPI_DGEGLU, PZ_EPI_DGELU, PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_SILU
+from .ops import PZ_EPI_DGEGLU, PZ_EPI_DGELU, PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_NONE, PZ_EPI_SILU
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -179,6 +179,8 @@ class Engine:
         self.joint_flash = os.environ.get("PZ_JOINT_ATTN", "gemm") == "flash"
         # inference (prefill / denoise) attention: fused kernel unless PZ_INFER_ATTN=gemm
         self.infer_flash = os.environ.get("PZ_INFER_ATTN", "flash") == "flash"
+        # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
+        self.f8 = None
         if self.d.nkv != 1:
             raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
 
@@ -201,6 +203,58 @@ class Engine:
 
     def gu_w(self, p):
         return self.ar.span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight")
+
+    # ------------------------------------------------------------ fp8 (C5) --
+    def prepare_fp8(self):
+        """fp8 e4m3 copies (per-tensor scale max|W|/448) of every inference Linear of SigLIP, the vlm
+        mixture and the action expert (BASELINE.json configs[4]: fp8 attention / MLP GEMMs).  Prefill
+        GEMMs (>= 65 rows) run W8A8 on the fp8 MFMA with per-row activation scales; denoise rows
+        (<= 64) run W8A16 (codes expanded to bf16 in registers, RMSNorm still fused).  Taken from the
+        current weights: call again after the weights change."""
+        d = self.d
+        vt = "vision_tower.vision_model.encoder.layers."
+        keys = []
+        for i in range(d.vL):
+            p = f"{vt}{i}."
+            keys += [("span", p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"),
+                     ("w", p + "self_attn.out_proj.weight"), ("w", p + "mlp.fc1.weight"), ("w", p + "mlp.fc2.weight")]
+        for mix in ("vlm", "action"):
+            for l in range(d.nL):
+                p = f"joint_model.mixtures.{mix}.layers.{l}."
+                keys += [("span", p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"),
+                         ("w", p + "self_attn.o_proj.weight"),
+                         ("span", p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"),
+                         ("w", p + "mlp.down_proj.weight")]
+        f8 = {}
+        for k in keys:
+            W = self.ar.span(k[1], k[2]) if k[0] == "span" else self.w(k[1])
+            sc = ops.fp8_weight_scale(W)
+            q = torch.empty(W.shape, device=W.device, dtype=torch.uint8)
+            ops.fp8_quant_tensor(W, q, sc)
+            f8[k[1]] = (q, sc)
+        self.f8 = f8
+
+    def lin(self, x, key, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, norm=None):
+        """ops.linear, or its fp8 form when prepare_fp8() holds codes for ``key`` (the weight name; the
+        first name of a span): W8A16 for <= 64 rows (norm may stay fused), else per-row quantised
+        activations (norm must already be applied) and W8A8."""
+        f = self.f8.get(key) if self.f8 else None
+        if f is None:
+            return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
+        q, sc = f
+        M, K = x.shape
+        if M <= 64:
+            if K % 64:  # (SigLIP fc2, K = 4304, never has so few rows in practice)
+                return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
+            return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
+        if norm is not None:
+            raise ValueError("lin: a fused norm needs <= 64 rows")
+        if K % 16 or x.stride(0) % 16:  # W8A8 stages K in 16-code steps (tiny test widths: bf16)
+            return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux)
+        xq = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+        xs = torch.empty(M, device=x.device, dtype=F32)
+        ops.fp8_quant_rows(x, xq, xs)
+        return ops.linear_fp8(xq, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=xs)
 
     def rope(self, theta, maxpos=None):
         """fp32 cos|sin table for positions 0..maxpos (default L + 8: every training / action position);
@@ -274,6 +328,10 @@ class Engine:
         nh, hd = d.vheads, d.vH // d.vheads
         Np = Nt
         layers = []
+
+        def L(x_, key, W, out, **kw):  # fp8 codes (prepare_fp8) serve inference only
+            return self.lin(x_, p + key, W, out, **kw) if save is None else ops.linear(x_, W, out, **kw)
+
         for i in range(d.vL):
             p = f"{vt}encoder.layers.{i}."
             st = {"x": x}
@@ -282,25 +340,26 @@ class Engine:
             r1 = torch.empty(M, device=dev, dtype=F32)
             ops.layernorm(x, self.w(p + "layer_norm1.weight"), self.w(p + "layer_norm1.bias"), h1, mu1, r1, d.ln_eps)
             qkv = torch.empty(M, 3 * d.vH, device=dev, dtype=BF16)
-            ops.linear(h1, self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"), qkv,
-                       bias=self.ar.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias"))
+            L(h1, "self_attn.q_proj.weight", self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"),
+              qkv, bias=self.ar.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias"))
             # fused attention (siglip.py:108-166) in place on the q|k|v rows: O and one fp32
             # log-sum-exp per (head, query) row; no [B, heads, N, N] tensor exists
             O = torch.empty(M, d.vH, device=dev, dtype=BF16)
             lse = torch.empty(B * nh, Np, device=dev, dtype=F32)
             ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, Np))
             xm = torch.empty_like(x)
-            ops.linear(O, self.w(p + "self_attn.out_proj.weight"), xm, bias=self.w(p + "self_attn.out_proj.bias"),
-                       resid=x)
+            L(O, "self_attn.out_proj.weight", self.w(p + "self_attn.out_proj.weight"), xm,
+              bias=self.w(p + "self_attn.out_proj.bias"), resid=x)
             h2 = torch.empty_like(x)
             mu2 = torch.empty(M, device=dev, dtype=F32)
             r2 = torch.empty(M, device=dev, dtype=F32)
             ops.layernorm(xm, self.w(p + "layer_norm2.weight"), self.w(p + "layer_norm2.bias"), h2, mu2, r2, d.ln_eps)
             a1 = torch.empty(M, d.vI, device=dev, dtype=BF16) if save is not None else None
             g1 = torch.empty(M, d.vI, device=dev, dtype=BF16)
-            ops.linear(h2, self.w(p + "mlp.fc1.weight"), g1, bias=self.w(p + "mlp.fc1.bias"), epi=PZ_EPI_GELU, aux=a1)
+            L(h2, "mlp.fc1.weight", self.w(p + "mlp.fc1.weight"), g1, bias=self.w(p + "mlp.fc1.bias"), epi=PZ_EPI_GELU,
+              aux=a1)
             xn = torch.empty_like(x)
-            ops.linear(g1, self.w(p + "mlp.fc2.weight"), xn, bias=self.w(p + "mlp.fc2.bias"), resid=xm)
+            L(g1, "mlp.fc2.weight", self.w(p + "mlp.fc2.weight"), xn, bias=self.w(p + "mlp.fc2.bias"), resid=xm)
             if save is not None:
                 st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, lse=lse, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1, g1=g1)
                 layers.append(st)
@@ -845,6 +904,11 @@ class Engine:
         d = self.d
         return d.H * d.nh <= 32 and d.hd == 256 and os.environ.get("PZ_DECODE_ATTN", "1") != "0"
 
+    def few_rows(self, M, K):
+        """row counts the few-row GEMM kernels take with the RMSNorm fused (pz_gemm skinny paths:
+        M <= 16 with K % 32 == 0, 16 < M <= 64 with K % 64 == 0)"""
+        return (M <= 16 and K % 32 == 0) or (M <= 64 and K % 64 == 0)
+
     def gemv_ok(self, M, K):
         """few-row GEMV kernels (pz_gemv.hip): M <= 8 rows, K % 512 == 0 (PZ_GEMV=0 disables)"""
         return M <= 8 and K % 512 == 0 and os.environ.get("PZ_GEMV", "1") != "0"
@@ -899,7 +963,7 @@ class Engine:
                                        g.off, Lp, g.off)
                     continue
                 qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
-                ops.linear(h, self.qkv_w(p), qkv)
+                self.lin(h, p + "self_attn.q_proj.weight", self.qkv_w(p), qkv)
                 ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, B, g.T, nh, 1, hd, L1, g.off,
                                    Lp, g.off)
                 hs[g.name] = h
@@ -1003,17 +1067,17 @@ class Engine:
         M = x.shape[0]
         dev = x.device
         xm = torch.empty_like(x)
-        ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
+        self.lin(O, p + "self_attn.o_proj.weight", self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
         hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
-        if M <= 16:  # few rows (denoise / proprio): RMSNorm fused into the gate|up GEMM
-            ops.linear(xm, self.gu_w(p), hm, epi=PZ_EPI_GEGLU,
-                       norm=(self.w(p + "post_attention_layernorm.weight"), d.rms_eps))
+        if self.few_rows(M, x.shape[1]):  # few rows (denoise / proprio): RMSNorm fused into the gate|up GEMM
+            self.lin(xm, p + "mlp.gate_proj.weight", self.gu_w(p), hm, epi=PZ_EPI_GEGLU,
+                     norm=(self.w(p + "post_attention_layernorm.weight"), d.rms_eps))
         else:
             h2 = torch.empty_like(x)
             ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)
-            ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
+            self.lin(h2, p + "mlp.gate_proj.weight", self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
         xn = torch.empty_like(x)
-        ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
+        self.lin(hm, p + "mlp.down_proj.weight", self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
         return xn
 
     def _post_attn(self, g, p, x, Pm, Vj, B, Lq, Lp, qrow0=None):
@@ -1058,12 +1122,13 @@ class Engine:
                                   g.off, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
             else:
                 qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
-                if M <= 16:  # RMSNorm fused into the q|k|v GEMM
-                    ops.linear(x, self.qkv_w(p), qkv, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                if self.few_rows(M, d.aH):  # RMSNorm fused into the q|k|v GEMM
+                    self.lin(x, p + "self_attn.q_proj.weight", self.qkv_w(p), qkv,
+                             norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
                 else:
                     h = torch.empty_like(x)
                     ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
-                    ops.linear(h, self.qkv_w(p), qkv)
+                    self.lin(h, p + "self_attn.q_proj.weight", self.qkv_w(p), qkv)
                 ops.qkv_rope_split(qkv, apos, self.rope(g.theta), Q, Kj, Vj, B, d.H, nh, 1, hd, d.H, 0, Lp, g.off)
             if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over every cached key
                 if O is None:

@@ -144,6 +144,47 @@ def linear(x, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, alpha
     return out
 
 
+# ---------------------------------------------------------------- fp8 (C5) ----
+ABSMAX_PARTS = 1024  # include/pz_abi.h PZ_ABSMAX_PARTS
+E4M3_MAX = 448.0
+
+
+def fp8_quant_rows(x, q, row_scale):
+    """per-row fp8 e4m3 codes of bf16 x [R, D] (q uint8 [R, D], row_scale fp32 [R] = max|row| / 448)"""
+    R, D = x.shape
+    call("pz_fp8_quant_rows", _p(x), x.stride(0), _p(q), q.stride(0), _p(row_scale), R, D, _st())
+
+
+def fp8_quant_tensor(x, q, scale):
+    """q = e4m3(x / scale) elementwise (weights; scale = max|x| / 448 from fp8_weight_scale)"""
+    call("pz_fp8_quant_tensor", _p(x), x.numel(), _p(q), 1.0 / float(scale), _st())
+
+
+def fp8_weight_scale(x):
+    """per-tensor weight scale max|x| / 448 (load-time: pz_fp8_absmax partials, host max)"""
+    parts = torch.empty(ABSMAX_PARTS, device=x.device, dtype=torch.float32)
+    call("pz_fp8_absmax", _p(x), x.numel(), _p(parts), _st())
+    m = float(parts.max().item())
+    return m / E4M3_MAX if m > 0 else 1.0
+
+
+def linear_fp8(x, Wq, w_scale, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, norm=None,
+               x_scale=None):
+    """out = epi(x @ W^T) with fp8 e4m3 weights Wq [N, K] (uint8 codes, per-tensor w_scale).
+    x_scale None: x bf16 rows (W8A16, M <= 64: codes expanded to bf16 in registers; norm allowed);
+    else x uint8 codes [M, K] with per-row scales x_scale (W8A8 on the fp8 MFMA, 256-tile kernel)."""
+    M, K = x.shape
+    N = Wq.shape[0]
+    a = _args(M, N, K, x, x.stride(0), True, Wq, Wq.stride(0), True, out, out.stride(0), epi, w_scale, False, bias,
+              resid, 0 if resid is None else resid.stride(0), aux, 0 if aux is None else aux.stride(0),
+              N // 2 if epi == PZ_EPI_GEGLU else 0, 1, 1, (0, 0), (0, 0), (0, 0), (0, 0), workspace(out.device),
+              norm)
+    a.fp8_mode = 2 if x_scale is None else 1
+    a.a_row_scale = _p(x_scale)
+    call("pz_gemm", C.byref(a), _st())
+    return out
+
+
 def linear_dgrad(dy, W, dx, *, beta=False, resid=None, epi=PZ_EPI_NONE, aux=None):
     """dx[M,K] (+)= dy[M,N] @ W[N,K] (+ resid).
 

@@ -251,7 +251,23 @@ class PiZero(nn.Module, NoSyncBase):
             if self._arena.data.device.type != "cuda":
                 raise RuntimeError("PiZero runs on the MI355X HIP path only: move the model to a GPU (.to('cuda'))")
             self._eng = Engine(self)
+            if getattr(self, "_fp8_infer", False):
+                self._eng.prepare_fp8()
         return self._eng
+
+    def use_fp8_inference(self, enabled: bool = True):
+        """Config C5 (BASELINE.json configs[4], "fp8 MFMA attention/MLP"): run inference (infer_action,
+        infer_text) with OCP e4m3 weights -- per-tensor scales -- for every Linear of SigLIP, the vlm
+        mixture and the action expert: prefill GEMMs W8A8 on the fp8 MFMA (per-row activation scales),
+        denoise rows W8A16.  Training never uses them.  The codes are a snapshot of the current weights:
+        call again after the weights change.  An extension: the reference has no fp8 path."""
+        self._fp8_infer = bool(enabled)
+        eng = self._engine()
+        if enabled:
+            eng.prepare_fp8()
+        else:
+            eng.f8 = None
+        return self
 
     # ========================================================= param groups ==
     @property

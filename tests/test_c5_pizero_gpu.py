@@ -75,3 +75,31 @@ def test_c5_full_shape_inference_graph_equals_eager():
     a = ig.replay()
     torch.cuda.synchronize()
     assert torch.equal(a.float(), eager.float())
+
+
+def test_c5_full_shape_fp8_inference():
+    """C5 as BASELINE.json names it (fp8 MFMA attention/MLP): the full 3-image / chunk-50 shape with
+    PiZero.use_fp8_inference -- hipGraph replay equals eager, the chunk is finite and stays close to the
+    bf16 chunk of the same weights (rel-L2 printed; parity vs fp8 is pinned only through the bridge-size
+    fixture gate of test_pizero_gpu.py::test_full_actions_fp8)"""
+    from pizero_native.graph import InferenceGraph
+
+    d = C5_FULL
+    m = build_gpu_model(d)
+    m.eval()
+    gi = gpu_inputs(m, d, 1, ragged=False)
+    a16 = run_infer(m, gi, clip=False).float()
+    m.use_fp8_inference(True)
+    eager = run_infer(m, gi, clip=False)
+    assert eager.shape == (1, 50, 7) and torch.isfinite(eager.float()).all()
+    rel = float((eager.float() - a16).norm() / a16.norm())
+    print(f"C5 fp8 vs bf16 action chunk rel-L2 {rel:.4g}")
+    assert rel < 0.1, rel
+    ig = InferenceGraph(m, 1, clip=False)
+    ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"],
+            gi["ppos"], gi["apos"], gi["proprios"].float(), gi["noise"])
+    ig.capture()
+    a = ig.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a.float(), eager.float())
+

@@ -1,0 +1,175 @@
+"""fp8 (OCP e4m3fn) kernels of the C5 path (BASELINE.json configs[4]: "fp8 MFMA attention/MLP") and the
+16 < M <= 64 few-row GEMM (C5 denoise rows), against torch fp32 references of the same op.
+
+  * pz_fp8_quant_rows / pz_fp8_quant_tensor: codes bit-identical to torch's float8_e4m3fn cast (round to
+    nearest even) of the same fp32 quotient, scales = max|x| / 448;
+  * W8A8 (fp8_mode 1, the 8-phase kernel on code pairs with v_mfma_f32_16x16x128_f8f6f4): against
+    torch fp32 of the DEQUANTISED operands -- the same products, so only summation order and the bf16
+    output rounding differ (rel-L2 <= 1e-2); every epilogue the C5 prefill uses, K tails, split tails;
+  * W8A16 (fp8_mode 2, skinny-64 kernel, codes expanded to bf16 in registers): same reference;
+  * bf16 skinny-64 (16 < M <= 64): against torch fp32.
+"""
+
+import pytest
+import torch
+
+from pizero_native import ops
+from pizero_native.ops import PZ_EPI_GEGLU, PZ_EPI_GELU, PZ_EPI_NONE, PZ_EPI_SILU
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    return (torch.randn(*shape, device=DEV, generator=g) * scale).to(torch.bfloat16)
+
+
+def _deq(q, s):
+    """codes uint8 -> fp32 values times scale (per-row [R] or scalar)"""
+    v = q.view(torch.float8_e4m3fn).float()
+    return v * (s[:, None] if torch.is_tensor(s) else s)
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm())
+
+
+def _epi_ref(acc, epi, bias=None, resid=None, I=None):
+    if epi == PZ_EPI_GEGLU:
+        g, u = acc[:, :I], acc[:, I:]
+        return torch.nn.functional.gelu(g, approximate="tanh") * u
+    if bias is not None:
+        acc = acc + bias.float()
+    if epi == PZ_EPI_GELU:
+        acc = torch.nn.functional.gelu(acc, approximate="tanh")
+    elif epi == PZ_EPI_SILU:
+        acc = torch.nn.functional.silu(acc)
+    if resid is not None:
+        acc = acc + resid.float()
+    return acc
+
+
+def test_quant_rows_matches_torch_cast():
+    for R, D in ((5, 1024), (788, 2048), (3, 16384), (7, 1152), (2, 4304)):
+        x = _rand(R, D, scale=3.0, seed=R)
+        x[0, :5] = torch.tensor([0.0, -0.0, 1e-8, 60000.0, -2.5], dtype=torch.bfloat16)
+        if R > 2:
+            x[2] = 0  # all-zero row: scale 1, zero codes
+        q = torch.empty(R, D, device=DEV, dtype=torch.uint8)
+        s = torch.empty(R, device=DEV, dtype=torch.float32)
+        ops.fp8_quant_rows(x, q, s)
+        # IEEE quotients via float64 (torch divides by a scalar through its reciprocal on the GPU)
+        amax = x.float().abs().amax(1).double()
+        s_ref = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax)).float()
+        torch.testing.assert_close(s, s_ref, rtol=0, atol=0)
+        inv = (1.0 / s_ref.double()).float()[:, None]
+        q_ref = (x.float() * inv).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+        assert torch.equal(q, q_ref), (R, D, int((q != q_ref).sum()))
+
+
+def test_quant_tensor_and_weight_scale():
+    W = _rand(1024, 4096, scale=0.02, seed=3)
+    s = ops.fp8_weight_scale(W)
+    assert abs(s - float(W.float().abs().max()) / 448.0) <= 1e-12 * s
+    q = torch.empty_like(W, dtype=torch.uint8)
+    ops.fp8_quant_tensor(W, q, s)
+    inv = torch.tensor(1.0 / s, dtype=torch.float32, device=DEV)
+    q_ref = (W.float() * inv).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    assert torch.equal(q, q_ref)
+    # quantisation error of e4m3 (3 mantissa bits): relative error <= 2^-4 per element, ~3 % rel-L2
+    assert _rel(_deq(q, s), W.float()) < 0.04
+
+
+def _quant_w(W):
+    s = ops.fp8_weight_scale(W)
+    q = torch.empty_like(W, dtype=torch.uint8)
+    ops.fp8_quant_tensor(W, q, s)
+    return q, s
+
+
+def _quant_x(x):
+    q = torch.empty_like(x, dtype=torch.uint8)
+    s = torch.empty(x.shape[0], device=DEV, dtype=torch.float32)
+    ops.fp8_quant_rows(x, q, s)
+    return q, s
+
+
+@pytest.mark.parametrize("M,N,K,epi,extras", [
+    (788, 2048, 16384, PZ_EPI_NONE, "resid"),       # Gemma down (C5 prefill), split tail
+    (788, 2 * 2048, 2048, PZ_EPI_GEGLU, ""),        # Gemma gate|up, GeGLU (I = 2048 here)
+    (768, 4304, 1152, PZ_EPI_GELU, "bias"),         # SigLIP fc1 (3 images)
+    (768, 1152, 4304, PZ_EPI_NONE, "bias,resid"),   # SigLIP fc2: K % 128 != 0 (K tail)
+    (300, 1024, 2048, PZ_EPI_SILU, "bias"),
+])
+def test_w8a8_gemm(M, N, K, epi, extras):
+    x = _rand(M, K, scale=1.0, seed=M + K)
+    W = _rand(N, K, scale=0.03, seed=N)
+    xq, xs = _quant_x(x)
+    Wq, ws = _quant_w(W)
+    bias = _rand(N, scale=0.1, seed=7) if "bias" in extras else None
+    resid = _rand(M, N, scale=0.5, seed=9) if "resid" in extras else None
+    I = N // 2
+    out = torch.empty(M, I if epi == PZ_EPI_GEGLU else N, device=DEV, dtype=torch.bfloat16)
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if epi in (PZ_EPI_GEGLU, PZ_EPI_GELU) else None
+    ops.linear_fp8(xq, Wq, ws, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=xs)
+    acc = _deq(xq, xs) @ _deq(Wq, ws).t()
+    ref = _epi_ref(acc, epi, bias, resid, I)
+    assert _rel(out.float(), ref) < 1e-2, _rel(out.float(), ref)
+    if aux is not None:
+        pre = acc if bias is None else acc + bias.float()
+        assert _rel(aux.float(), pre) < 1e-2
+    # against the unquantised bf16 product: the fp8 error itself (reported, loose)
+    full = _epi_ref(x.float() @ W.float().t(), epi, bias, resid, I)
+    assert _rel(out.float(), full) < 0.08, _rel(out.float(), full)
+
+
+@pytest.mark.parametrize("M", [1, 8, 17, 50, 64])
+@pytest.mark.parametrize("epi", [PZ_EPI_NONE, PZ_EPI_GEGLU, PZ_EPI_SILU])
+def test_w8a16_skinny(M, epi):
+    K, N = 2048, 2048
+    x = _rand(M, K, seed=M)
+    W = _rand(N, K, scale=0.03, seed=5)
+    Wq, ws = _quant_w(W)
+    nw = _rand(K, scale=0.1, seed=11)
+    I = N // 2
+    out = torch.empty(M, I if epi == PZ_EPI_GEGLU else N, device=DEV, dtype=torch.bfloat16)
+    resid = _rand(M, N, seed=13) if epi == PZ_EPI_NONE else None
+    bias = _rand(N, scale=0.1, seed=17) if epi == PZ_EPI_SILU else None
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if epi != PZ_EPI_NONE else None
+    for norm in (None, (nw, 1e-6)):
+        ops.linear_fp8(x, Wq, ws, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
+        xf = x.float()
+        if norm is not None:
+            xf = xf * torch.rsqrt(xf.pow(2).mean(1, keepdim=True) + 1e-6) * (1 + nw.float())
+            xf = xf.to(torch.bfloat16).float()  # the kernel rounds the normalised row to bf16 (x * (1 + w))
+        ref = _epi_ref(xf @ _deq(Wq, ws).t(), epi, bias, resid, I)
+        assert _rel(out.float(), ref) < 1e-2, (M, epi, norm is not None, _rel(out.float(), ref))
+
+
+@pytest.mark.parametrize("M", [17, 33, 50, 64])
+@pytest.mark.parametrize("N,K,epi", [(2560, 1024, PZ_EPI_NONE), (1024, 4096, PZ_EPI_NONE),
+                                     (2 * 4096, 1024, PZ_EPI_GEGLU), (1024, 2048, PZ_EPI_SILU)])
+def test_bf16_skinny64(M, N, K, epi):
+    x = _rand(M, K, seed=M + 1)
+    W = _rand(N, K, scale=0.03, seed=N + K)
+    I = N // 2
+    out = torch.empty(M, I if epi == PZ_EPI_GEGLU else N, device=DEV, dtype=torch.bfloat16)
+    resid = _rand(M, N, seed=3) if epi == PZ_EPI_NONE else None
+    bias = _rand(N, scale=0.1, seed=4) if epi == PZ_EPI_SILU else None
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if epi != PZ_EPI_NONE else None
+    name = ops.gemm_kernel_name(M, N, K, epi=epi, geglu_inter=I if epi == PZ_EPI_GEGLU else 0)
+    assert name.startswith("gemm_skinny64_kernel"), name
+    ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux)
+    ref = _epi_ref(x.float() @ W.float().t(), epi, bias, resid, I)
+    assert _rel(out.float(), ref) < 1e-2, _rel(out.float(), ref)
+    if epi == PZ_EPI_GEGLU:
+        assert _rel(aux.float(), x.float() @ W.float().t()) < 1e-2

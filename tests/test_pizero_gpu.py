@@ -141,6 +141,38 @@ def test_full_actions_hipgraph(full):
     assert torch.equal(a.float(), eager.float()), float((a.float() - eager.float()).abs().max())
 
 
+def test_full_actions_fp8(full):
+    """Config C5's fp8 inference (PiZero.use_fp8_inference: e4m3 weights with per-tensor scales; prefill
+    GEMMs W8A8 on the fp8 MFMA with per-row activation scales, denoise rows W8A16) at bridge size
+    against the reference's fp32 action chunk.  Parity vs an fp8 reference is unpinned (the reference
+    has no fp8 path): the gate is the bf16 action tolerance widened 2x (fp8 e4m3 keeps 3 mantissa bits
+    against bf16's 7), and the measured deviation is printed."""
+    from pizero_native.graph import InferenceGraph
+
+    d, g, m, gi = full
+    ref = g["fp32/actions_unclipped"]
+    dev = np.abs(g["bf16/actions_unclipped"] - ref)
+    a16 = run_infer(m, gi, clip=False).float().cpu().numpy()
+    try:
+        m.use_fp8_inference(True)
+        a8 = run_infer(m, gi, clip=False)
+        e8, e16 = np.abs(a8.float().cpu().numpy() - ref), np.abs(a16 - ref)
+        print(f"fp8 actions: mean|d| {e8.mean():.4g} max {e8.max():.4g}; bf16 {e16.mean():.4g} / {e16.max():.4g}; "
+              f"reference bf16 {dev.mean():.4g} / {dev.max():.4g}")
+        assert e8.mean() <= 2 * max(3 * dev.mean(), 5e-3), (e8.mean(), dev.mean())
+        assert e8.max() <= 2 * max(3 * dev.max(), 3e-2), (e8.max(), dev.max())
+        B = int(g["bsz"])
+        ig = InferenceGraph(m, B, clip=False)
+        ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"],
+                gi["ppos"], gi["apos"], gi["proprios"].float(), gi["noise"])
+        ig.capture()
+        a = ig.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(a.float(), a8.float())
+    finally:
+        m.use_fp8_inference(False)
+
+
 @pytest.fixture(scope="module")
 def b16(full_model):
     d = O.FULL_DIMS

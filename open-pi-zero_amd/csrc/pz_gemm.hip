@@ -2240,7 +2240,8 @@ Plan make_plan(const pz_gemm_args* a) {
   // skinny-64 path: 16 < M <= 64 rows (bf16), or any M <= 64 with fp8 weights (W8A16)
   const bool sk64_ok = a->M <= 64 && pl.akc && pl.bkc && a->K % 64 == 0 && a->batch == 1 && !a->c_fp32 &&
                        a->epilogue < PZ_EPI_DGELU;
-  if (a->fp8_mode == 2 || (sk64_ok && a->M > 16)) {
+  const char* e64 = getenv("PZ_SK64");  // "0": rows 17..64 take the tile kernels (A/B; read per call)
+  if (a->fp8_mode == 2 || (sk64_ok && a->M > 16 && !(e64 && e64[0] == '0'))) {
     pl.kind = PATH_SKINNY64;
     pl.skinny_mb = (int)((a->M + 15) / 16);
     pl.skinny_mb = pl.skinny_mb == 3 ? 4 : pl.skinny_mb;

@@ -179,6 +179,10 @@ class Engine:
         self.joint_flash = os.environ.get("PZ_JOINT_ATTN", "gemm") == "flash"
         # inference (prefill / denoise) attention: fused kernel unless PZ_INFER_ATTN=gemm
         self.infer_flash = os.environ.get("PZ_INFER_ATTN", "flash") == "flash"
+        # activation backward of the training MLPs (PZ_SPLIT_DACT, A/B): "1" (default) = plain dgrad GEMM + a
+        # vectorised elementwise pass; "0" = fused into the dgrad GEMM's epilogue, which the 8-phase kernel
+        # cannot overlap with its main loop (measured: "1" +0.7 % samples/s)
+        self.split_dact = os.environ.get("PZ_SPLIT_DACT", "1") == "1"
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
         if self.d.nkv != 1:
@@ -410,8 +414,12 @@ class Engine:
             p = f"{vt}encoder.layers.{i}."
             st = sv["layers"][i]
             # MLP: x' = xm + fc2(gelu(fc1(ln2(xm))))
-            # dgrad through fc2 with the GELU derivative fused into its epilogue (saved pre-activation a1)
-            ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg, epi=PZ_EPI_DGELU, aux=st["a1"])
+            # dgrad through fc2, then the GELU derivative at the saved pre-activation a1
+            if self.split_dact:  # plain dgrad GEMM, then the GELU backward (HBM-bound) in place
+                ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg)
+                ops.act_bwd(dg, st["a1"], dg, None, PZ_EPI_GELU)
+            else:
+                ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg, epi=PZ_EPI_DGELU, aux=st["a1"])
             if self.rg(p + "mlp.fc2.weight"):
                 ops.linear_wgrad(dx, st["g1"], self.gw(p + "mlp.fc2.weight"), beta=beta)
             st["g1"] = None
@@ -644,7 +652,13 @@ class Engine:
                 # dgrad through down_proj with the GeGLU derivative fused into its epilogue:
                 # gu (saved g|u) <- d(gate|up) in place; hm (saved GeGLU output) feeds the down_proj wgrad
                 gu = gs["gu"]
-                ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), gu, epi=PZ_EPI_DGEGLU, aux=gu)
+                if self.split_dact:  # plain dgrad GEMM, then the HBM-bound GeGLU backward in place on gu
+                    dh = torch.empty(M, g.inter, device=dev, dtype=BF16)
+                    ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dh)
+                    ops.geglu_bwd(dh, gu, gu, None, M, g.inter)
+                    del dh
+                else:
+                    ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), gu, epi=PZ_EPI_DGEGLU, aux=gu)
                 if self.rg(p + "mlp.down_proj.weight"):
                     ops.linear_wgrad(dx, gs["hm"], self.gw(p + "mlp.down_proj.weight"), beta=beta)
                 gs["hm"] = None

@@ -113,6 +113,8 @@ def _worker(rank, world, port, q):
             for n in ar.order:
                 if not m._requires_grad(n):
                     continue
+                if n.startswith("vision_tower") and n.endswith("self_attn.k_proj.bias"):
+                    continue  # exact gradient 0 (softmax shift invariance): both sides are rounding noise
                 a, b = ar.view(n, gavg), ar.view(n, gref)
                 nb = float(b.norm())
                 if nb > 0:

@@ -305,7 +305,7 @@ def test_skinny_fused_rmsnorm(K, N, gemv, monkeypatch):
 
     monkeypatch.setenv("PZ_GEMV", gemv)
     eps = 1e-6
-    for M in (1, 4, 16):
+    for M in (1, 4, 16, 50, 64):  # 50 / 64: the skinny-64 kernel (C5 denoise rows)
         x = bf(M, K, scale=3.0)
         w = bf(K, scale=0.5)
         W = bf(N, K, scale=K ** -0.5)
@@ -319,9 +319,9 @@ def test_skinny_fused_rmsnorm(K, N, gemv, monkeypatch):
         ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, norm=(w, eps))
         raw = _rms_ref(x, w, eps).float() @ W.float().t()
         close(h, torch.nn.functional.gelu(raw[:, :I], approximate="tanh") * raw[:, I:], rtol=3e-2, atol=6e-2)
-    with pytest.raises(RuntimeError):  # many rows: not the few-row path
-        x = bf(64, K)
-        ops.linear(x, W, torch.empty(64, N, device=dev, dtype=torch.bfloat16), norm=(w, eps))
+    with pytest.raises(RuntimeError):  # many rows: not a few-row path
+        x = bf(65, K)
+        ops.linear(x, W, torch.empty(65, N, device=dev, dtype=torch.bfloat16), norm=(w, eps))
 
 
 @pytest.mark.parametrize("K", [1024, 2048, 4096])

@@ -17,7 +17,22 @@ for s in $STEPS; do
       timeout -k 10 600 python -u bench.py > "$OUT/bench.log" 2>&1 ;;
     prof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
-        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/prof.log" 2>&1 ;;
+        -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+      # the full trace (~100 MB) exceeds what gpurun copies back; keep the per-dispatch rows of the
+      # dominant GEMM only (grid split / duration check) and the stats summary
+      python3 - "$OUT/prof" <<'PY'
+import csv, glob, os, sys
+for f in glob.glob(os.path.join(sys.argv[1], "*kernel_trace.csv")):
+    with open(f) as fi, open(f.replace("kernel_trace", "dominant_trace"), "w", newline="") as fo:
+        r = csv.DictReader(fi)
+        w = csv.DictWriter(fo, fieldnames=r.fieldnames)
+        w.writeheader()
+        for row in r:
+            if "gemm8p_kernel<true, true, true, false>" in row.get("Kernel_Name", ""):
+                w.writerow(row)
+    os.remove(f)
+PY
+      ;;
     infprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/infprof" -o infer \
         -- python3 tools/infer_bench.py --iters 20 > "$OUT/infprof.log" 2>&1 ;;

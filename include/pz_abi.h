@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 11
+#define PZ_ABI_VERSION 12
 
 enum {
   PZ_OK = 0,
@@ -234,12 +234,12 @@ int pz_flash_bwd_prep(const pz_flash_args* a, void* stream);
 int pz_flash_bwd(const pz_flash_args* a, void* stream);
 
 /* Decode-shaped joint attention (denoise steps, pizero.py:461-481; joint_model.py:259-292): for each
- * sample b, the T query tokens x nh heads (T*nh <= 32 rows, MQA) q[(b*Lq + qoff + t)*ldq + h*256 ..]
+ * sample b, the T query tokens x nh heads (T*nh <= 1024 rows, MQA) q[(b*Lq + qoff + t)*ldq + h*256 ..]
  * against the nk cached keys/values k/v[b*k_bstride + j*256 ..] (head_dim 256): logits
  * cap*tanh(scale*q.k/cap), the Pi0 block mask for joint query token qtok0 + t (prefix counts cnt[b],
  * prefix / cond sizes; NULL cnt: no mask), fp32 softmax, O[(b*T + t)*ldo + h*256 ..] bf16.  Two
- * launches: per 32-key chunk partial (m, l, O) into the fp32 workspace ws (pz_decode_attn_ws_bytes),
- * then a fixed-order merge.  Deterministic. */
+ * launches: per (32-key chunk, 32-row tile) partial (m, l, O) into the fp32 workspace ws
+ * (pz_decode_attn_ws_bytes(B, T*nh, nk)), then a fixed-order merge per row.  Deterministic. */
 typedef struct pz_decode_attn_args {
   const void* q; int64_t ldq, Lq, qoff;
   const void* k; const void* v; int64_t k_bstride, v_bstride;
@@ -249,7 +249,7 @@ typedef struct pz_decode_attn_args {
   const int32_t* cnt; int64_t prefix, cond, qtok0;
   float* ws; int64_t ws_bytes;
 } pz_decode_attn_args;
-int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t nk);
+int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t rows, int64_t nk);
 int pz_decode_attn(const pz_decode_attn_args* a, void* stream);
 
 /* SigLIP patch embed im2col (siglip.py:42-48,69-74): pixels bf16 [B,3,H,W] -> cols bf16

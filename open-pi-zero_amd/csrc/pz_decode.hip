@@ -4,7 +4,8 @@
 // the action tokens themselves).
 //
 // Two launches, each short and wide:
-//   decode_attn_part: one workgroup per 32-key chunk of one sample, ALL query rows (T x nh <= 32):
+//   decode_attn_part: one workgroup per (32-key chunk, 32-row tile) of one sample (C4: one row tile
+//     holds all 4 tokens x 8 heads; C5's chunk of 50 tokens = 13 row tiles):
 //     S^T = K Q^T on the MFMA (16 keys x 16 rows tiles, one tile per wave, K and Q fragments loaded
 //     straight from global memory), soft-cap + Pi0 block mask, chunk-local softmax stats (m, l),
 //     partial O = P V on the VALU (each thread 8 head dims x 4 query rows, its 16-byte V loads issued
@@ -17,7 +18,8 @@
 namespace {
 
 constexpr int DA_KC = 32;    // keys per chunk (workgroup)
-constexpr int DA_R = 32;     // max query rows per sample (tokens x heads)
+constexpr int DA_R = 32;     // query rows per row tile (tokens x heads)
+constexpr int DA_RMAX = 1024;  // query rows per sample
 constexpr int DA_HD = 256;   // head dim (Gemma)
 constexpr int DA_RS = DA_HD + 4;  // workspace row: O[256], m, l (16-byte aligned rows)
 
@@ -28,12 +30,14 @@ __device__ __forceinline__ bool da_allowed(int t, int j, int nk, int cnt, int P,
   return j < cnt || j >= P;
 }
 
-// grid (nchunks, B), 256 threads = 4 waves: wave w computes key tile (w & 1) x row tile (w >> 1)
+// grid (nchunks, B * rtiles), 256 threads = 4 waves: wave w computes key tile (w & 1) x row block (w >> 1)
+// of row tile rt (rows 32 rt ..); workspace rows [b][chunk][Rpad][DA_RS], Rpad = 32 * rtiles
 __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
   __shared__ float S[DA_R][DA_KC + 1];  // logits -> probabilities, [row][key]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int c = blockIdx.x, b = blockIdx.y;
   const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
+  const int rtiles = (R + DA_R - 1) / DA_R, Rpad = rtiles * DA_R;
+  const int c = blockIdx.x, b = blockIdx.y / rtiles, rt = blockIdx.y % rtiles, r0 = rt * DA_R;
   const bool masked = a.cnt != nullptr;  // NULL: no mask (text generation, pizero.py:336-365)
   const int cnt = masked ? a.cnt[b] : nk;
   const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
@@ -47,10 +51,10 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
   for (int u = 0; u < DA_KC / 2; ++u)
     vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + u, nk - 1) * DA_HD + 8 * dg);
   {
-    const int kt = wave & 1, rt = wave >> 1;
+    const int kt = wave & 1;
     const int g = lane >> 4;
     const int key = min(j0 + kt * 16 + (lane & 15), nk - 1);
-    const int row = rt * 16 + (lane & 15);  // query row = t * nh + h
+    const int row = r0 + (wave >> 1) * 16 + (lane & 15);  // query row = t * nh + h
     const bool rok = row < R;
     const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
     const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
@@ -73,12 +77,12 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
       float x = acc[e] * a.scale;
       if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
       const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
-      S[row][kl] = ok ? x : -INFINITY;
+      S[row - r0][kl] = ok ? x : -INFINITY;
     }
   }
   __syncthreads();
   // chunk-local softmax stats per row (thread r < 32): m, l; S <- p
-  float* ws = a.ws + ((int64_t)b * gridDim.x + c) * DA_R * DA_RS;
+  float* ws = a.ws + (((int64_t)b * gridDim.x + c) * Rpad + r0) * DA_RS;
   if (threadIdx.x < DA_R) {
     const int r = threadIdx.x;
     float m = -INFINITY;
@@ -136,7 +140,7 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = 4 * rg + r;
-    if (row < R) {
+    if (r0 + row < R) {
       float4* dst = reinterpret_cast<float4*>(ws + row * DA_RS + 8 * dg);
       dst[0] = float4{o[r][0], o[r][1], o[r][2], o[r][3]};
       dst[1] = float4{o[r][4], o[r][5], o[r][6], o[r][7]};
@@ -148,12 +152,13 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
 __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a, int nchunks) {
   const int r = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int nh = (int)a.nh, t = r / nh, h = r % nh;
-  const float* ws = a.ws + (int64_t)b * nchunks * DA_R * DA_RS + r * DA_RS;
+  const int Rpad = ((int)(a.T * a.nh) + DA_R - 1) / DA_R * DA_R;
+  const float* ws = a.ws + (int64_t)b * nchunks * Rpad * DA_RS + r * DA_RS;
   float M = -INFINITY;
-  for (int c = 0; c < nchunks; ++c) M = fmaxf(M, ws[(int64_t)c * DA_R * DA_RS + DA_HD]);
+  for (int c = 0; c < nchunks; ++c) M = fmaxf(M, ws[(int64_t)c * Rpad * DA_RS + DA_HD]);
   float o = 0.f, l = 0.f;
   for (int c = 0; c < nchunks; ++c) {
-    const float* w = ws + (int64_t)c * DA_R * DA_RS;
+    const float* w = ws + (int64_t)c * Rpad * DA_RS;
     const float mc = w[DA_HD];
     const float s = mc == -INFINITY ? 0.f : __expf(mc - M);
     o += s * w[d];
@@ -165,21 +170,24 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
 
 }  // namespace
 
-extern "C" int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t nk) {
-  return B * ((nk + DA_KC - 1) / DA_KC) * DA_R * DA_RS * (int64_t)sizeof(float);
+extern "C" int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t rows, int64_t nk) {
+  const int64_t rpad = (rows + DA_R - 1) / DA_R * DA_R;
+  return B * ((nk + DA_KC - 1) / DA_KC) * rpad * DA_RS * (int64_t)sizeof(float);
 }
 
 extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->q && a->k && a->v && a->o && a->ws && a->B > 0 && a->nh > 0, "decode_attn: bad args");
-  PZ_CHECK_ARG(a->head_dim == DA_HD && a->T >= 1 && a->T * a->nh <= DA_R && a->nk >= 1,
-               "decode_attn: head_dim 256 and tokens x heads <= 32 query rows per sample");
-  PZ_CHECK_ARG(a->ws_bytes >= pz_decode_attn_ws_bytes(a->B, a->nk), "decode_attn: workspace too small");
+  PZ_CHECK_ARG(a->head_dim == DA_HD && a->T >= 1 && a->T * a->nh <= DA_RMAX && a->nk >= 1,
+               "decode_attn: head_dim 256 and tokens x heads <= 1024 query rows per sample");
+  PZ_CHECK_ARG(a->ws_bytes >= pz_decode_attn_ws_bytes(a->B, a->T * a->nh, a->nk), "decode_attn: workspace too small");
   PZ_CHECK_ARG(PZ_ALIGNED(a->q, 16) && PZ_ALIGNED(a->k, 16) && PZ_ALIGNED(a->v, 16) && PZ_ALIGNED(a->o, 2) &&
                    PZ_ALIGNED(a->ws, 16) && a->ldq % 8 == 0 && a->k_bstride % 8 == 0 && a->v_bstride % 8 == 0,
                "decode_attn: alignment");
   const int nchunks = (int)((a->nk + DA_KC - 1) / DA_KC);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)nchunks, (unsigned)a->B), dim3(256), 0, st, *a);
+  const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
+  PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
+  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)nchunks, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a);
   PZ_CHECK_LAUNCH();
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
                      nchunks);

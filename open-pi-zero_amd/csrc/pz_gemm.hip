@@ -1906,6 +1906,9 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   const int64_t n0 = (int64_t)blockIdx.x * NC;
   const int64_t nr = n0 + (lane & 15) % NC;
   const bool nok = nr < ncols;
+  // row chunks of 64 (blockIdx.y): M > 64 runs as independent 64-row problems sharing the weights in L2
+  const int64_t row0 = (int64_t)blockIdx.y * 64;
+  const int64_t Mc = min((int64_t)64, p.M - row0);
   constexpr int ES = F8W ? 1 : 2;  // weight element bytes
   const char* Bc = reinterpret_cast<const char*>(p.B);
   const char* Brow = Bc + (nr * p.ldb + 16 * g) * ES;
@@ -1915,8 +1918,8 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int64_t m = mb * 16 + (lane & 15);
-    mok[mb] = m < p.M;
-    Arow[mb] = p.A + m * p.lda + 16 * g;
+    mok[mb] = m < Mc;
+    Arow[mb] = p.A + (row0 + m) * p.lda + 16 * g;
   }
   const bf16_t* Wn = p.nw + 16 * g;
   f32x4 acc[MB], acc2[MB];
@@ -2019,8 +2022,9 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
       for (int w = 0; w < W; ++w) o2 += red[w][mb][lane];
   }
   if (mb >= MB) return;
-  const int64_t mm = mb * 16 + (lane & 15);
-  if (mm >= p.M) return;
+  const int64_t ml = mb * 16 + (lane & 15);
+  if (ml >= Mc) return;
+  const int64_t mm = row0 + ml;
   float scale = p.alpha;
   if (nrm) {
     float t = 0.f;
@@ -2238,12 +2242,15 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   // skinny-64 path: 16 < M <= 64 rows (bf16), or any M <= 64 with fp8 weights (W8A16)
-  const bool sk64_ok = a->M <= 64 && pl.akc && pl.bkc && a->K % 64 == 0 && a->batch == 1 && !a->c_fp32 &&
-                       a->epilogue < PZ_EPI_DGELU;
+  // rows 65..PZ_SK64_MAXM run as 64-row chunks of the same kernel (blockIdx.y)
+  const char* emax = getenv("PZ_SK64_MAXM");
+  const int64_t sk_maxm = emax ? atoll(emax) : 64;
+  const bool sk64_ok = (a->M <= 64 || a->M <= sk_maxm) && pl.akc && pl.bkc && a->K % 64 == 0 && a->batch == 1 &&
+                       !a->c_fp32 && a->epilogue < PZ_EPI_DGELU;
   const char* e64 = getenv("PZ_SK64");  // "0": rows 17..64 take the tile kernels (A/B; read per call)
   if (a->fp8_mode == 2 || (sk64_ok && a->M > 16 && !(e64 && e64[0] == '0'))) {
     pl.kind = PATH_SKINNY64;
-    pl.skinny_mb = (int)((a->M + 15) / 16);
+    pl.skinny_mb = a->M > 64 ? 4 : (int)((a->M + 15) / 16);
     pl.skinny_mb = pl.skinny_mb == 3 ? 4 : pl.skinny_mb;
     // 16 real columns per block, 8 waves: every block re-reads the (L2-resident) activation rows, so
     // narrower blocks multiply that traffic -- measured at 50 rows (tools/skinny_bench.py): q|k|v
@@ -2369,7 +2376,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
 
 template <int W, int NC, int MB, bool F8W>
 static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n), dim3(W * 64), 0, st, p);
+  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64)),
+                     dim3(W * 64), 0, st, p);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

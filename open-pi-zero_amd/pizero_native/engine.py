@@ -913,10 +913,13 @@ class Engine:
 
     # ============================================================ inference ==
     def decode_attn_ok(self):
-        """pz_decode_attn for the denoise attention (H x nh <= 32 query rows per sample, head_dim 256);
-        PZ_DECODE_ATTN=0 uses the key-split flash kernel + combine"""
+        """pz_decode_attn for the denoise attention (head_dim 256) when the chunk is one 32-row tile (C4: 4 tokens
+        x 8 heads); the kernel takes up to 1024 rows in 32-row tiles, but at C5's 400 rows its 351 (key chunk,
+        row tile) partials cost more than the key-split flash kernel (measured 27.6 vs 26.4 ms per C5 chunk):
+        PZ_DECODE_ATTN=0 never / =all always uses it"""
         d = self.d
-        return d.H * d.nh <= 32 and d.hd == 256 and os.environ.get("PZ_DECODE_ATTN", "1") != "0"
+        mode = os.environ.get("PZ_DECODE_ATTN", "1")
+        return d.hd == 256 and mode != "0" and d.H * d.nh <= (1024 if mode == "all" else 32)
 
     def few_rows(self, M, K):
         """row counts the few-row GEMM kernels take with the RMSNorm fused (pz_gemm skinny paths:

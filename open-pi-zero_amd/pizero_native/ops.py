@@ -347,7 +347,7 @@ def decode_attn(q, Lq, qoff, k, v, o, B, nh, T, nk, scale, cap, cnt, prefix, con
     a.B, a.nh, a.T, a.nk, a.head_dim = B, nh, T, nk, k.shape[-1]
     a.scale, a.cap = float(scale), float(cap)
     a.cnt, a.prefix, a.cond, a.qtok0 = _p(cnt), prefix, cond, qtok0
-    need = lib().pz_decode_attn_ws_bytes(B, nk)
+    need = lib().pz_decode_attn_ws_bytes(B, T * nh, nk)
     ws = workspace(o.device)  # the GEMM split-K scratch: stream-ordered, not in use between kernels
     if ws.numel() * 4 < need:
         raise ValueError(f"decode_attn: {B} samples x {nk} keys need {need} B of workspace (> {ws.numel() * 4})")

@@ -634,13 +634,15 @@ def test_time_embed_modes_match_reference():
         assert outs[1] < outs[0], outs
 
 
-@pytest.mark.parametrize("B,T,cnts", [(1, 4, [270]), (2, 4, [276, 259]), (1, 2, [100]), (2, 1, [5, 276])])
-def test_decode_attn_matches_reference(B, T, cnts):
+@pytest.mark.parametrize("B,T,cnts,P", [(1, 4, [270], 276), (2, 4, [276, 259], 276), (1, 2, [100], 276),
+                                          (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276)])
+def test_decode_attn_matches_reference(B, T, cnts, P):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
-    with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306)"""
+    with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
+    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile"""
     from pizero_native import ops
 
-    P, C, nh, hd = 276, 1, 8, 256
+    C, nh, hd = 1, 8, 256
     nk = P + C + T
     Lp = (nk + 7) // 8 * 8
     q = bf(B, T, nh * hd)

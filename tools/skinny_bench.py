@@ -29,6 +29,23 @@ def main():
     dev = "cuda"
     shapes = [("qkv", 2560, 1024, PZ_EPI_NONE), ("o", 1024, 2048, PZ_EPI_NONE), ("gate|up", 8192, 1024, PZ_EPI_GEGLU),
               ("down", 1024, 4096, PZ_EPI_NONE)]
+    if a.rows > 64:  # B=1 SigLIP prefill shapes (256 rows / image): row-chunked skinny-64 vs the tile path
+        shapes = [("sig qkv", 3456, 1152, PZ_EPI_NONE), ("sig o", 1152, 1152, PZ_EPI_NONE),
+                  ("sig fc1", 4304, 1152, PZ_EPI_NONE), ("sig fc2", 1152, 4352, PZ_EPI_NONE),
+                  ("vlm o", 2048, 2048, PZ_EPI_NONE), ("vlm qkv", 2560, 2048, PZ_EPI_NONE)]
+        for name, N, K, epi in shapes:
+            x = (torch.randn(M, K, device=dev)).to(torch.bfloat16)
+            W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            os.environ.pop("PZ_SK64_MAXM", None)
+            t0 = graph_us(lambda: ops.linear(x, W, out), a.n)
+            n0 = ops.gemm_kernel_name(M, N, K)
+            os.environ["PZ_SK64_MAXM"] = str(M)
+            t1 = graph_us(lambda: ops.linear(x, W, out), a.n)
+            n1 = ops.gemm_kernel_name(M, N, K)
+            os.environ.pop("PZ_SK64_MAXM")
+            print(f"{name:8s} M={M} N={N} K={K}: default {t0:7.2f} us ({n0})   row-chunked {t1:7.2f} us ({n1})")
+        return
     for name, N, K, epi in shapes:
         x = (torch.randn(M, K, device=dev)).to(torch.bfloat16)
         W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)

@@ -1929,9 +1929,13 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
     acc[mb] = acc2[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
     ss[mb] = 0.f;
   }
-  const int64_t kchunks = p.K / 64;
+  // split-K over blockIdx.z (p.ksplit > 0: raw fp32 partials -> ws, summed by splitk_epilogue_kernel)
+  const bool split = p.ksplit > 0;
+  const int64_t kchunks_all = p.K / 64;
+  const int64_t kz0 = split ? (int64_t)blockIdx.z * (p.ksplit / 64) : 0;
+  const int64_t kchunks = split ? min(kchunks_all - kz0, p.ksplit / 64) : kchunks_all;
   const int64_t per = (kchunks + W - 1) / W;
-  const int64_t kb = wave * per, ke = min(kchunks, kb + per);
+  const int64_t kb = kz0 + wave * per, ke = kz0 + min(kchunks, (int64_t)(wave + 1) * per);
   auto load_b = [&](const char* row, int64_t c, bf16x8& lo, bf16x8& hi) {
     if (!nok) {
       lo = hi = bf16x8{};
@@ -2025,6 +2029,14 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   const int64_t ml = mb * 16 + (lane & 15);
   if (ml >= Mc) return;
   const int64_t mm = row0 + ml;
+  if (split) {  // (host: no fused norm, no GeGLU with split)
+    float* wz = p.ws + (int64_t)blockIdx.z * p.M * p.ldw + mm * p.ldw;
+    for (int r = 0; r < 4; ++r) {
+      const int64_t nn = n0 + 4 * g + r;
+      if (4 * g + r < NC && nn < ncols) wz[nn] = o[r];
+    }
+    return;
+  }
   float scale = p.alpha;
   if (nrm) {
     float t = 0.f;
@@ -2257,6 +2269,27 @@ Plan make_plan(const pz_gemm_args* a) {
     // 7.3 vs 16.8 us, gate|up 8.6 vs 25.6 us for 16 vs 4 columns; W = 8 never slower than 4
     pl.skinny_w = a->K / 64 >= 8 ? 8 : 4;
     pl.skinny_nc = 16;
+    // narrow outputs (o / down projections: 64 blocks of 16 columns) split K over blockIdx.z so the
+    // weight stream spreads over ~256 workgroups; partials summed by splitk_epilogue_kernel
+    // (PZ_SK64_SPLIT = 0 disables; no fused norm / GeGLU with a split)
+    {
+      const char* es = getenv("PZ_SK64_SPLIT");
+      const int64_t nblk = (ncols + 15) / 16 * ((a->M + 63) / 64);
+      const int64_t kch = a->K / 64;
+      if (!(es && es[0] == '0') && !a->norm_w && !pl.geglu && a->workspace && nblk < 128 &&
+          kch >= 16) {
+        int64_t S = (256 + nblk - 1) / nblk;
+        S = S < kch / 8 ? S : kch / 8;
+        S = S < 8 ? S : 8;
+        const int64_t ldw = (a->N + 3) / 4 * 4;
+        if (S >= 2 && S * a->M * ldw * 4 <= a->ws_bytes && PZ_ALIGNED(a->workspace, 16)) {
+          const int64_t per = (kch + S - 1) / S;
+          pl.splits = (int)((kch + per - 1) / per);
+          pl.ksplit = per * 64;
+          pl.ldw = ldw;
+        }
+      }
+    }
     {  // A/B overrides (read per call): PZ_SK64_NC = 4|8|16 columns per block, PZ_SK64_W = 4|8 waves
       const char* e = getenv("PZ_SK64_NC");
       if (e && (atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) pl.skinny_nc = atoi(e);
@@ -2314,7 +2347,8 @@ Plan make_plan(const pz_gemm_args* a) {
   // split-K when one 128x128 tile per WG leaves most of the 256 CUs idle
   const int64_t tiles = pl.tiles_m * pl.tiles_n;
   const int64_t nk = (a->K + BK - 1) / BK;
-  if (a->batch == 1 && a->workspace && tiles < 120 && nk >= 4) {
+  const char* esk = getenv("PZ_SPLITK");  // "0": whole-K tiles only (A/B; read per call)
+  if (a->batch == 1 && a->workspace && tiles < 120 && nk >= 4 && !(esk && esk[0] == '0')) {
     int64_t S = (240 + tiles - 1) / tiles;
     S = S < 16 ? S : 16;
     S = S < nk / 2 ? S : nk / 2;
@@ -2345,8 +2379,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
       break;
     case PATH_SKINNY64:
-      snprintf(buf, sizeof(buf), "gemm_skinny64_kernel<%d, %d, %d, %s>", pl.skinny_w, pl.skinny_nc, pl.skinny_mb,
-               bstr(a->fp8_mode == 2));
+      snprintf(buf, sizeof(buf), "gemm_skinny64_kernel<%d, %d, %d, %s>%s", pl.skinny_w, pl.skinny_nc, pl.skinny_mb,
+               bstr(a->fp8_mode == 2), pl.ksplit > 0 ? "+splitk_epilogue_kernel" : "");
       break;
     case PATH_GEMV:
       snprintf(buf, sizeof(buf), "gemv_kernel<M<=%d>", a->M <= 4 ? 4 : 8);
@@ -2376,9 +2410,15 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
 
 template <int W, int NC, int MB, bool F8W>
 static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64)),
+  const int S = p.ksplit > 0 ? (int)((p.K / 64 + p.ksplit / 64 - 1) / (p.ksplit / 64)) : 1;
+  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64), S),
                      dim3(W * 64), 0, st, p);
   PZ_CHECK_LAUNCH();
+  if (S > 1) {
+    const int64_t work = p.M * ((p.N + 3) / 4);
+    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, p, S);
+    PZ_CHECK_LAUNCH();
+  }
   return PZ_OK;
 }
 
@@ -2584,6 +2624,11 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
                  "(M <= 16) or K %% 64 == 0) and a 16-byte aligned weight");
   if (pl.kind == PATH_SKINNY64) {
     p.tiles_n = (int)pl.tiles_n;
+    if (pl.ksplit > 0) {
+      p.ws = (float*)a->workspace;
+      p.ksplit = pl.ksplit;
+      p.ldw = pl.ldw;
+    }
     return a->fp8_mode == 2 ? launch_sk64_any<true>(p, pl, st) : launch_sk64_any<false>(p, pl, st);
   }
   if (a->fp8_mode == 1) {

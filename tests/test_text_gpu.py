@@ -124,3 +124,21 @@ def test_text_cache_grows(setup):
         m.infer_text(toks[:, :1].cuda(), gi["pix"], am, kv_cache=cache)
     assert cache.k.shape[2] > cap and cache.num_items() == cap + 3
     assert torch.equal(cache.k[:, :, :n_before], k0)
+
+
+def test_text_generation_fp8(setup):
+    """infer_text under PiZero.use_fp8_inference (C5's fp8 weights: prefill W8A8 where the widths allow,
+    decode rows W8A16): logits stay close to the bf16 path's (fp8 e4m3 keeps 3 mantissa bits; parity vs
+    an fp8 reference is unpinned -- the reference has no fp8 path)"""
+    g, m, gi = setup
+    toks = torch.from_numpy(g["fp32/tokens"])
+    pre16, steps16 = _generate(m, gi, toks, m.build_text_cache())
+    try:
+        m.use_fp8_inference(True)
+        pre8, steps8 = _generate(m, gi, toks, m.build_text_cache())
+    finally:
+        m.use_fp8_inference(False)
+    r_pre, r_steps = _rel(pre8, pre16), _rel(steps8, steps16)
+    print(f"fp8 vs bf16 text logits rel-L2: prefill {r_pre:.4g}, decode {r_steps:.4g}")
+    assert np.isfinite(pre8).all() and np.isfinite(steps8).all()
+    assert r_pre < 0.1 and r_steps < 0.1, (r_pre, r_steps)

@@ -13,6 +13,8 @@
 //   decode_attn_combine: one workgroup per query row merges the chunks' (m, l, O) in fixed order.
 // The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of once per head.
 // Deterministic (no atomics).
+#include <stdlib.h>
+
 #include "pz_common.h"
 
 namespace {
@@ -30,118 +32,140 @@ __device__ __forceinline__ bool da_allowed(int t, int j, int nk, int cnt, int P,
   return j < cnt || j >= P;
 }
 
-// grid (nchunks, B * rtiles), 256 threads = 4 waves: wave w computes key tile (w & 1) x row block (w >> 1)
-// of row tile rt (rows 32 rt ..); workspace rows [b][chunk][Rpad][DA_RS], Rpad = 32 * rtiles
-__global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a) {
+// grid (ngroups, B * rtiles), 256 threads = 4 waves: workgroup = (group of nch consecutive 32-key chunks,
+// 32-row tile rt, sample b); per chunk wave w computes key tile (w & 1) x row block (w >> 1) of S, then an
+// online-softmax update of the workgroup's running (m, l, O) (C5's 27 chunks x 13 row tiles in groups of
+// 2: half the partial rows to merge).  Workspace rows [b][group][Rpad][DA_RS], Rpad = 32 * rtiles.
+__global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a, int nch) {
   __shared__ float S[DA_R][DA_KC + 1];  // logits -> probabilities, [row][key]
+  __shared__ float alpha_s[DA_R];       // per-row rescale of the running O for this chunk
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
   const int rtiles = (R + DA_R - 1) / DA_R, Rpad = rtiles * DA_R;
-  const int c = blockIdx.x, b = blockIdx.y / rtiles, rt = blockIdx.y % rtiles, r0 = rt * DA_R;
+  const int grp = blockIdx.x, b = blockIdx.y / rtiles, rt = blockIdx.y % rtiles, r0 = rt * DA_R;
   const bool masked = a.cnt != nullptr;  // NULL: no mask (text generation, pizero.py:336-365)
   const int cnt = masked ? a.cnt[b] : nk;
   const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
   const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
-  const int j0 = c * DA_KC;
+  const int nchunks = (nk + DA_KC - 1) / DA_KC;
+  const int c0 = grp * nch, c1 = min(nchunks, c0 + nch);
   // P.V ownership: thread = 8 head dims (dg) x 4 query rows (rg); its V loads (16 keys x 16 B, 128 B
   // contiguous per 8 lanes) are issued before the S phase so their latency overlaps it
   const int dg = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  u32x4 vv[DA_KC / 2];
-#pragma unroll
-  for (int u = 0; u < DA_KC / 2; ++u)
-    vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + u, nk - 1) * DA_HD + 8 * dg);
+  // this lane's query fragments (the same for every chunk): row block (wave >> 1), 8 x 16 B
+  const int g = lane >> 4;
+  const int row = r0 + (wave >> 1) * 16 + (lane & 15);  // query row = t * nh + h
+  const bool rok = row < R;
+  const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
+  const int qt = (int)a.qtok0 + t;
+  bf16x8 qf[8];
   {
-    const int kt = wave & 1;
-    const int g = lane >> 4;
-    const int key = min(j0 + kt * 16 + (lane & 15), nk - 1);
-    const int row = r0 + (wave >> 1) * 16 + (lane & 15);  // query row = t * nh + h
-    const bool rok = row < R;
-    const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
-    const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
     const bf16_t* qp = (const bf16_t*)a.q + ((int64_t)b * a.Lq + a.qoff + t) * a.ldq + (int64_t)h * DA_HD + 8 * g;
-    bf16x8 kf[8], qf[8];
 #pragma unroll
-    for (int dc = 0; dc < 8; ++dc) {
-      kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
-      qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
-    }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int dc = 0; dc < 8; ++dc) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], acc, 0, 0, 0);
-    // lane holds S^T[key = kt*16 + 4g + e][row = rt*16 + (lane & 15)]
-    const int qt = (int)a.qtok0 + t;
-    const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int kl = kt * 16 + 4 * g + e;
-      float x = acc[e] * a.scale;
-      if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
-      const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
-      S[row - r0][kl] = ok ? x : -INFINITY;
-    }
+    for (int dc = 0; dc < 8; ++dc) qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
   }
-  __syncthreads();
-  // chunk-local softmax stats per row (thread r < 32): m, l; S <- p
-  float* ws = a.ws + (((int64_t)b * gridDim.x + c) * Rpad + r0) * DA_RS;
-  if (threadIdx.x < DA_R) {
-    const int r = threadIdx.x;
-    float m = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
-    float l = 0.f;
-#pragma unroll
-    for (int k = 0; k < DA_KC; ++k) {
-      const float p = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
-      S[r][k] = p;
-      l += p;
-    }
-    ws[r * DA_RS + DA_HD] = m;
-    ws[r * DA_RS + DA_HD + 1] = l;
-  }
-  __syncthreads();
-  // partial O[row][d] = sum_k p[row][k] V[k][d]: 4 rows x 8 dims per thread, two halves of 16 keys
+  const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
   float o[4][8];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[r][e] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;  // threads < 32: row threadIdx.x's running stats
+  for (int c = c0; c < c1; ++c) {
+    const int j0 = c * DA_KC;
+    u32x4 vv[DA_KC / 2];
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    if (half == 1) {
+    for (int u = 0; u < DA_KC / 2; ++u)
+      vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + u, nk - 1) * DA_HD + 8 * dg);
+    {
+      const int kt = wave & 1;
+      const int key = min(j0 + kt * 16 + (lane & 15), nk - 1);
+      const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
+      bf16x8 kf[8];
 #pragma unroll
-      for (int u = 0; u < DA_KC / 2; ++u)
-        vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + DA_KC / 2 + u, nk - 1) * DA_HD + 8 * dg);
+      for (int dc = 0; dc < 8; ++dc) kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dc = 0; dc < 8; ++dc) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], acc, 0, 0, 0);
+      // lane holds S^T[key = kt*16 + 4g + e][row]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kl = kt * 16 + 4 * g + e;
+        float x = acc[e] * a.scale;
+        if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
+        const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
+        S[row - r0][kl] = ok ? x : -INFINITY;
+      }
+    }
+    __syncthreads();
+    // online softmax per row (thread r < 32): new max, rescale factor, S <- p
+    if (threadIdx.x < DA_R) {
+      const int r = threadIdx.x;
+      float m = m_run;
+#pragma unroll
+      for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
+      const float al = m_run == -INFINITY ? 0.f : __expf(m_run - m);
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < DA_KC; ++k) {
+        const float p = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
+        S[r][k] = p;
+        l += p;
+      }
+      l_run = l_run * al + l;
+      m_run = m;
+      alpha_s[r] = al;
+    }
+    __syncthreads();
+    // O[row][d] = alpha * O + sum_k p[row][k] V[k][d]: 4 rows x 8 dims per thread, two halves of 16 keys
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float al = alpha_s[4 * rg + r];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[r][e] *= al;
     }
 #pragma unroll
-    for (int u4 = 0; u4 < DA_KC / 8; ++u4) {
-      float pr[4][4];
+    for (int half = 0; half < 2; ++half) {
+      if (half == 1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = 4 * rg + r;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pr[r][q] = S[row][half * (DA_KC / 2) + 4 * u4 + q];
+        for (int u = 0; u < DA_KC / 2; ++u)
+          vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + DA_KC / 2 + u, nk - 1) * DA_HD + 8 * dg);
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float vf[8];
-        const u32x4 vr = vv[4 * u4 + q];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          vf[2 * e] = __uint_as_float(vr[e] << 16);
-          vf[2 * e + 1] = __uint_as_float(vr[e] & 0xffff0000u);
-        }
+      for (int u4 = 0; u4 < DA_KC / 8; ++u4) {
+        float pr[4][4];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) o[r][e] += pr[r][q] * vf[e];
+          for (int q = 0; q < 4; ++q) pr[r][q] = S[4 * rg + r][half * (DA_KC / 2) + 4 * u4 + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float vf[8];
+          const u32x4 vr = vv[4 * u4 + q];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            vf[2 * e] = __uint_as_float(vr[e] << 16);
+            vf[2 * e + 1] = __uint_as_float(vr[e] & 0xffff0000u);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[r][e] += pr[r][q] * vf[e];
+        }
       }
     }
+    __syncthreads();  // S / alpha_s are rewritten by the next chunk
+  }
+  float* ws = a.ws + (((int64_t)b * gridDim.x + grp) * Rpad + r0) * DA_RS;
+  if (threadIdx.x < DA_R) {
+    ws[threadIdx.x * DA_RS + DA_HD] = m_run;
+    ws[threadIdx.x * DA_RS + DA_HD + 1] = l_run;
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int row = 4 * rg + r;
-    if (r0 + row < R) {
-      float4* dst = reinterpret_cast<float4*>(ws + row * DA_RS + 8 * dg);
+    const int rr = 4 * rg + r;
+    if (r0 + rr < R) {
+      float4* dst = reinterpret_cast<float4*>(ws + rr * DA_RS + 8 * dg);
       dst[0] = float4{o[r][0], o[r][1], o[r][2], o[r][3]};
       dst[1] = float4{o[r][4], o[r][5], o[r][6], o[r][7]};
     }
@@ -187,10 +211,17 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
   PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
-  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)nchunks, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a);
+  // chunks per workgroup: one (C4: 9 workgroups) until the (chunk, row tile) grid passes 256 workgroups,
+  // then groups of nch chunks (fewer partial rows for the merge)
+  const int64_t wg1 = (int64_t)nchunks * a->B * rtiles;
+  const char* e = getenv("PZ_DECODE_WG");  // target workgroups (A/B; read per call)
+  const int64_t target = e && atoll(e) > 0 ? atoll(e) : 256;
+  const int nch = (int)((wg1 + target - 1) / target);
+  const int ngroups = (nchunks + nch - 1) / nch;
+  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
   PZ_CHECK_LAUNCH();
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
-                     nchunks);
+                     ngroups);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

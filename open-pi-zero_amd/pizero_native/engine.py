@@ -913,13 +913,12 @@ class Engine:
 
     # ============================================================ inference ==
     def decode_attn_ok(self):
-        """pz_decode_attn for the denoise attention (head_dim 256) when the chunk is one 32-row tile (C4: 4 tokens
-        x 8 heads); the kernel takes up to 1024 rows in 32-row tiles, but at C5's 400 rows its 351 (key chunk,
-        row tile) partials cost more than the key-split flash kernel (measured 27.6 vs 26.4 ms per C5 chunk):
-        PZ_DECODE_ATTN=0 never / =all always uses it"""
+        """pz_decode_attn for the denoise attention (head_dim 256, up to 1024 query rows per sample in 32-row
+        tiles: C4's 4 tokens x 8 heads = one tile, C5's 50 x 8 = 13 tiles with 2 key chunks per workgroup --
+        measured 23.5 vs 24.3 ms per C5 chunk against the key-split flash kernel); PZ_DECODE_ATTN=0 uses
+        the flash kernel + combine"""
         d = self.d
-        mode = os.environ.get("PZ_DECODE_ATTN", "1")
-        return d.hd == 256 and mode != "0" and d.H * d.nh <= (1024 if mode == "all" else 32)
+        return d.hd == 256 and os.environ.get("PZ_DECODE_ATTN", "1") != "0" and d.H * d.nh <= 1024
 
     def few_rows(self, M, K):
         """row counts the few-row GEMM kernels take with the RMSNorm fused (pz_gemm skinny paths:

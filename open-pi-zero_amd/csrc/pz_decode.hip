@@ -156,6 +156,22 @@ __global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a, i
     }
     __syncthreads();  // S / alpha_s are rewritten by the next chunk
   }
+  if (gridDim.x == 1) {  // one group holds every key: normalise and write O directly (no merge launch)
+    if (threadIdx.x < DA_R) alpha_s[threadIdx.x] = l_run > 0.f ? 1.f / l_run : 0.f;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int rr = r0 + 4 * rg + r;
+      if (rr < R) {
+        const float il = alpha_s[4 * rg + r];
+        const int tt = rr / nh, hh = rr % nh;
+        bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD + 8 * dg;
+        *reinterpret_cast<u32x4*>(out) = u32x4{pack2bf(o[r][0] * il, o[r][1] * il), pack2bf(o[r][2] * il, o[r][3] * il),
+                                              pack2bf(o[r][4] * il, o[r][5] * il), pack2bf(o[r][6] * il, o[r][7] * il)};
+      }
+    }
+    return;
+  }
   float* ws = a.ws + (((int64_t)b * gridDim.x + grp) * Rpad + r0) * DA_RS;
   if (threadIdx.x < DA_R) {
     ws[threadIdx.x * DA_RS + DA_HD] = m_run;
@@ -177,16 +193,35 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
   const int r = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
   const int nh = (int)a.nh, t = r / nh, h = r % nh;
   const int Rpad = ((int)(a.T * a.nh) + DA_R - 1) / DA_R * DA_R;
-  const float* ws = a.ws + (int64_t)b * nchunks * Rpad * DA_RS + r * DA_RS;
-  float M = -INFINITY;
-  for (int c = 0; c < nchunks; ++c) M = fmaxf(M, ws[(int64_t)c * Rpad * DA_RS + DA_HD]);
-  float o = 0.f, l = 0.f;
-  for (int c = 0; c < nchunks; ++c) {
-    const float* w = ws + (int64_t)c * Rpad * DA_RS;
-    const float mc = w[DA_HD];
-    const float s = mc == -INFINITY ? 0.f : __expf(mc - M);
-    o += s * w[d];
-    l += s * w[DA_HD + 1];
+  const int64_t cs = (int64_t)Rpad * DA_RS;  // chunk stride
+  const float* ws = a.ws + (int64_t)b * nchunks * cs + r * DA_RS;
+  // batches of 16 chunks: every (m, l, O[d]) load of a batch issued before any is consumed (the merge
+  // is a chain of tiny dependent loads otherwise); running max / rescale across batches, fixed order
+  constexpr int CB = 16;
+  float M = -INFINITY, o = 0.f, l = 0.f;
+  for (int c0 = 0; c0 < nchunks; c0 += CB) {
+    float mv[CB], lv[CB], ov[CB];
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const bool ok = c0 + u < nchunks;
+      const float* w = ws + (int64_t)(ok ? c0 + u : 0) * cs;
+      mv[u] = ok ? w[DA_HD] : -INFINITY;
+      lv[u] = ok ? w[DA_HD + 1] : 0.f;
+      ov[u] = ok ? w[d] : 0.f;
+    }
+    float Mn = M;
+#pragma unroll
+    for (int u = 0; u < CB; ++u) Mn = fmaxf(Mn, mv[u]);
+    const float sc = M == -INFINITY ? 0.f : __expf(M - Mn);
+    o *= sc;
+    l *= sc;
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
+      const float s = mv[u] == -INFINITY ? 0.f : __expf(mv[u] - Mn);
+      o += s * ov[u];
+      l += s * lv[u];
+    }
+    M = Mn;
   }
   bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + t) * a.ldo + (int64_t)h * DA_HD + d;
   *out = f2bf(l > 0.f ? o / l : 0.f);
@@ -216,10 +251,16 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   const int64_t wg1 = (int64_t)nchunks * a->B * rtiles;
   const char* e = getenv("PZ_DECODE_WG");  // target workgroups (A/B; read per call)
   const int64_t target = e && atoll(e) > 0 ? atoll(e) : 256;
-  const int nch = (int)((wg1 + target - 1) / target);
-  const int ngroups = (nchunks + nch - 1) / nch;
+  int nch = (int)((wg1 + target - 1) / target);
+  int ngroups = (nchunks + nch - 1) / nch;
+  if (ngroups == 1 && !(PZ_ALIGNED(a->o, 16) && a->ldo % 8 == 0)) {  // the direct-O path stores 16 B per lane
+    PZ_CHECK_ARG(nchunks > 1, "decode_attn: a single key chunk needs a 16-byte aligned O with ldo %% 8 == 0");
+    nch = (nchunks + 1) / 2;
+    ngroups = (nchunks + nch - 1) / nch;
+  }
   hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
   PZ_CHECK_LAUNCH();
+  if (ngroups == 1) return PZ_OK;  // the part kernel wrote O
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
                      ngroups);
   PZ_CHECK_LAUNCH();

@@ -378,17 +378,29 @@ __global__ void __launch_bounds__(256) flash_fwd_combine_kernel(pz_flash_args a,
   const int64_t zr = i / (HD / 4), r = zr % a.nq, zh = zr / a.nq;
   const float* pO = (const float*)a.ws;
   const float* pml = pO + (int64_t)nsp * ZH * a.nq * HD;
+  // every split's (m, l, O[d..d+3]) loaded before any is consumed (nsp <= 16, host-checked): one round
+  // of independent loads instead of a dependent chain per split
+  constexpr int SMAX = 16;
+  float mv[SMAX], lv[SMAX];
+  f32x4 ov[SMAX];
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    const bool ok = s < nsp;
+    const int64_t row = ((int64_t)(ok ? s : 0) * ZH + zh) * a.nq + r;
+    mv[s] = ok ? pml[2 * row] : -INFINITY;
+    lv[s] = ok ? pml[2 * row + 1] : 0.f;
+    ov[s] = ok ? *reinterpret_cast<const f32x4*>(pO + row * HD + d) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   float M = -INFINITY;
-  for (int s = 0; s < nsp; ++s) M = fmaxf(M, pml[2 * ((s * ZH + zh) * a.nq + r)]);
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) M = fmaxf(M, mv[s]);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float L = 0.f;
-  for (int s = 0; s < nsp; ++s) {
-    const int64_t row = (s * ZH + zh) * a.nq + r;
-    const float ms = pml[2 * row];
-    if (ms == -INFINITY) continue;
-    const float w = __expf(ms - M);
-    L += w * pml[2 * row + 1];
-    acc += w * *reinterpret_cast<const f32x4*>(pO + row * HD + d);
+#pragma unroll
+  for (int s = 0; s < SMAX; ++s) {
+    const float w = mv[s] == -INFINITY ? 0.f : __expf(mv[s] - M);
+    L += w * lv[s];
+    acc += w * ov[s];
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   const FaRow fr{&a};

@@ -1698,7 +1698,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
 // Split tail, second pass: 16 blocks of 512 threads per leftover tile (one accumulator row-block rb and
 // one column half each, so the partial sums stream through many CUs); thread t sums the tail_s
 // partial accumulators it owned in gemm8p_kernel (fixed order) and applies the same epilogue.
-template <bool GEGLU>
+template <bool GEGLU, int PB = 8>
 __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
   const int tile = blockIdx.x >> 4, rb = (blockIdx.x >> 1) & 7, h = blockIdx.x & 1;
   int tm, tn;
@@ -1707,20 +1707,20 @@ __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
   const f32x4* W = reinterpret_cast<const f32x4*>(p.ws) + (int64_t)tile * p.tail_s * (32 * NT2);
   // GeGLU pairs gate cb = h with up cb = h + 2; plain outputs take cb = 2h, 2h + 1
   const int c0 = GEGLU ? h : 2 * h, c1 = GEGLU ? h + 2 : 2 * h + 1;
-  // pieces loaded 4 at a time (all in flight together), summed in piece order (deterministic)
+  // pieces loaded PB at a time (2 PB loads in flight per thread), summed in piece order (deterministic)
   const f32x4* W0 = W + (rb * 4 + c0) * NT2 + t;
   const f32x4* W1 = W + (rb * 4 + c1) * NT2 + t;
   f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-  for (int z = 0; z < p.tail_s; z += 4) {
-    f32x4 v0[4], v1[4];
+  for (int z = 0; z < p.tail_s; z += PB) {
+    f32x4 v0[PB], v1[PB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PB; ++u) {
       const bool ok = z + u < p.tail_s;
       v0[u] = ok ? W0[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
       v1[u] = ok ? W1[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PB; ++u) {
       a0 += v0[u];
       a1 += v1[u];
     }
@@ -2458,7 +2458,7 @@ static int launch8p_f8(const GemmP& p, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(units, 1), dim3(NT2), smem, st, p);
   PZ_CHECK_LAUNCH();
   if (p.tail_s) {
-    hipLaunchKernelGGL(gemm8p_tail_epilogue<GEGLU>, dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+    launch_tail<GEGLU>(p, T, st);
     PZ_CHECK_LAUNCH();
   }
   return PZ_OK;
@@ -2502,6 +2502,16 @@ static bool use_khalf(bool akc, bool bkc) {
   return !(akc && bkc);
 }
 
+// split-tail merge; PZ_TAIL_PB = 4 | 8 partial pieces loaded per round (A/B; read per call)
+template <bool GEGLU>
+static void launch_tail(const GemmP& p, int T, hipStream_t st) {
+  const char* e = getenv("PZ_TAIL_PB");
+  if (e && atoi(e) == 4)
+    hipLaunchKernelGGL((gemm8p_tail_epilogue<GEGLU, 4>), dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm8p_tail_epilogue<GEGLU, 8>), dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+}
+
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
@@ -2517,7 +2527,7 @@ static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(units, (unsigned)batch), dim3(NT2), smem, st, p);
   PZ_CHECK_LAUNCH();
   if (p.tail_s) {
-    hipLaunchKernelGGL(gemm8p_tail_epilogue<GEGLU>, dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
+    launch_tail<GEGLU>(p, T, st);
     PZ_CHECK_LAUNCH();
   }
   return PZ_OK;

@@ -2337,7 +2337,8 @@ Plan make_plan(const pz_gemm_args* a) {
     if (use_8phase()) plan_tail(cand, a);
     // enough workgroups to fill the chip: whole tiles, or tiles split into K-pieces
     const int64_t units = cand.tail_s ? cand.dp_tiles + (tm * tn - cand.dp_tiles) * cand.tail_s : a->batch * tm * tn;
-    if (units >= 160) return cand;
+    const char* mu = getenv("PZ_GEMM_256_MINUNITS");  // A/B: workgroups the 256-tile path must reach
+    if (units >= (mu ? atoll(mu) : 160)) return cand;
   }
   pl.kind = PATH_TILE;
   pl.tiles_m = (a->M + BM - 1) / BM;

@@ -44,12 +44,13 @@ def main():
             t1 = graph_us(lambda: ops.linear(x, W, out), a.n)
             n1 = ops.gemm_kernel_name(M, N, K)
             os.environ.pop("PZ_SK64_MAXM")
-            os.environ["PZ_SPLITK"] = "0"
+            os.environ["PZ_GEMM_256_MINM"], os.environ["PZ_GEMM_256_MINUNITS"] = "1", "1"
             t2 = graph_us(lambda: ops.linear(x, W, out), a.n)
-            n2 = "no split-K"
-            os.environ.pop("PZ_SPLITK")
+            n2 = ops.gemm_kernel_name(M, N, K)
+            os.environ.pop("PZ_GEMM_256_MINM")
+            os.environ.pop("PZ_GEMM_256_MINUNITS")
             print(f"{name:8s} M={M} N={N} K={K}: default {t0:7.2f} us ({n0})   row-chunked {t1:7.2f} us ({n1})   "
-                  f"whole-K tiles {t2:7.2f} us")
+                  f"256-tile {t2:7.2f} us ({n2})")
         return
     for name, N, K, epi in shapes:
         x = (torch.randn(M, K, device=dev)).to(torch.bfloat16)

@@ -1131,6 +1131,419 @@ __global__ void __launch_bounds__(FR_NW * 64) flash_bwd_kv_res_kernel(pz_flash_a
 constexpr int FR_SMEM_KQ = 2 * FR_MAX * FaDims<72>::ROW * 2;  // forward / dQ: K + V images
 constexpr int FR_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FA_KB * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
 
+// ---- one workgroup per unit (SigLIP: 16 heads x 72, 256 tokens) -----------------------------
+// The resident kernels above give each unit 2 (forward, dQ) or 4 (dK/dV) workgroups, and every one
+// of them stages the unit's whole resident side (114 KiB) before its first MFMA: at one workgroup
+// per CU the staging is most of their time (dK/dV: 585 MB staged per micro-batch layer).  Here one
+// workgroup of 8 waves owns the whole unit, each wave 32 rows (queries) or 32 keys, so each
+// resident operand is staged once per unit, every LDS fragment read feeds two MFMAs (two 16-row
+// blocks), and the dK/dV pass takes its K/V fragments straight from global memory into registers
+// (no K/V image, no query-half reduction).  Grid = Z * H workgroups (1024 per micro-batch layer).
+constexpr int FU_NW = 8;
+
+// PLAIN (no mask, no soft-cap: SigLIP): the element-wise softmax in the log2 domain with the scale
+// folded into one multiply and no mask / -inf guards -- the per-score VALU work, not the MFMAs,
+// bounds these head-72 kernels (5 instead of ~17 vector instructions per score)
+constexpr float FA_LOG2E = 1.4426950408889634f, FA_LN2 = 0.6931471805599453f;
+
+template <int HD, bool PLAIN>
+__global__ void __launch_bounds__(FU_NW * 64) flash_fwd_unit_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FU_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Vall = Kall + FR_MAX * D::ROW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stk, stv;
+    stk.load(K, a.ldk, 0, a.nk);
+    stv.load(V, a.ldv, 0, a.nk);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Kall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Vall);
+    stk.store(Kall);
+    stv.store(Vall);
+  }
+  bf16x8 qf[2][D::NKS];
+  int t[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t rq = wave * 32 + qb * 16 + (lane & 15);
+    t[qb] = mk.token((int)rq);
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      qf[qb][ks] = (rq < a.nq && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + rq * a.ldq + c) : bf16x8{};
+    }
+  }
+  f32x4 o[D::NDB][2];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) o[db][0] = o[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};
+  const float sl2 = a.scale * FA_LOG2E;
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Kall + kb * FA_KB * D::ROW;
+    const bf16_t* Vs = Vall + kb * FA_KB * D::ROW;
+    f32x4 sc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[i][0] = sc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 kf = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+        sc[i][0] = mfma(kf, qf[0][ks], sc[i][0]);
+        sc[i][1] = mfma(kf, qf[1][ks], sc[i][1]);
+      }
+    bf16x8 pf[2][2];  // [k-step of 32 keys][query block]
+    const bool full = (kb + 1) * FA_KB <= (int)a.nk;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = kb * FA_KB + i * 16 + 4 * g + e;
+          float x;
+          if constexpr (PLAIN) {
+            x = sc[i][qb][e] * sl2;  // log2-domain logit
+            if (!full && j >= (int)a.nk) x = -INFINITY;
+          } else {
+            x = fa_logit(mk, sc[i][qb][e], t[qb], j);
+          }
+          sc[i][qb][e] = x;
+          mx = fmaxf(mx, x);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qb], mx);
+      float sum = 0.f, alpha;
+      if constexpr (PLAIN) {  // key 0 is valid: mn is finite from the first block on; exp2(-inf) = 0
+        alpha = __builtin_amdgcn_exp2f(m[qb] - mn);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = __builtin_amdgcn_exp2f(sc[i][qb][e] - mn);
+            sc[i][qb][e] = pv;
+            sum += pv;
+          }
+      } else {
+        alpha = mn == -INFINITY ? 1.f : __expf(m[qb] - mn);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = mn == -INFINITY ? 0.f : __expf(sc[i][qb][e] - mn);
+            sc[i][qb][e] = pv;
+            sum += pv;
+          }
+      }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      l[qb] = l[qb] * alpha + sum;
+      m[qb] = mn;
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) o[db][qb] *= alpha;
+      pf[0][qb] = pack8(sc[0][qb], sc[1][qb]);
+      pf[1][qb] = pack8(sc[2][qb], sc[3][qb]);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) {
+        const bf16x8 vf = frag_tr<D::ROW>(Vs, k2 * 32, db * 16, lane);
+        o[db][0] = mfma(vf, pf[k2][0], o[db][0]);
+        o[db][1] = mfma(vf, pf[k2][1], o[db][1]);
+      }
+  }
+  const FaRow fr{&a};
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t rq = wave * 32 + qb * 16 + (lane & 15);
+    if (rq >= a.nq) continue;
+    const float inv = l[qb] > 0.f ? 1.f / l[qb] : 0.f;
+    const int gi = fr.grp(rq);
+    bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, rq, gi);
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD)
+        *reinterpret_cast<u32x2*>(O + d) =
+            u32x2{pack2bf(o[db][qb][0] * inv, o[db][qb][1] * inv), pack2bf(o[db][qb][2] * inv, o[db][qb][3] * inv)};
+    }
+    if (g == 0 && a.lse) a.lse[zh * a.nq + rq] = PLAIN ? m[qb] * FA_LN2 + __logf(l[qb]) : m[qb] + __logf(l[qb]);
+  }
+}
+
+// dQ (+ delta): one workgroup per unit, K / V resident, wave w owns query rows 32w .. 32w + 31
+template <int HD, bool PLAIN>
+__global__ void __launch_bounds__(FU_NW * 64) flash_bwd_q_unit_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FU_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Vall = Kall + FR_MAX * D::ROW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaRow fr{&a};
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stk, stv;
+    stk.load(K, a.ldk, 0, a.nk);
+    stv.load(V, a.ldv, 0, a.nk);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Kall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Vall);
+    stk.store(Kall);
+    stv.store(Vall);
+  }
+  bf16x8 qf[2][D::NKS], df[2][D::NKS];
+  float del[2], lse[2];
+  int tq[2];
+  bool live[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t r = wave * 32 + qb * 16 + (lane & 15);
+    live[qb] = r < a.nq;
+    tq[qb] = mk.token((int)r);
+    const bf16_t* dOr = nullptr;
+    const bf16_t* Or = nullptr;
+    if (live[qb]) {
+      const int gi = fr.grp(r);
+      dOr = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
+      Or = (const bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+    }
+    float dl = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      const bool ok = live[qb] && c < HD;
+      qf[qb][ks] = ok ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+      df[qb][ks] = ok ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
+      if (ok) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dl += (float)df[qb][ks][e] * (float)ov[e];
+      }
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    del[qb] = dl;
+    if (live[qb] && g == 0) a.delta[zh * a.nq + r] = dl;
+    lse[qb] = live[qb] ? a.lse[zh * a.nq + r] : 0.f;
+    if constexpr (PLAIN) lse[qb] *= FA_LOG2E;
+  }
+  const float sl2 = a.scale * FA_LOG2E;
+  f32x4 dq[D::NDB][2];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dq[db][0] = dq[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Kall + kb * FA_KB * D::ROW;
+    const bf16_t* Vs = Vall + kb * FA_KB * D::ROW;
+    f32x4 ds[4][2];  // dS^T[key 16i + 4g + e][query of block qb]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 kfr[D::NKS], vfr[D::NKS];
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        kfr[ks] = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+        vfr[ks] = frag_row<D::ROW>(Vs, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < D::NKS; ++ks) {
+          sv = mfma(kfr[ks], qf[qb][ks], sv);
+          dp = mfma(vfr[ks], df[qb][ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = kb * FA_KB + i * 16 + 4 * g + e;
+          float dse = 0.f;
+          if constexpr (PLAIN) {  // keys past nk are zero rows of the K / V images: no contribution;
+            // dS without the scale (applied to dQ once, in the epilogue)
+            dse = __builtin_amdgcn_exp2f(sv[e] * sl2 - lse[qb]) * (dp[e] - del[qb]);
+          } else if (live[qb]) {
+            const FaLogit lg = fa_logit_d(mk, sv[e], tq[qb], j);
+            const float pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse[qb]);
+            dse = pe * (dp[e] - del[qb]) * lg.dxds;
+          }
+          ds[i][qb][e] = dse;
+        }
+      }
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const bf16x8 sb0 = pack8(ds[2 * k2][0], ds[2 * k2 + 1][0]);
+      const bf16x8 sb1 = pack8(ds[2 * k2][1], ds[2 * k2 + 1][1]);
+#pragma unroll
+      for (int db = 0; db < D::NDB; ++db) {
+        const bf16x8 kt = frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane);
+        dq[db][0] = mfma(kt, sb0, dq[db][0]);
+        dq[db][1] = mfma(kt, sb1, dq[db][1]);
+      }
+    }
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    if (!live[qb]) continue;
+    const int64_t r = wave * 32 + qb * 16 + (lane & 15);
+    bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+    const float f = PLAIN ? a.scale : 1.f;
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD)
+        *reinterpret_cast<u32x2*>(dQ + d) =
+            u32x2{pack2bf(dq[db][qb][0] * f, dq[db][qb][1] * f), pack2bf(dq[db][qb][2] * f, dq[db][qb][3] * f)};
+    }
+  }
+}
+
+// dK, dV: one workgroup per unit, Q / dO / lse / delta resident; wave w owns keys 32w .. 32w + 31,
+// their K / V fragments loaded once from global memory into registers
+template <int HD, bool PLAIN>
+__global__ void __launch_bounds__(FU_NW * 64) flash_bwd_kv_unit_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = FU_NW * 64;
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  bf16_t* Qall = reinterpret_cast<bf16_t*>(fa_smem);
+  bf16_t* Dall = Qall + FR_MAX * D::ROW;
+  float* lse_all = reinterpret_cast<float*>(Dall + FR_MAX * D::ROW);
+  float* del_all = lse_all + FR_MAX;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  {
+    TileStager<HD, D::ROW, FR_MAX, NT> stq, std_;
+    stq.load_q(a, Q, b, h, 0, false);
+    std_.load_q(a, Q, b, h, 0, true);
+    const int tr = threadIdx.x;
+    const float lv = tr < FR_MAX && tr < a.nq ? a.lse[zh * a.nq + tr] : 0.f;
+    const float dv_ = tr < FR_MAX && tr < a.nq ? a.delta[zh * a.nq + tr] : 0.f;
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Qall);
+    zero_pad_cols<HD, D::HDK, D::ROW, FR_MAX, NT>(Dall);
+    stq.store(Qall);
+    std_.store(Dall);
+    if (tr < FR_MAX) {
+      lse_all[tr] = PLAIN ? lv * FA_LOG2E : lv;
+      del_all[tr] = dv_;
+    }
+  }
+  const float sl2 = a.scale * FA_LOG2E;
+  // B operands of S = Q K^T / dP = dO V^T: n = key (lane & 15), k = head dim 32 ks + 8g ..
+  bf16x8 kfr[2][D::NKS], vfr[2][D::NKS];
+  int key[2];
+#pragma unroll
+  for (int kb2 = 0; kb2 < 2; ++kb2) {
+    key[kb2] = wave * 32 + kb2 * 16 + (lane & 15);
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      const bool ok = key[kb2] < a.nk && c < HD;
+      kfr[kb2][ks] = ok ? *reinterpret_cast<const bf16x8*>(K + (int64_t)key[kb2] * a.ldk + c) : bf16x8{};
+      vfr[kb2][ks] = ok ? *reinterpret_cast<const bf16x8*>(V + (int64_t)key[kb2] * a.ldv + c) : bf16x8{};
+    }
+  }
+  f32x4 dk[D::NDB][2], dv[D::NDB][2];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dk[db][0] = dk[db][1] = dv[db][0] = dv[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  const int nqs = (int)((a.nq + FA_QS - 1) / FA_QS);
+  for (int qs = 0; qs < nqs; ++qs) {
+    const int r0 = qs * FA_QS;
+    const bf16_t* Qs = Qall + r0 * D::ROW;
+    const bf16_t* Ds = Dall + r0 * D::ROW;
+    f32x4 p[2][2], ds[2][2];  // [16-row query block][key block of the wave]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float l2r[4], dlr[4];  // this lane's 4 rows of the block (shared by both key blocks)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        l2r[e] = lse_all[r0 + i * 16 + 4 * g + e];
+        dlr[e] = del_all[r0 + i * 16 + 4 * g + e];
+      }
+      bf16x8 qa[D::NKS], da[D::NKS];
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        qa[ks] = frag_row<D::ROW>(Qs, i * 16, ks * 32, lane);
+        da[ks] = frag_row<D::ROW>(Ds, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int kb2 = 0; kb2 < 2; ++kb2) {
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < D::NKS; ++ks) {
+          sv = mfma(qa[ks], kfr[kb2][ks], sv);
+          dp = mfma(da[ks], vfr[kb2][ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = r0 + i * 16 + 4 * g + e;
+          float pe = 0.f, dse = 0.f;
+          if constexpr (PLAIN) {  // query rows past nq are zero rows of the Q / dO images: no contribution;
+            // dS without the scale (applied to dK once, in the epilogue)
+            pe = __builtin_amdgcn_exp2f(sv[e] * sl2 - l2r[e]);
+            dse = pe * (dp[e] - dlr[e]);
+          } else if (rr < a.nq) {
+            const FaLogit lg = fa_logit_d(mk, sv[e], mk.token(rr), key[kb2]);
+            pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - l2r[e]);
+            dse = pe * (dp[e] - dlr[e]) * lg.dxds;
+          }
+          p[i][kb2][e] = pe;
+          ds[i][kb2][e] = dse;
+        }
+      }
+    }
+    const bf16x8 pb0 = pack8(p[0][0], p[1][0]), pb1 = pack8(p[0][1], p[1][1]);
+    const bf16x8 sb0 = pack8(ds[0][0], ds[1][0]), sb1 = pack8(ds[0][1], ds[1][1]);
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const bf16x8 dt = frag_tr<D::ROW>(Ds, 0, db * 16, lane);
+      const bf16x8 qt = frag_tr<D::ROW>(Qs, 0, db * 16, lane);
+      dv[db][0] = mfma(dt, pb0, dv[db][0]);
+      dv[db][1] = mfma(dt, pb1, dv[db][1]);
+      dk[db][0] = mfma(qt, sb0, dk[db][0]);
+      dk[db][1] = mfma(qt, sb1, dk[db][1]);
+    }
+  }
+#pragma unroll
+  for (int kb2 = 0; kb2 < 2; ++kb2) {
+    if (key[kb2] >= a.nk) continue;
+    bf16_t* dK = (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + (int64_t)key[kb2] * a.ldk;
+    bf16_t* dV = (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + (int64_t)key[kb2] * a.ldv;
+    const float f = PLAIN ? a.scale : 1.f;
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD) {
+        *reinterpret_cast<u32x2*>(dK + d) = u32x2{pack2bf(dk[db][kb2][0] * f, dk[db][kb2][1] * f),
+                                                  pack2bf(dk[db][kb2][2] * f, dk[db][kb2][3] * f)};
+        *reinterpret_cast<u32x2*>(dV + d) =
+            u32x2{pack2bf(dv[db][kb2][0], dv[db][kb2][1]), pack2bf(dv[db][kb2][2], dv[db][kb2][3])};
+      }
+    }
+  }
+}
+
+constexpr int FU_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
+
 }  // namespace
 
 // head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
@@ -1149,6 +1562,15 @@ static bool fa_resident(const pz_flash_args* a) {
   if (e && e[0] == '0') return false;
   return a->head_dim == 72 && a->nq <= FR_MAX && a->nk <= FR_MAX;
 }
+
+// one workgroup per unit for the resident shape ("0": the 2- / 4-workgroup resident kernels, A/B runs)
+static bool fa_unit() {
+  const char* e = getenv("PZ_FLASH_UNIT");
+  return !(e && e[0] == '0');
+}
+
+// no mask, no soft-cap (SigLIP): the unit kernels' log2-domain element-wise fast path
+static bool fa_plain(const pz_flash_args* a) { return a->mask_mode == 0 && a->cap == 0.f; }
 
 // Raise the kernel's dynamic-LDS limit once; a refusal is cleared here (the launch is checked on
 // its own) so it cannot surface as a later launch's error
@@ -1191,6 +1613,20 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   }
   dim3 grid((unsigned)qblk, (unsigned)(a->Z * a->H), (unsigned)sp);
   hipStream_t st = (hipStream_t)stream;
+  if (sp == 1 && fa_resident(a) && fa_unit()) {
+    static bool attr = false;
+    static bool attr2 = false;
+    const dim3 gu((unsigned)(a->Z * a->H));
+    if (fa_plain(a)) {
+      fa_smem_attr(flash_fwd_unit_kernel<72, true>, FR_SMEM_KQ, attr);
+      hipLaunchKernelGGL((flash_fwd_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);
+    } else {
+      fa_smem_attr(flash_fwd_unit_kernel<72, false>, FR_SMEM_KQ, attr2);
+      hipLaunchKernelGGL((flash_fwd_unit_kernel<72, false>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);
+    }
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   if (sp == 1 && fa_resident(a)) {
     static bool attr = false;
     fa_smem_attr(flash_fwd_res_kernel<72>, FR_SMEM_KQ, attr);
@@ -1240,6 +1676,25 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
   dim3 gkv((unsigned)nkb, (unsigned)(a->Z * a->H), (unsigned)splits);
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
+  if (fa_resident(a) && fa_unit()) {
+    static bool aq = false, akv = false, aq2 = false, akv2 = false;
+    const dim3 gu((unsigned)(a->Z * a->H));
+    if (fa_plain(a)) {
+      fa_smem_attr(flash_bwd_q_unit_kernel<72, true>, FR_SMEM_KQ, aq);
+      fa_smem_attr(flash_bwd_kv_unit_kernel<72, true>, FU_SMEM_KV, akv);
+      hipLaunchKernelGGL((flash_bwd_q_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);
+      PZ_CHECK_LAUNCH();
+      hipLaunchKernelGGL((flash_bwd_kv_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FU_SMEM_KV, st, *a);
+    } else {
+      fa_smem_attr(flash_bwd_q_unit_kernel<72, false>, FR_SMEM_KQ, aq2);
+      fa_smem_attr(flash_bwd_kv_unit_kernel<72, false>, FU_SMEM_KV, akv2);
+      hipLaunchKernelGGL((flash_bwd_q_unit_kernel<72, false>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);
+      PZ_CHECK_LAUNCH();
+      hipLaunchKernelGGL((flash_bwd_kv_unit_kernel<72, false>), gu, dim3(FU_NW * 64), FU_SMEM_KV, st, *a);
+    }
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   if (fa_resident(a)) {
     static bool aq = false, akv = false;
     fa_smem_attr(flash_bwd_q_res_kernel<72>, FR_SMEM_KQ, aq);

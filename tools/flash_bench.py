@@ -65,9 +65,13 @@ def main():
     dqkv = torch.empty_like(qkv)
     sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
     fl = 4.0 * B * nh * N * N * hd
-    tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
-    tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
-    print(f"siglip fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
+    for unit in ("1", "0"):  # PZ_FLASH_UNIT: one workgroup per (image, head) unit vs the 2-/4-workgroup kernels
+        os.environ["PZ_FLASH_UNIT"] = unit
+        tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
+        tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
+        print(f"siglip(unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s",
+              flush=True)
+    os.environ.pop("PZ_FLASH_UNIT")
 
 
 if __name__ == "__main__":

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 12
+#define PZ_ABI_VERSION 13
 
 enum {
   PZ_OK = 0,
@@ -228,6 +228,13 @@ typedef struct pz_flash_args {
   int64_t mask_row0;
 } pz_flash_args;
 int pz_flash_fwd(const pz_flash_args* a, void* stream);
+/* Joint attention forward that also exports the softmax (head_dim 256, nk <= 320, mask mode 0/1;
+ * joint_model.py:259-292, pizero.py:271-306): O as pz_flash_fwd (no lse), plus P[z][r][0..ldp) =
+ * the bf16 row softmax and tcap[z][r][..] = tanh(scale*s/cap) (NULL: not stored) with exactly
+ * pz_attn_softmax's conventions (fully masked rows uniform over the nk keys with tcap 0, zeros past
+ * nk), so the GEMM-path backward (P / tcap consumers) runs unchanged.  Replaces the S GEMM +
+ * pz_attn_softmax + P V GEMM of the reference's eager attention (joint_model.py:261-292). */
+int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, int64_t ldp, void* stream);
 /* delta[z][r] = sum_d dO[r][d] * O[r][d] (fp32) */
 int pz_flash_bwd_prep(const pz_flash_args* a, void* stream);
 /* dQ and delta (query-parallel), then dK, dV (key-parallel over all query rows of the unit); overwrite */

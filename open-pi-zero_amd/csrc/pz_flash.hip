@@ -186,6 +186,21 @@ struct FaMask {
   }
 };
 
+// 1-D grid of nblk workgroups per unit: the nblk workgroups of one unit get ids of one residue mod 8,
+// i.e. land on one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2 for the
+// unit's resident operand, which every one of them stages
+__device__ __forceinline__ void fa_unit_block(int nblk, int units, int64_t& zh, int& blk) {
+  const int id = blockIdx.x;
+  if (units % 8 == 0) {
+    const int xcd = id & 7, local = id >> 3;
+    zh = (int64_t)(local / nblk) * 8 + xcd;
+    blk = local % nblk;
+  } else {
+    zh = id / nblk;
+    blk = id % nblk;
+  }
+}
+
 // logits with soft-cap and mask for key j of a query row of token t; dead rows (pad tokens of the
 // prefix, pizero.py:291: finfo.min absorbs s) attend uniformly to every key
 __device__ __forceinline__ float fa_logit(const FaMask& mk, float s, int t, int j) {
@@ -430,6 +445,55 @@ __device__ __forceinline__ FaLogit fa_logit_d(const FaMask& mk, float s, int t, 
   return o;
 }
 
+// ---- fast element-wise path of the joint backward (soft-cap and/or the Pi0 block mask) ----------
+// The per-score vector work bounds the step-staged backward kernels as much as their MFMAs do, so
+// each score costs: exp2(s k2) -> rcp -> th (soft-cap tanh), exp2(th * crow - lse2) = P, the mask as
+// one bit test (and only in key blocks that reach past the valid prefix), dS' = P (dP - delta)
+// (1 - th^2); the softmax scale is applied once to dQ / dK instead of per score.
+//   key class kc(j): 0 j < cnt, 1 cond token, 2 action token, 3 prefix padding, 4 j >= nk
+//   row bits rb(t) over key classes: valid prefix 0x1, cond 0x3, action 0x7, dead prefix row 0xF
+//   (dead rows attend every key with logit 0: crow = 0); no mask: every row 0xF
+__device__ __forceinline__ int fa_row_bits(const FaMask& mk, int t) {
+  if (mk.mode != 1) return 0xF;
+  if (t < mk.P) return t < mk.cnt ? 0x1 : 0xF;
+  return t < mk.P + mk.C ? 0x3 : 0x7;
+}
+__device__ __forceinline__ int fa_key_class(const FaMask& mk, int j) {
+  if (j >= mk.nk) return 4;
+  if (mk.mode != 1 || j < mk.cnt) return 0;
+  if (j < mk.P) return 3;
+  return j < mk.P + mk.C ? 1 : 2;
+}
+// keys [0, fa_full_keys) are class 0: allowed for every row
+__device__ __forceinline__ int fa_full_keys(const FaMask& mk) { return mk.mode == 1 ? min(mk.cnt, mk.nk) : mk.nk; }
+
+struct FaFast {
+  float k2, crow_live, scale;  // exp2 argument of tanh's exp(2u), log2-domain logit factor
+  __device__ __forceinline__ FaFast(const pz_flash_args& a) {
+    scale = a.scale;
+    k2 = a.cap > 0.f ? 2.f * a.scale / a.cap * 1.4426950408889634f : 0.f;
+    crow_live = (a.cap > 0.f ? a.cap : a.scale) * 1.4426950408889634f;
+  }
+  // P and dS' (dS / scale) of raw score s and dP; masked -> 0
+  template <bool CAP>
+  __device__ __forceinline__ void eval(float s, float dp, float lse2, float crow, float del, bool ok, float& p,
+                                       float& ds) const {
+    float pe, dd;
+    if constexpr (CAP) {
+      const float e2 = __builtin_amdgcn_exp2f(s * k2);
+      const float th = fmaf(-2.f, __builtin_amdgcn_rcpf(e2 + 1.f), 1.f);
+      pe = __builtin_amdgcn_exp2f(fmaf(th, crow, -lse2));
+      dd = fmaf(-th, th, 1.f);
+    } else {
+      pe = __builtin_amdgcn_exp2f(fmaf(s, crow, -lse2));
+      dd = 1.f;
+    }
+    pe = ok ? pe : 0.f;
+    p = pe;
+    ds = pe * (dp - del) * dd;
+  }
+};
+
 // delta[z][r] = sum_d dO[r][d] O[r][d]: one wave per row
 template <int HD>
 __global__ void __launch_bounds__(256) flash_bwd_prep_kernel(pz_flash_args a) {
@@ -458,18 +522,26 @@ __global__ void __launch_bounds__(256) flash_bwd_prep_kernel(pz_flash_args a) {
 
 // dK, dV: grid (ceil(nk / 64), Z * H), 4 waves; wave w owns keys kb*64 + 16w + (lane & 15) and
 // sweeps every query row of the unit in staged steps of 32 (Q, dO, lse, delta in LDS)
-template <int HD>
-__global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_kernel(pz_flash_args a) {
+// FM: 0 generic element-wise (fa_logit_d), 1 fast path (FaFast), 2 fast path with the soft-cap.
+// 1-D grid of nkb x (units x splits) workgroups, the key blocks of one (unit, split) on one XCD.
+template <int HD, int FM>
+__global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_kernel(pz_flash_args a, int splits) {
   using D = FaDims<HD>;
   constexpr int NT = FA_NW * 64;
   __shared__ __attribute__((aligned(16))) bf16_t Qs2[2][FA_QS * D::ROW];  // double-buffered Q / dO steps
   __shared__ __attribute__((aligned(16))) bf16_t Ds2[2][FA_QS * D::ROW];
-  __shared__ float lse2[2][FA_QS], del2[2][FA_QS];
+  __shared__ float lse2[2][FA_QS], del2[2][FA_QS], crw2[2][FA_QS];
+  __shared__ int rbw2[2][FA_QS];
   __shared__ __attribute__((aligned(16))) bf16_t Kk[FA_KB * D::ROW];  // this workgroup's 64 keys / values
   __shared__ __attribute__((aligned(16))) bf16_t Vk[FA_KB * D::ROW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int64_t zh = blockIdx.y, b = zh / a.H, h = zh % a.H;
-  const int k0 = blockIdx.x * FA_KB;
+  const int64_t ZH = a.Z * a.H;
+  int64_t grp;
+  int kblk;
+  fa_unit_block((int)((a.nk + FA_KB - 1) / FA_KB), (int)(ZH * splits), grp, kblk);
+  const int64_t zh = grp % ZH, b = zh / a.H, h = zh % a.H;
+  const int split = (int)(grp / ZH);
+  const int k0 = kblk * FA_KB;
   const int key = k0 + wave * 16 + (lane & 15);
   const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
   const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
@@ -481,18 +553,29 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Qs2[bi]);
     zero_pad_cols<HD, D::HDK, D::ROW, FA_QS, NT>(Ds2[bi]);
   }
-  // query split (blockIdx.z of gridDim.z): this workgroup sweeps query steps [qs0, qs1)
+  // query split: this workgroup sweeps query steps [qs0, qs1)
   const int nqs_all = (int)((a.nq + FA_QS - 1) / FA_QS);
-  const int per = (nqs_all + (int)gridDim.z - 1) / (int)gridDim.z;
-  const int qs0 = min(nqs_all, (int)blockIdx.z * per), qs1 = min(nqs_all, qs0 + per);
+  const int per = (nqs_all + splits - 1) / splits;
+  const int qs0 = min(nqs_all, split * per), qs1 = min(nqs_all, qs0 + per);
+  const FaFast ff(a);
+  // fast path: this lane's key class and whether the wave's 16 keys are all class 0 (no mask test)
+  const int kcl = fa_key_class(mk, key);
+  const bool wfull = k0 + wave * 16 + 16 <= fa_full_keys(mk);
   TileStager<HD, D::ROW, FA_QS, NT> stq, std_;
   stq.load_q(a, Q, b, h, (int64_t)qs0 * FA_QS, false);
   std_.load_q(a, Q, b, h, (int64_t)qs0 * FA_QS, true);
-  float lse_v = 0.f, del_v = 0.f;  // threads < FA_QS carry one row's lse / delta
+  float lse_v = 0.f, del_v = 0.f, crw_v = 0.f;  // threads < FA_QS carry one row's lse / delta / mask
+  int rbw_v = 0;
   auto load_rows = [&](int64_t r0) {
     const int64_t rr = r0 + threadIdx.x;
     lse_v = threadIdx.x < FA_QS && rr < a.nq ? a.lse[zh * a.nq + rr] : 0.f;
     del_v = threadIdx.x < FA_QS && rr < a.nq ? a.delta[zh * a.nq + rr] : 0.f;
+    if constexpr (FM != 0) {
+      const int t = mk.token((int)rr);
+      lse_v *= 1.4426950408889634f;
+      rbw_v = fa_row_bits(mk, t);
+      crw_v = mk.dead(t) ? 0.f : ff.crow_live;
+    }
   };
   load_rows((int64_t)qs0 * FA_QS);
   // this workgroup's keys / values, read as B operands (n = key, k = head dim) from LDS:
@@ -516,6 +599,8 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
   if (threadIdx.x < FA_QS) {
     lse2[0][threadIdx.x] = lse_v;
     del2[0][threadIdx.x] = del_v;
+    crw2[0][threadIdx.x] = crw_v;
+    rbw2[0][threadIdx.x] = rbw_v;
   }
   __syncthreads();
   for (int qs = qs0; qs < qs1; ++qs) {
@@ -525,6 +610,8 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     const bf16_t* Ds = Ds2[cur];
     const float* lse_s = lse2[cur];
     const float* del_s = del2[cur];
+    const float* crw_s = crw2[cur];
+    const int* rbw_s = rbw2[cur];
     const bool more = qs + 1 < qs1;
     if (more) {  // next query step in flight during this step's MFMAs
       stq.load_q(a, Q, b, h, r0 + FA_QS, false);
@@ -557,7 +644,10 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
         const int rr = i * 16 + 4 * g + e;
         const int r = (int)r0 + rr;
         float pe = 0.f, dse = 0.f;
-        if (r < a.nq) {
+        if constexpr (FM != 0) {  // rows past nq: zero Q / dO rows and delta, no contribution
+          const bool ok = wfull || ((rbw_s[rr] >> kcl) & 1);
+          ff.eval<FM == 2>(sv[e], dp[e], lse_s[rr], crw_s[rr], del_s[rr], ok, pe, dse);
+        } else if (r < a.nq) {
           const FaLogit lg = fa_logit_d(mk, sv[e], mk.token(r), key);
           pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse_s[rr]);
           dse = pe * (dp[e] - del_s[rr]) * lg.dxds;
@@ -596,15 +686,21 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
       if (threadIdx.x < FA_QS) {
         lse2[cur ^ 1][threadIdx.x] = lse_v;
         del2[cur ^ 1][threadIdx.x] = del_v;
+        crw2[cur ^ 1][threadIdx.x] = crw_v;
+        rbw2[cur ^ 1][threadIdx.x] = rbw_v;
       }
     }
     __syncthreads();
   }
   if (key >= a.nk) return;
-  if (gridDim.z > 1) {  // fp32 partial sums of this query split -> ws[split][unit][key][HD] (dK), then dV
-    const int64_t slab = (int64_t)gridDim.y * a.nk * HD;
-    float* pk = a.ws + ((int64_t)blockIdx.z * gridDim.y + zh) * a.nk * HD + (int64_t)key * HD;
-    float* pv = pk + (int64_t)gridDim.z * slab;
+  if constexpr (FM != 0) {  // the fast path's dS' excludes the softmax scale
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) dk[db] *= ff.scale;
+  }
+  if (splits > 1) {  // fp32 partial sums of this query split -> ws[split][unit][key][HD] (dK), then dV
+    const int64_t slab = ZH * a.nk * HD;
+    float* pk = a.ws + ((int64_t)split * ZH + zh) * a.nk * HD + (int64_t)key * HD;
+    float* pv = pk + (int64_t)splits * slab;
 #pragma unroll
     for (int db = 0; db < D::NDB; ++db) {
       const int d = db * 16 + 4 * g;
@@ -767,27 +863,315 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_ker
   }
 }
 
+// dQ (+ delta), fast path: 4 waves x 32 query rows (two 16-row blocks per K / V fragment read, half
+// the LDS reads per score of flash_bwd_q_kernel), 32-key blocks double-buffered in LDS (70 KiB), the
+// query blocks of one unit on one XCD (its K / V served from that L2).  1-D grid.
+constexpr int JQ_NW = 4, JQ_KB = 32;
+template <int HD, bool CAP>
+__global__ void __launch_bounds__(JQ_NW * 64, 1) flash_bwd_q2_kernel(pz_flash_args a) {
+  using D = FaDims<HD>;
+  constexpr int NT = JQ_NW * 64, RPW = JQ_NW * 32;
+  __shared__ __attribute__((aligned(16))) bf16_t Ks2[2][JQ_KB * D::ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][JQ_KB * D::ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaFast ff(a);
+  const FaRow fr{&a};
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) {
+    zero_pad_cols<HD, D::HDK, D::ROW, JQ_KB, NT>(Ks2[bi]);
+    zero_pad_cols<HD, D::HDK, D::ROW, JQ_KB, NT>(Vs2[bi]);
+  }
+  const int nkb = (int)((a.nk + JQ_KB - 1) / JQ_KB);
+  const int full_keys = fa_full_keys(mk);
+  TileStager<HD, D::ROW, JQ_KB, NT> stk, stv;
+  stk.load(K, a.ldk, 0, a.nk);
+  stv.load(V, a.ldv, 0, a.nk);
+  bf16x8 qf[2][D::NKS], df[2][D::NKS];
+  float del[2], lse2[2], crow[2];
+  int rb[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t r = (int64_t)qblk * RPW + wave * 32 + qb * 16 + (lane & 15);
+    const bool live = r < a.nq;
+    const bf16_t* dOr = nullptr;
+    const bf16_t* Or = nullptr;
+    if (live) {
+      const int gi = fr.grp(r);
+      dOr = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
+      Or = (const bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+    }
+    float dl = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      const bool ok = live && c < HD;
+      qf[qb][ks] = ok ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+      df[qb][ks] = ok ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
+      if (ok) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dl += (float)df[qb][ks][e] * (float)ov[e];
+      }
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    del[qb] = dl;
+    if (live && g == 0) a.delta[zh * a.nq + r] = dl;
+    lse2[qb] = live ? a.lse[zh * a.nq + r] * 1.4426950408889634f : 0.f;
+    const int t = mk.token((int)r);
+    rb[qb] = fa_row_bits(mk, t);
+    crow[qb] = mk.dead(t) ? 0.f : ff.crow_live;
+  }
+  f32x4 dq[D::NDB][2];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dq[db][0] = dq[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // pad columns zeroed
+  stk.store(Ks2[0]);
+  stv.store(Vs2[0]);
+  __syncthreads();
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bf16_t* Ks = Ks2[kb & 1];
+    const bf16_t* Vs = Vs2[kb & 1];
+    const bool more = kb + 1 < nkb;
+    if (more) {
+      stk.load(K, a.ldk, (int64_t)(kb + 1) * JQ_KB, a.nk);
+      stv.load(V, a.ldv, (int64_t)(kb + 1) * JQ_KB, a.nk);
+    }
+    const bool full = (kb + 1) * JQ_KB <= full_keys;
+    f32x4 ds[2][2];  // dS'^T[key 16i + 4g + e][query of block qb]
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bf16x8 kfr[D::NKS], vfr[D::NKS];
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks) {
+        kfr[ks] = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
+        vfr[ks] = frag_row<D::ROW>(Vs, i * 16, ks * 32, lane);
+      }
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < D::NKS; ++ks) {
+          sv = mfma(kfr[ks], qf[qb][ks], sv);
+          dp = mfma(vfr[ks], df[qb][ks], dp);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool ok = full || ((rb[qb] >> fa_key_class(mk, kb * JQ_KB + i * 16 + 4 * g + e)) & 1);
+          float pe, dse;
+          ff.eval<CAP>(sv[e], dp[e], lse2[qb], crow[qb], del[qb], ok, pe, dse);
+          ds[i][qb][e] = dse;
+        }
+      }
+    }
+    const bf16x8 sb0 = pack8(ds[0][0], ds[1][0]), sb1 = pack8(ds[0][1], ds[1][1]);
+    constexpr int HB = (D::NDB + 1) / 2;  // transposed K reads in two batches ahead of their MFMAs
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      bf16x8 kt[HB];
+#pragma unroll
+      for (int x = 0; x < HB; ++x)
+        if (hb * HB + x < D::NDB) kt[x] = frag_tr<D::ROW>(Ks, 0, (hb * HB + x) * 16, lane);
+#pragma unroll
+      for (int x = 0; x < HB; ++x) {
+        const int db = hb * HB + x;
+        if (db < D::NDB) {
+          dq[db][0] = mfma(kt[x], sb0, dq[db][0]);
+          dq[db][1] = mfma(kt[x], sb1, dq[db][1]);
+        }
+      }
+    }
+    if (more) {
+      stk.store(Ks2[(kb + 1) & 1]);
+      stv.store(Vs2[(kb + 1) & 1]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int64_t r = (int64_t)qblk * RPW + wave * 32 + qb * 16 + (lane & 15);
+    if (r >= a.nq) continue;
+    bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+    for (int db = 0; db < D::NDB; ++db) {
+      const int d = db * 16 + 4 * g;
+      if (d < HD)
+        *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][qb][0] * ff.scale, dq[db][qb][1] * ff.scale),
+                                                  pack2bf(dq[db][qb][2] * ff.scale, dq[db][qb][3] * ff.scale)};
+    }
+  }
+}
+
+// ---- joint forward with the softmax probabilities exported (training default) ----------------
+// One pass over K (S^T for all keys of the row block held in registers: nk <= 320), the EXACT row
+// softmax (no online rescaling: every key of a row is in the wave's registers), P and tanh(cap)
+// stored as the bf16 [row][ldp] tensors the GEMM-path backward reads (pz_attn_softmax's contract:
+// pizero.py:271-306 mask, fully masked rows uniform over the N keys with tcap 0, zeros past N), then
+// one pass over V for O = P V with the bf16 P as the MFMA operand (what the GEMM path's P V GEMM
+// reads).  No fp32 S, no separate softmax launch.  HD 256 (joint), 8 waves x 16 query rows.
+constexpr int JP_NW = 8, JP_MAXKB = 5;
+template <int HD>
+__global__ void __launch_bounds__(JP_NW * 64) flash_fwd_probs_kernel(pz_flash_args a, bf16_t* P, bf16_t* TC,
+                                                                      int64_t ldp) {
+  using D = FaDims<HD>;
+  constexpr int NT = JP_NW * 64, RPW = JP_NW * 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Ts2[2][FA_KB * D::ROW];  // K blocks, then V blocks
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)qblk * RPW + wave * 16 + (lane & 15);  // this lane's query row
+  const bool live = r < a.nq;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaFast ff(a);
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ts2[bi]);
+  TileStager<HD, D::ROW, FA_KB, NT> st;
+  st.load(K, a.ldk, 0, a.nk);
+  bf16x8 qf[D::NKS];
+#pragma unroll
+  for (int ks = 0; ks < D::NKS; ++ks) {
+    const int c = ks * 32 + 8 * g;
+    qf[ks] = (live && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
+  }
+  const int t = mk.token((int)r);
+  const bool dead = mk.dead(t);
+  const int rb = fa_row_bits(mk, t), full_keys = fa_full_keys(mk);
+  __syncthreads();  // pad columns zeroed
+  st.store(Ts2[0]);
+  __syncthreads();
+  // pass 1: S^T[key][q] for every key of the row block (stage kb = K block kb)
+  f32x4 sc[JP_MAXKB][4];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kb < nkb) {
+      const bf16_t* Ks = Ts2[kb & 1];
+      if (kb + 1 < nkb) st.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
+      else st.load(V, a.ldv, 0, a.nk);  // stage nkb: V block 0
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sc[kb][i] = mfma(frag_row<D::ROW>(Ks, i * 16, ks * 32, lane), qf[ks], sc[kb][i]);
+      st.store(Ts2[(kb + 1) & 1]);
+      __syncthreads();
+    }
+  }
+  // logits (log2 domain) + the tanh(cap) export; keys past nk / masked -> -inf
+  bf16_t* prow = P + (b * a.nq + r) * ldp;
+  bf16_t* trow = TC ? TC + (b * a.nq + r) * ldp : nullptr;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float tv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = kb * FA_KB + i * 16 + 4 * g + e;
+        const float sv = sc[kb][i][e];
+        float th = 0.f, x2;
+        if (a.cap > 0.f) {
+          th = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(sv * ff.k2) + 1.f), 1.f);
+          x2 = th * ff.crow_live;
+        } else {
+          x2 = sv * ff.crow_live;
+        }
+        const bool ok = j < (int)a.nk && (j < full_keys || ((rb >> fa_key_class(mk, j)) & 1));
+        x2 = ok ? x2 : -INFINITY;
+        sc[kb][i][e] = x2;
+        mx = fmaxf(mx, x2);
+        tv[e] = (dead || j >= (int)a.nk) ? 0.f : th;
+      }
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      if (trow && live && kb < nkb && j0 < ldp)
+        *reinterpret_cast<u32x2*>(trow + j0) = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = __builtin_amdgcn_exp2f(sc[kb][i][e] - mx);  // exp2(-inf) = 0
+        sc[kb][i][e] = pv;
+        sum += pv;
+      }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  // fully masked (dead) rows: uniform over the N keys (the finfo.min mask absorbs the logits)
+  const float inv = 1.f / sum, uni = 1.f / (float)a.nk;
+  bf16x8 pf[JP_MAXKB][2];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = kb * FA_KB + i * 16 + 4 * g + e;
+        sc[kb][i][e] = dead ? (j < (int)a.nk ? uni : 0.f) : sc[kb][i][e] * inv;
+      }
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      if (live && kb < nkb && j0 < ldp)
+        *reinterpret_cast<u32x2*>(prow + j0) =
+            u32x2{pack2bf(sc[kb][i][0], sc[kb][i][1]), pack2bf(sc[kb][i][2], sc[kb][i][3])};
+    }
+    pf[kb][0] = pack8(sc[kb][0], sc[kb][1]);
+    pf[kb][1] = pack8(sc[kb][2], sc[kb][3]);
+  }
+  // pass 2: O^T[d][q] = V^T[d][key] P^T[key][q] with the bf16 P (stage nkb + kb = V block kb)
+  f32x4 o[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    if (kb < nkb) {
+      const bf16_t* Vs = Ts2[(nkb + kb) & 1];
+      const bool more = kb + 1 < nkb;
+      if (more) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int db = 0; db < D::NDB; ++db) o[db] = mfma(frag_tr<D::ROW>(Vs, k2 * 32, db * 16, lane), pf[kb][k2], o[db]);
+      if (more) st.store(Ts2[(nkb + kb + 1) & 1]);
+      __syncthreads();
+    }
+  }
+  if (!live) return;
+  const FaRow fr{&a};
+  const int gi = fr.grp(r);
+  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(o[db][0], o[db][1]), pack2bf(o[db][2], o[db][3])};
+  }
+}
+
 // ---- resident variants (SigLIP: nq, nk <= 256) ---------------------------------
 // The whole key side (forward, dQ) or query side (dK/dV) of a unit is staged in LDS once, by
 // loads all in flight together: one global-latency round per workgroup instead of one per
 // 64-key / 32-query step, which the step-staged kernels above expose at SigLIP's small per-step
 // work (16 heads x 72).  8 waves per workgroup (two per SIMD), dynamic LDS up to 142 KiB.
 constexpr int FR_MAX = 256, FR_NW = 8;
-
-// 1-D grid of nblk workgroups per unit: the nblk workgroups of one unit get ids of one residue mod 8,
-// i.e. land on one XCD (blocks are dealt round-robin over the 8 XCDs) and share its L2 for the
-// unit's resident operand, which every one of them stages
-__device__ __forceinline__ void fa_unit_block(int nblk, int units, int64_t& zh, int& blk) {
-  const int id = blockIdx.x;
-  if (units % 8 == 0) {
-    const int xcd = id & 7, local = id >> 3;
-    zh = (int64_t)(local / nblk) * 8 + xcd;
-    blk = local % nblk;
-  } else {
-    zh = id / nblk;
-    blk = id % nblk;
-  }
-}
 
 template <int HD>
 __global__ void __launch_bounds__(FR_NW * 64) flash_fwd_res_kernel(pz_flash_args a) {
@@ -1554,6 +1938,19 @@ constexpr int FU_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
     case 32: hipLaunchKernelGGL(KERNEL<32>, GRID, __VA_ARGS__); break;                              \
     default: hipLaunchKernelGGL(KERNEL<16>, GRID, __VA_ARGS__); break;                              \
   }
+// FA_DISPATCH over a kernel with a second template argument: FA_T2(k, X)<HD> = k<HD, X>
+#define FA_T2(K, X) FaT2<X>::template K##_t
+template <auto X>
+struct FaT2 {
+  template <int HD> static constexpr auto flash_bwd_q2_kernel_t = flash_bwd_q2_kernel<HD, (bool)X>;
+  template <int HD> static constexpr auto flash_bwd_kv_kernel_t = flash_bwd_kv_kernel<HD, (int)X>;
+};
+// joint backward element-wise path: 0 generic, 1 fast, 2 fast + soft-cap ("0" in PZ_FLASH_FAST: generic)
+static int fa_fast_bwd(const pz_flash_args* a) {
+  const char* e = getenv("PZ_FLASH_FAST");
+  if (e && e[0] == '0') return 0;
+  return a->cap > 0.f ? 2 : 1;
+}
 static bool fa_hd_ok(int64_t hd) { return hd == 256 || hd == 72 || hd == 32 || hd == 16; }
 
 // SigLIP shape: the whole key / query side of a unit fits the resident kernels' LDS images
@@ -1647,6 +2044,28 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
 }
 
 
+extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, int64_t ldp, void* stream) {
+  PZ_CHECK_ARG(a && a->q && a->k && a->v && P && a->Z > 0 && a->H > 0 && a->nq > 0 && a->nk > 0,
+               "flash_fwd_probs: bad args");
+  PZ_CHECK_ARG(a->head_dim == 256, "flash_fwd_probs: head_dim %lld (256 only)", (long long)a->head_dim);
+  PZ_CHECK_ARG(a->nk <= JP_MAXKB * FA_KB && ldp >= a->nk && ldp % 4 == 0, "flash_fwd_probs: nk %lld / ldp %lld",
+               (long long)a->nk, (long long)ldp);
+  PZ_CHECK_ARG(a->mask_mode == 0 || (a->mask_mode == 1 && a->cnt && a->rows_per_token > 0),
+               "flash_fwd_probs: mask mode %d", a->mask_mode);
+  PZ_CHECK_ARG(a->n_groups >= 1 && a->n_groups <= 3 && a->g_row0[0] == 0, "flash_fwd_probs: output groups");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_ld[i] % 4 == 0, "flash_fwd_probs: group %d", i);
+  PZ_CHECK_ARG(PZ_ALIGNED(a->q, 16) && PZ_ALIGNED(a->k, 16) && PZ_ALIGNED(a->v, 16) && PZ_ALIGNED(P, 8) &&
+                   (!tcap || PZ_ALIGNED(tcap, 8)) && a->ldq % 8 == 0 && a->ldk % 8 == 0 && a->ldv % 8 == 0 &&
+                   a->q_bstride % 8 == 0 && a->k_bstride % 8 == 0 && a->v_bstride % 8 == 0,
+               "flash_fwd_probs: operands need 16-byte aligned rows");
+  PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z * a->H < 65536, "flash_fwd_probs: nq / units too large");
+  const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
+  hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
+                     (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
 extern "C" int pz_flash_bwd_prep(const pz_flash_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->delta && a->n_groups >= 1 && a->n_groups <= 3, "flash_bwd_prep: bad args");
   for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_do[i], "flash_bwd_prep: group %d", i);
@@ -1673,7 +2092,6 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     splits = splits < 8 ? splits : 8;
     while (splits > 1 && splits * 2 * a->Z * a->H * a->nk * a->head_dim * 4 > a->ws_bytes) --splits;
   }
-  dim3 gkv((unsigned)nkb, (unsigned)(a->Z * a->H), (unsigned)splits);
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
   if (fa_resident(a) && fa_unit()) {
@@ -1707,9 +2125,27 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     PZ_CHECK_LAUNCH();
     return PZ_OK;
   }
-  FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
+  const int fm = fa_fast_bwd(a);
+  if (fm) {
+    const int64_t units = a->Z * a->H, nqb = (a->nq + JQ_NW * 32 - 1) / (JQ_NW * 32);
+    const dim3 gq2((unsigned)(nqb * units));
+    if (fm == 2) {
+      FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_q2_kernel, true), gq2, dim3(JQ_NW * 64), 0, st, *a);
+    } else {
+      FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_q2_kernel, false), gq2, dim3(JQ_NW * 64), 0, st, *a);
+    }
+  } else {
+    FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
+  }
   PZ_CHECK_LAUNCH();
-  FA_DISPATCH(a->head_dim, flash_bwd_kv_kernel, gkv, dim3(FA_NW * 64), 0, st, *a);
+  const dim3 gkv1((unsigned)(nkb * a->Z * a->H * splits));
+  if (fm == 2) {
+    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 2), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
+  } else if (fm == 1) {
+    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 1), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
+  } else {
+    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 0), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
+  }
   if (splits > 1) {
     PZ_CHECK_LAUNCH();
     const int64_t n4 = 2 * a->Z * a->H * a->nk * (a->head_dim / 4);

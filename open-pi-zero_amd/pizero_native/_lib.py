@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 12  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 13  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -131,6 +131,7 @@ SIGNATURES = {
     "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],
     "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
     "pz_flash_fwd": [C.POINTER(FlashArgs), vp],
+    "pz_flash_fwd_probs": [C.POINTER(FlashArgs), vp, vp, i64, vp],
     "pz_flash_bwd_prep": [C.POINTER(FlashArgs), vp],
     "pz_flash_bwd": [C.POINTER(FlashArgs), vp],
     "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],

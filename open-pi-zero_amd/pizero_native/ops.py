@@ -418,6 +418,12 @@ def flash_fwd(a):
     call("pz_flash_fwd", C.byref(a), _st())
 
 
+def flash_fwd_probs(a, P, tcap, ldp):
+    """Joint fused forward that also stores the bf16 softmax P and tanh(cap) [Z, nq, ldp] (the
+    GEMM-path backward's inputs); pz_flash_fwd_probs."""
+    call("pz_flash_fwd_probs", C.byref(a), _p(P), _p(tcap), int(ldp), _st())
+
+
 def flash_bwd(a):
     """dQ (+ delta = rowsum(dO * O)), then dK/dV (overwritten); a.delta is fp32 scratch [Z*H, nq]."""
     call("pz_flash_bwd", C.byref(a), _st())

@@ -56,11 +56,12 @@ def _rel(a, b):
     return float(np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-30))
 
 
-@pytest.mark.parametrize("joint_attn", ["gemm", "flash"])
+@pytest.mark.parametrize("joint_attn", ["gemm", "flash", "probs"])
 def test_c5_joint_model_forward_backward(c5, joint_attn):
     g, m, inp, pos, cnt = c5
     eng = m._engine()
-    eng.joint_flash = joint_attn == "flash"
+    prev = eng.joint_flash, eng.joint_probs
+    eng.joint_flash, eng.joint_probs = joint_attn == "flash", joint_attn == "probs"
     try:
         m.zero_grad(set_to_none=True)
         emb = {n: inp[f"c5/embeds.{n}"].to(torch.bfloat16) for n in ("vlm", "proprio", "action")}
@@ -70,7 +71,7 @@ def test_c5_joint_model_forward_backward(c5, joint_attn):
         m._attach_grads()
         torch.cuda.synchronize()
     finally:
-        eng.joint_flash = False
+        eng.joint_flash, eng.joint_probs = prev
     ref, refb = g["fp32/action_hidden"], g["bf16/action_hidden"]
     mine = out.float().cpu().numpy()
     tol = max(3 * _rel(refb, ref), 3e-2)

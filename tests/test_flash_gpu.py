@@ -108,6 +108,54 @@ def test_flash_fwd_joint_block_mask(cnt, key_split):
     close(lse.view(B, L, nh), rlse.permute(0, 2, 1), rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("cnt", [[276, 276, 276], [276, 250, 9]])
+def test_flash_fwd_probs_joint_block_mask(cnt):
+    """pz_flash_fwd_probs (training-default joint forward): O, and the exported bf16 softmax P and
+    tanh(cap) with pz_attn_softmax's conventions (dead rows uniform over L keys with tcap 0, zeros in
+    the L..Lp pad columns), against torch fp32"""
+    from pizero_native import ops
+
+    B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
+    L = P + C + Hc
+    Lp = (L + 7) // 8 * 8
+    Q = (torch.randn(B, L * nh, hd, device=dev) * 2).to(torch.bfloat16)
+    K = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    V = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    K[:, :L] = (torch.randn(B, L, hd, device=dev) * 2).to(torch.bfloat16)
+    V[:, :L] = torch.randn(B, L, hd, device=dev).to(torch.bfloat16)
+    Ov = torch.empty(B * P, nh * hd, device=dev, dtype=torch.bfloat16)
+    Oe = torch.empty(B * (C + Hc), nh * hd, device=dev, dtype=torch.bfloat16)
+    Pm = torch.full((B, L * nh, Lp), float("nan"), device=dev, dtype=torch.bfloat16)
+    tc = torch.full_like(Pm, float("nan"))
+    cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                       [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + Hc) * nh * hd, hd)], 0, None, 1 / math.sqrt(hd),
+                       cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh)
+    ops.flash_fwd_probs(a, Pm, tc, Lp)
+    allowed, dead = joint_mask(cnt, P, C, L)
+    allowed, dead = allowed.to(dev), dead.to(dev)
+    q = Q.float().view(B, L, nh, hd).permute(0, 2, 1, 3)
+    k = K.float()[:, None, :L]
+    v = V.float()[:, None, :L]
+    ref, _ = ref_attention(q, k, v, 1 / math.sqrt(hd), 50.0, allowed, dead)
+    ref = ref.permute(0, 2, 1, 3)
+    close(Ov.view(B, P, nh, hd), ref[:, :P])
+    close(Oe.view(B, C + Hc, nh, hd), ref[:, P:])
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(hd)  # [B, nh, L, L]
+    th = torch.tanh(s / 50.0)
+    x = (50.0 * th).masked_fill(~allowed[:, None], float("-inf"))
+    pr = torch.softmax(x, -1)
+    pr = torch.where(dead[:, None, :, None], torch.full_like(pr, 1.0 / L), pr)
+    th = torch.where(dead[:, None, :, None], torch.zeros_like(th), th)
+    got_p = Pm.float().view(B, L, nh, Lp).permute(0, 2, 1, 3)
+    got_t = tc.float().view(B, L, nh, Lp).permute(0, 2, 1, 3)
+    close(got_p[..., :L], pr, rtol=1e-2, atol=1e-3)
+    close(got_t[..., :L], th, rtol=1e-2, atol=2e-3)
+    assert (got_p[..., L:] == 0).all() and (got_t[..., L:] == 0).all()
+    # rows sum to 1 within bf16 rounding
+    assert (got_p.sum(-1) - 1).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("B,cnt", [(1, [276]), (2, [276, 100])])
 def test_flash_fwd_denoise_key_split(B, cnt):
     """Inference denoise shape: only the action rows query (mask_row0 = first action row), keys =

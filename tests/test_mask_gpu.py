@@ -55,17 +55,19 @@ def test_general_mask_is_routed_to_general_path(setup):
     assert isinstance(m._mask_spec([gi["causal_mask"]], [torch.arange(L, device="cuda")]), GeneralMask)
 
 
-@pytest.mark.parametrize("joint_attn", ["flash", "gemm"])
+@pytest.mark.parametrize("joint_attn", ["flash", "gemm", "probs"])
 def test_general_mask_loss_and_grads(setup, joint_attn):
     from tests.golden.gradprobe import compare, probe
 
     d, ref, m, gi = setup
     eng = m._engine()
-    eng.joint_flash = joint_attn == "flash"  # a general mask must take the GEMM path either way
+    prev = eng.joint_flash, eng.joint_probs
+    # a general mask must take the GEMM path whatever the joint-attention mode
+    eng.joint_flash, eng.joint_probs = joint_attn == "flash", joint_attn == "probs"
     try:
         loss = run_loss(m, gi).item()
     finally:
-        eng.joint_flash = False
+        eng.joint_flash, eng.joint_probs = prev
     assert abs(loss - ref["loss"]) <= 1e-2 * abs(ref["loss"]), (loss, ref["loss"])
     params = dict(m.named_parameters())
     bad = []

@@ -205,14 +205,29 @@ def test_loss_and_grads_fused_joint_attention(which, request):
     """the fused (flash) joint attention path against the same fixtures"""
     d, g, m, gi = request.getfixturevalue(which)
     eng = m._engine()
-    prev = eng.joint_flash
-    eng.joint_flash = True
+    prev = eng.joint_flash, eng.joint_probs
+    eng.joint_flash, eng.joint_probs = True, False
     try:
         loss = run_loss(m, gi)
         _check_loss(g, loss.item())
         _check_grads(g, m, f"{which} flash")
     finally:
-        eng.joint_flash = prev
+        eng.joint_flash, eng.joint_probs = prev
+
+
+@pytest.mark.parametrize("which", ["tiny", "full"])
+def test_loss_and_grads_probs_joint_attention(which, request):
+    """the fused forward exporting P / tanh(cap) (pz_flash_fwd_probs) + GEMM-path backward"""
+    d, g, m, gi = request.getfixturevalue(which)
+    eng = m._engine()
+    prev = eng.joint_flash, eng.joint_probs
+    eng.joint_flash, eng.joint_probs = False, True
+    try:
+        loss = run_loss(m, gi)
+        _check_loss(g, loss.item())
+        _check_grads(g, m, f"{which} probs")
+    finally:
+        eng.joint_flash, eng.joint_probs = prev
 
 
 @pytest.mark.parametrize("which", ["tiny", "full"])
@@ -220,14 +235,14 @@ def test_loss_and_grads_gemm_joint_attention(which, request):
     """the GEMM + softmax joint attention path against the same fixtures"""
     d, g, m, gi = request.getfixturevalue(which)
     eng = m._engine()
-    prev = eng.joint_flash
-    eng.joint_flash = False
+    prev = eng.joint_flash, eng.joint_probs
+    eng.joint_flash, eng.joint_probs = False, False
     try:
         loss = run_loss(m, gi)
         _check_loss(g, loss.item())
         _check_grads(g, m, f"{which} gemm")
     finally:
-        eng.joint_flash = prev
+        eng.joint_flash, eng.joint_probs = prev
 
 
 def test_interleaved_forwards_keep_their_saved_state(tiny):

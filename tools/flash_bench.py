@@ -54,8 +54,16 @@ def main():
                         delta=delta, dq=dQ, dk=dK, dv=dV)
     fl = 4.0 * B * L * nh * L * hd
     tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
-    tb = timeit(lambda: ops.flash_bwd(fa), a.iters)
-    print(f"joint  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
+    Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
+    tcm = torch.empty_like(Pm)
+    tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
+    print(f"joint  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)", flush=True)
+    for fast in ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
+        os.environ["PZ_FLASH_FAST"] = fast
+        tb = timeit(lambda: ops.flash_bwd(fa), a.iters)
+        print(f"joint(fast={fast})  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
+              f"{2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
+    os.environ.pop("PZ_FLASH_FAST")
     nh, hd, N = 16, 72, 256
     qkv = torch.randn(B * N, 3 * nh * hd, device=dev).to(torch.bfloat16)
     O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)

@@ -1166,6 +1166,104 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_fwd_probs_kernel(pz_flash_ar
   }
 }
 
+// ---- joint backward: dS from the exported softmax (training default) --------------------------
+// dP^T = V dO^T for every key of a 16-row block in registers (V staged through LDS, dO rows straight
+// into MFMA B fragments), delta = sum_j P dP over the whole row, dS = P (dP - delta) scale (1 - tc^2)
+// written in bf16 -- pz_attn_softmax_bwd's result without the fp32 dP tensor (one launch instead of
+// the dP GEMM + the softmax-backward pass).  Mixtures without dO (g_do NULL) contribute dP = 0.
+template <int HD>
+__global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args a, const bf16_t* P,
+                                                                   const bf16_t* TC, bf16_t* dS, int64_t ldp) {
+  using D = FaDims<HD>;
+  constexpr int NT = JP_NW * 64, RPW = JP_NW * 16;
+  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][FA_KB * D::ROW];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)qblk * RPW + wave * 16 + (lane & 15);
+  const bool live = r < a.nq;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
+#pragma unroll
+  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
+  TileStager<HD, D::ROW, FA_KB, NT> st;
+  st.load(V, a.ldv, 0, a.nk);
+  bf16x8 df[D::NKS];
+  {
+    const FaRow fr{&a};
+    const int gi = live ? fr.grp(r) : 0;
+    const bf16_t* dOr = live && a.g_do[gi] ? (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi) : nullptr;
+#pragma unroll
+    for (int ks = 0; ks < D::NKS; ++ks) {
+      const int c = ks * 32 + 8 * g;
+      df[ks] = (dOr && c < HD) ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
+    }
+  }
+  __syncthreads();
+  st.store(Vs2[0]);
+  __syncthreads();
+  f32x4 dp[JP_MAXKB][4];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dp[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (kb < nkb) {
+      const bf16_t* Vs = Vs2[kb & 1];
+      const bool more = kb + 1 < nkb;
+      if (more) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+#pragma unroll
+      for (int ks = 0; ks < D::NKS; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dp[kb][i] = mfma(frag_row<D::ROW>(Vs, i * 16, ks * 32, lane), df[ks], dp[kb][i]);
+      if (more) st.store(Vs2[(kb + 1) & 1]);
+      __syncthreads();
+    }
+  }
+  if (!live) return;
+  const bf16_t* prow = P + (b * a.nq + r) * ldp;
+  const bf16_t* trow = TC + (b * a.nq + r) * ldp;
+  bf16_t* orow = dS + (b * a.nq + r) * ldp;
+  const int N = (int)a.nk;
+  u32x2 pw[JP_MAXKB][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      pw[kb][i] = j0 < N ? *reinterpret_cast<const u32x2*>(prow + j0) : u32x2{0u, 0u};  // P = 0 past N
+      const float p0 = __uint_as_float(pw[kb][i][0] << 16), p1 = __uint_as_float(pw[kb][i][0] & 0xffff0000u);
+      const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
+      dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
+    }
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  const bool cap = a.cap > 0.f;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      if (j0 >= ldp) continue;
+      u32x2 tw = {0u, 0u};
+      if (cap && j0 < N) tw = *reinterpret_cast<const u32x2*>(trow + j0);
+      const float pv[4] = {__uint_as_float(pw[kb][i][0] << 16), __uint_as_float(pw[kb][i][0] & 0xffff0000u),
+                           __uint_as_float(pw[kb][i][1] << 16), __uint_as_float(pw[kb][i][1] & 0xffff0000u)};
+      const float tv[4] = {__uint_as_float(tw[0] << 16), __uint_as_float(tw[0] & 0xffff0000u),
+                           __uint_as_float(tw[1] << 16), __uint_as_float(tw[1] & 0xffff0000u)};
+      float gv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = j0 + e < N ? pv[e] * (dp[kb][i][e] - dot) * a.scale : 0.f;
+        if (cap) x *= 1.f - tv[e] * tv[e];
+        gv[e] = x;
+      }
+      *reinterpret_cast<u32x2*>(orow + j0) = u32x2{pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
+    }
+}
+
 // ---- resident variants (SigLIP: nq, nk <= 256) ---------------------------------
 // The whole key side (forward, dQ) or query side (dK/dV) of a unit is staged in LDS once, by
 // loads all in flight together: one global-latency round per workgroup instead of one per
@@ -1960,10 +2058,14 @@ static bool fa_resident(const pz_flash_args* a) {
   return a->head_dim == 72 && a->nq <= FR_MAX && a->nk <= FR_MAX;
 }
 
-// one workgroup per unit for the resident shape ("0": the 2- / 4-workgroup resident kernels, A/B runs)
-static bool fa_unit() {
+// one workgroup per unit for the resident shape when there are enough units to fill the chip (the
+// training micro-batch: 1024); few units (B = 1 inference: 16) keep the 2- / 4-workgroup resident
+// kernels' parallelism.  PZ_FLASH_UNIT "0" / "1" forces either (tests, A/B runs)
+static bool fa_unit(const pz_flash_args* a) {
   const char* e = getenv("PZ_FLASH_UNIT");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return a->Z * a->H >= 128;
 }
 
 // no mask, no soft-cap (SigLIP): the unit kernels' log2-domain element-wise fast path
@@ -2010,7 +2112,7 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   }
   dim3 grid((unsigned)qblk, (unsigned)(a->Z * a->H), (unsigned)sp);
   hipStream_t st = (hipStream_t)stream;
-  if (sp == 1 && fa_resident(a) && fa_unit()) {
+  if (sp == 1 && fa_resident(a) && fa_unit(a)) {
     static bool attr = false;
     static bool attr2 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
@@ -2066,6 +2168,26 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
   return PZ_OK;
 }
 
+extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void* tcap, void* dS, int64_t ldp,
+                               void* stream) {
+  PZ_CHECK_ARG(a && a->v && P && dS && a->Z > 0 && a->H > 0 && a->nq > 0 && a->nk > 0, "flash_bwd_ds: bad args");
+  PZ_CHECK_ARG(a->head_dim == 256, "flash_bwd_ds: head_dim %lld (256 only)", (long long)a->head_dim);
+  PZ_CHECK_ARG(a->nk <= JP_MAXKB * FA_KB && ldp >= a->nk && ldp % 4 == 0, "flash_bwd_ds: nk %lld / ldp %lld",
+               (long long)a->nk, (long long)ldp);
+  PZ_CHECK_ARG(a->cap <= 0.f || tcap, "flash_bwd_ds: soft-cap needs tcap");
+  PZ_CHECK_ARG(a->n_groups >= 1 && a->n_groups <= 3 && a->g_row0[0] == 0, "flash_bwd_ds: output groups");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(!a->g_do[i] || a->g_ld[i] % 8 == 0, "flash_bwd_ds: dO group %d", i);
+  PZ_CHECK_ARG(PZ_ALIGNED(a->v, 16) && a->ldv % 8 == 0 && a->v_bstride % 8 == 0 && PZ_ALIGNED(P, 8) &&
+                   PZ_ALIGNED(dS, 8) && (!tcap || PZ_ALIGNED(tcap, 8)),
+               "flash_bwd_ds: alignment");
+  PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_bwd_ds: too many units");
+  const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
+  hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0, (hipStream_t)stream,
+                     *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
 extern "C" int pz_flash_bwd_prep(const pz_flash_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->delta && a->n_groups >= 1 && a->n_groups <= 3, "flash_bwd_prep: bad args");
   for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_do[i], "flash_bwd_prep: group %d", i);
@@ -2094,7 +2216,7 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
   }
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
-  if (fa_resident(a) && fa_unit()) {
+  if (fa_resident(a) && fa_unit(a)) {
     static bool aq = false, akv = false, aq2 = false, akv2 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_plain(a)) {

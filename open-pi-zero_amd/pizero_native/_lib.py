@@ -132,6 +132,7 @@ SIGNATURES = {
     "pz_attn_softmax_bwd": [vp, vp, i64, vp, vp, i64, i64, i64, f32, f32, vp],
     "pz_flash_fwd": [C.POINTER(FlashArgs), vp],
     "pz_flash_fwd_probs": [C.POINTER(FlashArgs), vp, vp, i64, vp],
+    "pz_flash_bwd_ds": [C.POINTER(FlashArgs), vp, vp, vp, i64, vp],
     "pz_flash_bwd_prep": [C.POINTER(FlashArgs), vp],
     "pz_flash_bwd": [C.POINTER(FlashArgs), vp],
     "pz_patchify": [vp, vp, i64, i64, i64, i64, i64, vp],

@@ -181,6 +181,9 @@ class Engine:
         ja = os.environ.get("PZ_JOINT_ATTN", "probs")
         self.joint_flash = ja == "flash"
         self.joint_probs = ja == "probs"
+        # GEMM-path backward's dS: "1" (default) = pz_flash_bwd_ds from the exported P (no fp32 dP), "0" = the
+        # dP GEMM + pz_attn_softmax_bwd (A/B)
+        self.joint_ds = os.environ.get("PZ_JOINT_DS", "1") == "1"
         # inference (prefill / denoise) attention: fused kernel unless PZ_INFER_ATTN=gemm
         self.infer_flash = os.environ.get("PZ_INFER_ATTN", "flash") == "flash"
         # activation backward of the training MLPs (PZ_SPLIT_DACT, A/B): "1" (default) = plain dgrad GEMM + a
@@ -531,7 +534,7 @@ class Engine:
             B, 1, Lq * nh, d.L, hd, Q, (hd, Lq * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
             [(g.off * nh, Os[g.name], g.T * nh * hd, hd) for g in gs], 0, lse, 1.0 / math.sqrt(hd), cap=50.0,
             mask_mode=1, cnt=cnt, prefix=d.P, cond=d.C, rows_per_token=nh,
-            dgroups=None if dO is None else [dO[g.name] for g in gs], delta=delta, dq=dq, dk=dk, dv=dv)
+            dgroups=None if dO is None else [dO.get(g.name) for g in gs], delta=delta, dq=dq, dk=dk, dv=dv)
 
     def _joint_kv(self, B, Lp, dev, save):
         """Joint K/V buffers [nL, B, Lp, hd] for one training forward.  The engine owns one zeroed set
@@ -701,18 +704,27 @@ class Engine:
                 ops.flash_bwd(self._joint_flash(groups, st["Q"], st["K"], st["V"], st["O"], st["lse"], cnt, B, L,
                                                 dO=dO, delta=delta, dq=dQ, dk=dK, dv=dV))
             else:
-                if dP is None:
-                    dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
-                    dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
                 Pm, tc, Qj, Kj, Vj = st["P"], st["tc"], st["Q"], st["K"], st["V"]
-                if any_skip:
-                    dP.zero_()
-                for g in groups:
-                    if g.name not in dO:
-                        continue
-                    ops.gemm(g.T * nh, L, hd, dO[g.name], hd, True, Vj, hd, True, dP[:, g.off * nh:], Lp, batch=B,
-                             sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
-                ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
+                if self.joint_ds and not isinstance(cnt, GeneralMask) and L <= 320 and hd == 256:
+                    # dS in one kernel: dP = dO V^T in registers, delta and the soft-cap/softmax backward
+                    # from the exported P / tanh(cap) (no fp32 dP tensor); a mixture without dO adds 0
+                    if dS is None:
+                        dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+                    ops.flash_bwd_ds(self._joint_flash(groups, Qj, Kj, Vj, st["O"], None, cnt, B, L, dO=dO), Pm, tc,
+                                     dS, Lp)
+                else:
+                    if dP is None:
+                        dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
+                    if dS is None:
+                        dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
+                    if any_skip:
+                        dP.zero_()
+                    for g in groups:
+                        if g.name not in dO:
+                            continue
+                        ops.gemm(g.T * nh, L, hd, dO[g.name], hd, True, Vj, hd, True, dP[:, g.off * nh:], Lp,
+                                 batch=B, sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
+                    ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
                 # dQ = dS K ; dK = dS^T Q ; dV = sum_g P_g^T dO_g
                 ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
                          sB=(Lp * hd, 0), sC=(L * nh * hd, 0))

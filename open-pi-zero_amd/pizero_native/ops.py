@@ -418,6 +418,12 @@ def flash_fwd(a):
     call("pz_flash_fwd", C.byref(a), _st())
 
 
+def flash_bwd_ds(a, P, tcap, dS, ldp):
+    """dS of the joint attention from the exported softmax P / tanh(cap) and dO (a.g_do groups);
+    pz_flash_bwd_ds."""
+    call("pz_flash_bwd_ds", C.byref(a), _p(P), _p(tcap), _p(dS), int(ldp), _st())
+
+
 def flash_fwd_probs(a, P, tcap, ldp):
     """Joint fused forward that also stores the bf16 softmax P and tanh(cap) [Z, nq, ldp] (the
     GEMM-path backward's inputs); pz_flash_fwd_probs."""

@@ -62,8 +62,12 @@ def ref_attention(q, k, v, scale, cap=0.0, allowed=None, dead=None):
     return p @ v, lse
 
 
-def test_flash_fwd_siglip():
+@pytest.mark.parametrize("unit", ["0", "1"])
+def test_flash_fwd_siglip(unit, monkeypatch):
+    """both SigLIP forward kernel families: 2 workgroups per unit (few units) and one (training)"""
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_FLASH_UNIT", unit)
 
     B, nh, hd, N = 3, 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
@@ -156,6 +160,51 @@ def test_flash_fwd_probs_joint_block_mask(cnt):
     assert (got_p.sum(-1) - 1).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("skip_action", [False, True])
+def test_flash_bwd_ds_matches_softmax_backward(skip_action):
+    """pz_flash_bwd_ds (dP = dO V^T in registers + the soft-cap softmax backward from the exported P /
+    tanh(cap)) against torch fp32 of pz_attn_softmax_bwd's formula on the same P / tcap; a mixture
+    without dO (the last layer's skipped prefix) contributes dP = 0"""
+    from pizero_native import ops
+
+    cnt = [276, 250]
+    B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
+    L = P + C + Hc
+    Lp = (L + 7) // 8 * 8
+    Q = (torch.randn(B, L * nh, hd, device=dev) * 2).to(torch.bfloat16)
+    K = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    V = torch.zeros(B, Lp, hd, device=dev, dtype=torch.bfloat16)
+    K[:, :L] = (torch.randn(B, L, hd, device=dev) * 2).to(torch.bfloat16)
+    V[:, :L] = torch.randn(B, L, hd, device=dev).to(torch.bfloat16)
+    Ov = torch.empty(B * P, nh * hd, device=dev, dtype=torch.bfloat16)
+    Oe = torch.empty(B * (C + Hc), nh * hd, device=dev, dtype=torch.bfloat16)
+    dOv = torch.randn(B * P, nh * hd, device=dev).to(torch.bfloat16)
+    dOe = torch.randn(B * (C + Hc), nh * hd, device=dev).to(torch.bfloat16)
+    Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
+    tc = torch.empty_like(Pm)
+    dS = torch.full_like(Pm, float("nan"))
+    cnt_t = torch.tensor(cnt, device=dev, dtype=torch.int32)
+    groups = [(0, Ov, P * nh * hd, hd), (P * nh, Oe, (C + Hc) * nh * hd, hd)]
+    kw = dict(cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh)
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0), groups,
+                       0, None, 1 / math.sqrt(hd), **kw)
+    ops.flash_fwd_probs(a, Pm, tc, Lp)
+    dgroups = [dOv, None] if skip_action else [dOv, dOe]
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0), groups,
+                       0, None, 1 / math.sqrt(hd), dgroups=dgroups, **kw)
+    ops.flash_bwd_ds(a, Pm, tc, dS, Lp)
+    dO = torch.cat([dOv.float().view(B, P * nh, hd),
+                    (torch.zeros_like(dOe) if skip_action else dOe).float().view(B, (C + Hc) * nh, hd)], 1)
+    dP = dO @ V.float().transpose(1, 2)  # [B, L*nh, Lp]
+    p, t = Pm.float(), tc.float()
+    dot = (p[..., :L] * dP[..., :L]).sum(-1, keepdim=True)
+    ref = p * (dP - dot) / math.sqrt(hd) * (1 - t * t)
+    ref[..., L:] = 0
+    close(dS, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 8)
+    assert (dS[..., L:] == 0).all()
+
+
+
 @pytest.mark.parametrize("B,cnt", [(1, [276]), (2, [276, 100])])
 def test_flash_fwd_denoise_key_split(B, cnt):
     """Inference denoise shape: only the action rows query (mask_row0 = first action row), keys =
@@ -191,8 +240,11 @@ def _grads(q, k, v, dO, scale, cap=0.0, allowed=None, dead=None):
     return q.grad, k.grad, v.grad
 
 
-def test_flash_bwd_siglip():
+@pytest.mark.parametrize("unit", ["0", "1"])
+def test_flash_bwd_siglip(unit, monkeypatch):
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_FLASH_UNIT", unit)
 
     B, nh, hd, N = 2, 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)

@@ -58,6 +58,9 @@ def main():
     tcm = torch.empty_like(Pm)
     tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
     print(f"joint  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)", flush=True)
+    dSm = torch.empty_like(Pm)
+    td = timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters)
+    print(f"joint  bwd dS {td:.3f} ms (dP = dO V^T in registers + softmax backward from P / tanh(cap))", flush=True)
     for fast in ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
         os.environ["PZ_FLASH_FAST"] = fast
         tb = timeit(lambda: ops.flash_bwd(fa), a.iters)

@@ -17,6 +17,13 @@ __device__ __forceinline__ void load8(const bf16_t* p, float (&v)[8]) {
     v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
   }
 }
+__device__ __forceinline__ void unpack8(const u32x4& r, float (&v)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(r[i] << 16);
+    v[2 * i + 1] = __uint_as_float(r[i] & 0xffff0000u);
+  }
+}
 __device__ __forceinline__ void store8(bf16_t* p, const float (&v)[8]) {
   u32x4 r;
 #pragma unroll
@@ -82,6 +89,13 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
     const float r = rstd[row];
     float xv[MAXC][8], gv[MAXC][8];
     float dot = 0.f;
+    u32x4 dr[MAXC];  // residual gradient: loaded with x / dy, not after the row reduction (one memory round trip)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      dr[c] = u32x4{0u, 0u, 0u, 0u};
+      if (ch < nc && dres) dr[c] = *reinterpret_cast<const u32x4*>(dres + row * lddx + ch * 8);
+    }
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + 64 * c;
@@ -105,11 +119,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_kernel(
       const int ch = lane + 64 * c;
       if (ch < nc) {
         float o[8];
-        if (dres) load8(dres + row * lddx + ch * 8, o);
-        else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = 0.f;
-        }
+        unpack8(dr[c], o);
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += r * gv[c][i] - k * xv[c][i];
         store8(dx + row * lddx + ch * 8, o);
@@ -203,6 +213,13 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
     const float mu = mean[row], r = rstd[row];
     float xh[MAXC][8], gv[MAXC][8];
     float sg = 0.f, sgx = 0.f;
+    u32x4 dr[MAXC];  // residual gradient: loaded with x / dy, not after the row reductions
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + 64 * c;
+      dr[c] = u32x4{0u, 0u, 0u, 0u};
+      if (ch < nc && dres) dr[c] = *reinterpret_cast<const u32x4*>(dres + row * lddx + ch * 8);
+    }
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int ch = lane + 64 * c;
@@ -229,11 +246,7 @@ __global__ void __launch_bounds__(256) layernorm_bwd_kernel(
       const int ch = lane + 64 * c;
       if (ch < nc) {
         float o[8];
-        if (dres) load8(dres + row * lddx + ch * 8, o);
-        else {
-#pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = 0.f;
-        }
+        unpack8(dr[c], o);
 #pragma unroll
         for (int i = 0; i < 8; ++i) o[i] += r * (gv[c][i] - sg - xh[c][i] * sgx);
         store8(dx + row * lddx + ch * 8, o);
@@ -371,6 +384,111 @@ __global__ void batch_sum_kernel(const bf16_t* __restrict__ X, int64_t B, int64_
 
 extern "C" int64_t pz_norm_rows_per_part(void) { return ROWS_PER_PART; }
 
+// Backward, one ROW per workgroup step (default): thread t owns the 8 columns 8t .. 8t + 7 of every
+// row (D <= 2048), so the dw / db accumulators are 8 + 8 registers per thread, the partial row is
+// written without an LDS reduction, and occupancy is high; the next row's x / dy / residual-gradient
+// loads are issued before the current row's reductions (two rows in flight per workgroup); the two
+// row sums go through a double-buffered LDS slot (one barrier per row).  The wave-per-row kernels
+// above hold MAXC x 8 accumulators per thread (2 waves / SIMD at D >= 1152): PZ_NORM_BWD=wave (A/B).
+template <bool LN>
+__global__ void __launch_bounds__(256) norm_bwd_row_kernel(
+    const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
+    const bf16_t* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const bf16_t* dres, bf16_t* dx, int64_t lddx, float* dw_part, float* db_part, int64_t R, int D) {
+  __shared__ float red[2][2][4];  // [row parity][sum][wave]
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const bool act = t < D / 8;
+  float wv[8];
+  if (act) load8(w + t * 8, wv);
+  else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wv[i] = 0.f;
+  }
+  float dwa[8], dba[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dwa[i] = dba[i] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
+  const int nrows = (int)(R - r0 < ROWS_PER_PART ? R - r0 : ROWS_PER_PART);
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  u32x4 xr = z4, dyr = z4, drr = z4;
+  if (act) {
+    xr = *reinterpret_cast<const u32x4*>(x + r0 * ldx + t * 8);
+    dyr = *reinterpret_cast<const u32x4*>(dy + r0 * lddy + t * 8);
+    if (dres) drr = *reinterpret_cast<const u32x4*>(dres + r0 * lddx + t * 8);
+  }
+  for (int i = 0; i < nrows; ++i) {
+    const int64_t row = r0 + i;
+    u32x4 xn = z4, dyn = z4, drn = z4;
+    if (act && i + 1 < nrows) {  // next row in flight during this row's reductions
+      xn = *reinterpret_cast<const u32x4*>(x + (row + 1) * ldx + t * 8);
+      dyn = *reinterpret_cast<const u32x4*>(dy + (row + 1) * lddy + t * 8);
+      if (dres) drn = *reinterpret_cast<const u32x4*>(dres + (row + 1) * lddx + t * 8);
+    }
+    const float r = rstd[row], mu = LN ? mean[row] : 0.f;
+    float xv[8], dv[8], g[8];
+    unpack8(xr, xv);
+    unpack8(dyr, dv);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      if (LN) {
+        xv[e] = (xv[e] - mu) * r;  // x-hat
+        g[e] = dv[e] * wv[e];
+        s1 += g[e];
+        s2 += g[e] * xv[e];
+        dwa[e] += dv[e] * xv[e];
+        dba[e] += dv[e];
+      } else {
+        g[e] = dv[e] * (1.f + wv[e]);  // Gemma RMSNorm scales by (1 + w)
+        s1 += g[e] * xv[e];
+        dwa[e] += dv[e] * xv[e] * r;
+      }
+    }
+    s1 = warp_sum(s1);
+    if (LN) s2 = warp_sum(s2);
+    if (lane == 0) {
+      red[i & 1][0][wave] = s1;
+      red[i & 1][1][wave] = s2;
+    }
+    __syncthreads();
+    s1 = red[i & 1][0][0] + red[i & 1][0][1] + red[i & 1][0][2] + red[i & 1][0][3];
+    s2 = red[i & 1][1][0] + red[i & 1][1][1] + red[i & 1][1][2] + red[i & 1][1][3];
+    if (act) {
+      float o[8];
+      unpack8(drr, o);
+      if (LN) {
+        const float a = s1 / (float)D, c = s2 / (float)D;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += r * (g[e] - a - xv[e] * c);
+      } else {
+        const float k = r * r * r * s1 / (float)D;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] += r * g[e] - k * xv[e];
+      }
+      store8(dx + row * lddx + t * 8, o);
+    }
+    xr = xn;
+    dyr = dyn;
+    drr = drn;
+  }
+  if (!act) return;
+  if (dw_part) {
+    float* d = dw_part + (int64_t)blockIdx.x * D + t * 8;
+    *reinterpret_cast<f32x4*>(d) = f32x4{dwa[0], dwa[1], dwa[2], dwa[3]};
+    *reinterpret_cast<f32x4*>(d + 4) = f32x4{dwa[4], dwa[5], dwa[6], dwa[7]};
+  }
+  if (LN && db_part) {
+    float* d = db_part + (int64_t)blockIdx.x * D + t * 8;
+    *reinterpret_cast<f32x4*>(d) = f32x4{dba[0], dba[1], dba[2], dba[3]};
+    *reinterpret_cast<f32x4*>(d + 4) = f32x4{dba[4], dba[5], dba[6], dba[7]};
+  }
+}
+
+static bool norm_bwd_rows() {
+  const char* e = getenv("PZ_NORM_BWD");
+  return !(e && e[0] == 'w');
+}
+
 #define NORM_DISPATCH(KERNEL, GRID, ...)                                                   \
   do {                                                                                    \
     const int nc = (int)(D / 8);                                                          \
@@ -409,8 +527,13 @@ extern "C" int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64
   if (R == 0) return PZ_OK;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
-  NORM_DISPATCH(rmsnorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
-                rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, R, (int)D);
+  if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16))
+    hipLaunchKernelGGL(norm_bwd_row_kernel<false>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
+                       ldx, (const bf16_t*)w, nullptr, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, nullptr,
+                       R, (int)D);
+  else
+    NORM_DISPATCH(rmsnorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
+                  rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, R, (int)D);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
@@ -437,8 +560,14 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   if (R == 0) return PZ_OK;
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
-  NORM_DISPATCH(layernorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
-                mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D);
+  if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16) &&
+      PZ_ALIGNED(db_part, 16))
+    hipLaunchKernelGGL(norm_bwd_row_kernel<true>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
+                       ldx, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R,
+                       (int)D);
+  else
+    NORM_DISPATCH(layernorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
+                  mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -404,9 +404,13 @@ def test_small_gemm():
         close(out[:, :7], 2 * (x.float() @ W.float().t() + b.float()), atol=2e-2)
 
 
+@pytest.mark.parametrize("kern", ["row", "wave"])
 @pytest.mark.parametrize("D", [1024, 2048, 64])
-def test_rmsnorm_fwd_bwd(D):
+def test_rmsnorm_fwd_bwd(D, kern, monkeypatch):
+    """both backward kernels: row-per-step (default) and wave-per-row (PZ_NORM_BWD=wave)"""
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_NORM_BWD", kern)
 
     R = 333
     x = bf(R, D)
@@ -431,8 +435,11 @@ def test_rmsnorm_fwd_bwd(D):
     close(dw, wr.grad, atol=0.1)
 
 
-def test_layernorm_fwd_bwd():
+@pytest.mark.parametrize("kern", ["row", "wave"])
+def test_layernorm_fwd_bwd(kern, monkeypatch):
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_NORM_BWD", kern)
 
     R, D = 300, 1152
     x = bf(R, D) * 3 + 1

@@ -238,7 +238,8 @@ int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, int64_t ldp,
 /* Joint attention backward from the exported softmax (head_dim 256, nk <= 320): dS[z][r][0..ldp) =
  * P (dP - sum_j P dP) scale (1 - tcap^2) in bf16 with dP = dO V^T computed in registers (dO from the
  * g_do groups; a NULL group counts as dO = 0), zeros past nk -- pz_attn_softmax_bwd's output without
- * the fp32 dP tensor.  Replaces the dP GEMM + softmax backward of joint_model.py:261-292's autograd. */
+ * the fp32 dP tensor.  Replaces the dP GEMM + softmax backward of joint_model.py:261-292's autograd.
+ * With a->dq set it also writes dQ = dS K (bf16 dS, K staged like V; the q strides address dQ). */
 int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void* tcap, void* dS, int64_t ldp, void* stream);
 /* delta[z][r] = sum_d dO[r][d] * O[r][d] (fp32) */
 int pz_flash_bwd_prep(const pz_flash_args* a, void* stream);

@@ -1176,7 +1176,7 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args 
                                                                    const bf16_t* TC, bf16_t* dS, int64_t ldp) {
   using D = FaDims<HD>;
   constexpr int NT = JP_NW * 64, RPW = JP_NW * 16;
-  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][FA_KB * D::ROW];
+  __shared__ __attribute__((aligned(16))) bf16_t Ts2[2][FA_KB * D::ROW];  // V blocks, then (dQ) K blocks
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   int64_t zh;
   int qblk;
@@ -1184,10 +1184,12 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args 
   const int64_t b = zh / a.H, h = zh % a.H;
   const int64_t r = (int64_t)qblk * RPW + wave * 16 + (lane & 15);
   const bool live = r < a.nq;
+  const bool want_dq = a.dq != nullptr;
   const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
   const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
 #pragma unroll
-  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
+  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ts2[bi]);
   TileStager<HD, D::ROW, FA_KB, NT> st;
   st.load(V, a.ldv, 0, a.nk);
   bf16x8 df[D::NKS];
@@ -1202,26 +1204,28 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args 
     }
   }
   __syncthreads();
-  st.store(Vs2[0]);
+  st.store(Ts2[0]);
   __syncthreads();
+  // pass 1 (stage kb = V block kb): dP^T[key][q] = V dO^T
   f32x4 dp[JP_MAXKB][4];
 #pragma unroll
   for (int kb = 0; kb < JP_MAXKB; ++kb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) dp[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (kb < nkb) {
-      const bf16_t* Vs = Vs2[kb & 1];
-      const bool more = kb + 1 < nkb;
-      if (more) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+      const bf16_t* Vs = Ts2[kb & 1];
+      const bool more = kb + 1 < nkb || want_dq;
+      if (kb + 1 < nkb) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
+      else if (want_dq) st.load(K, a.ldk, 0, a.nk);  // stage nkb: K block 0
 #pragma unroll
       for (int ks = 0; ks < D::NKS; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) dp[kb][i] = mfma(frag_row<D::ROW>(Vs, i * 16, ks * 32, lane), df[ks], dp[kb][i]);
-      if (more) st.store(Vs2[(kb + 1) & 1]);
+      if (more) st.store(Ts2[(kb + 1) & 1]);
       __syncthreads();
     }
   }
-  if (!live) return;
+  // dS = P (dP - delta) scale (1 - tc^2) for the row (kept in dp as fp32; stored in bf16)
   const bf16_t* prow = P + (b * a.nq + r) * ldp;
   const bf16_t* trow = TC + (b * a.nq + r) * ldp;
   bf16_t* orow = dS + (b * a.nq + r) * ldp;
@@ -1233,7 +1237,7 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      pw[kb][i] = j0 < N ? *reinterpret_cast<const u32x2*>(prow + j0) : u32x2{0u, 0u};  // P = 0 past N
+      pw[kb][i] = live && j0 < N ? *reinterpret_cast<const u32x2*>(prow + j0) : u32x2{0u, 0u};  // P = 0 past N
       const float p0 = __uint_as_float(pw[kb][i][0] << 16), p1 = __uint_as_float(pw[kb][i][0] & 0xffff0000u);
       const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
       dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
@@ -1241,27 +1245,58 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args 
   dot += __shfl_xor(dot, 16, 64);
   dot += __shfl_xor(dot, 32, 64);
   const bool cap = a.cap > 0.f;
+  bf16x8 dsf[JP_MAXKB][2];
 #pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb)
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      if (j0 >= ldp) continue;
       u32x2 tw = {0u, 0u};
-      if (cap && j0 < N) tw = *reinterpret_cast<const u32x2*>(trow + j0);
+      if (live && cap && j0 < N) tw = *reinterpret_cast<const u32x2*>(trow + j0);
       const float pv[4] = {__uint_as_float(pw[kb][i][0] << 16), __uint_as_float(pw[kb][i][0] & 0xffff0000u),
                            __uint_as_float(pw[kb][i][1] << 16), __uint_as_float(pw[kb][i][1] & 0xffff0000u)};
       const float tv[4] = {__uint_as_float(tw[0] << 16), __uint_as_float(tw[0] & 0xffff0000u),
                            __uint_as_float(tw[1] << 16), __uint_as_float(tw[1] & 0xffff0000u)};
-      float gv[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float x = j0 + e < N ? pv[e] * (dp[kb][i][e] - dot) * a.scale : 0.f;
         if (cap) x *= 1.f - tv[e] * tv[e];
-        gv[e] = x;
+        dp[kb][i][e] = x;
       }
-      *reinterpret_cast<u32x2*>(orow + j0) = u32x2{pack2bf(gv[0], gv[1]), pack2bf(gv[2], gv[3])};
+      if (live && kb < nkb && j0 < ldp)
+        *reinterpret_cast<u32x2*>(orow + j0) =
+            u32x2{pack2bf(dp[kb][i][0], dp[kb][i][1]), pack2bf(dp[kb][i][2], dp[kb][i][3])};
     }
+    dsf[kb][0] = pack8(dp[kb][0], dp[kb][1]);
+    dsf[kb][1] = pack8(dp[kb][2], dp[kb][3]);
+  }
+  if (!want_dq) return;  // uniform: every thread takes the same branch
+  // pass 2 (stage nkb + kb = K block kb): dQ^T[d][q] = K^T[d][key] dS^T[key][q] with the bf16 dS (what the
+  // GEMM path's dS K product reads)
+  f32x4 dq[D::NDB];
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    if (kb < nkb) {
+      const bf16_t* Ks = Ts2[(nkb + kb) & 1];
+      const bool more = kb + 1 < nkb;
+      if (more) st.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int db = 0; db < D::NDB; ++db) dq[db] = mfma(frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane), dsf[kb][k2], dq[db]);
+      if (more) st.store(Ts2[(nkb + kb + 1) & 1]);
+      __syncthreads();
+    }
+  }
+  if (!live) return;
+  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+  for (int db = 0; db < D::NDB; ++db) {
+    const int d = db * 16 + 4 * g;
+    if (d < HD) *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
+  }
 }
 
 // ---- resident variants (SigLIP: nq, nk <= 256) ---------------------------------
@@ -2180,6 +2215,10 @@ extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void
   PZ_CHECK_ARG(PZ_ALIGNED(a->v, 16) && a->ldv % 8 == 0 && a->v_bstride % 8 == 0 && PZ_ALIGNED(P, 8) &&
                    PZ_ALIGNED(dS, 8) && (!tcap || PZ_ALIGNED(tcap, 8)),
                "flash_bwd_ds: alignment");
+  if (a->dq)
+    PZ_CHECK_ARG(a->k && PZ_ALIGNED(a->k, 16) && a->ldk % 8 == 0 && a->k_bstride % 8 == 0 && PZ_ALIGNED(a->dq, 8) &&
+                     a->ldq % 4 == 0 && a->q_bstride % 4 == 0,
+                 "flash_bwd_ds: dQ needs K (16-byte rows) and an 8-byte aligned dQ");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_bwd_ds: too many units");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
   hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0, (hipStream_t)stream,

@@ -184,6 +184,8 @@ class Engine:
         # GEMM-path backward's dS: "1" (default) = pz_flash_bwd_ds from the exported P (no fp32 dP), "0" = the
         # dP GEMM + pz_attn_softmax_bwd (A/B)
         self.joint_ds = os.environ.get("PZ_JOINT_DS", "1") == "1"
+        # ... and dQ = dS K inside that launch ("0": the batched dQ GEMM, A/B)
+        self.joint_ds_dq = os.environ.get("PZ_JOINT_DS_DQ", "1") == "1"
         # inference (prefill / denoise) attention: fused kernel unless PZ_INFER_ATTN=gemm
         self.infer_flash = os.environ.get("PZ_INFER_ATTN", "flash") == "flash"
         # activation backward of the training MLPs (PZ_SPLIT_DACT, A/B): "1" (default) = plain dgrad GEMM + a
@@ -705,13 +707,16 @@ class Engine:
                                                 dO=dO, delta=delta, dq=dQ, dk=dK, dv=dV))
             else:
                 Pm, tc, Qj, Kj, Vj = st["P"], st["tc"], st["Q"], st["K"], st["V"]
+                dq_done = False
                 if self.joint_ds and not isinstance(cnt, GeneralMask) and L <= 320 and hd == 256:
                     # dS in one kernel: dP = dO V^T in registers, delta and the soft-cap/softmax backward
-                    # from the exported P / tanh(cap) (no fp32 dP tensor); a mixture without dO adds 0
+                    # from the exported P / tanh(cap) (no fp32 dP tensor), then dQ = dS K in the same launch;
+                    # a mixture without dO adds 0
                     if dS is None:
                         dS = torch.empty(B, L * nh, Lp, device=dev, dtype=BF16)
-                    ops.flash_bwd_ds(self._joint_flash(groups, Qj, Kj, Vj, st["O"], None, cnt, B, L, dO=dO), Pm, tc,
-                                     dS, Lp)
+                    ops.flash_bwd_ds(self._joint_flash(groups, Qj, Kj, Vj, st["O"], None, cnt, B, L, dO=dO,
+                                                       dq=dQ if self.joint_ds_dq else None), Pm, tc, dS, Lp)
+                    dq_done = self.joint_ds_dq
                 else:
                     if dP is None:
                         dP = torch.empty(B, L * nh, Lp, device=dev, dtype=F32)
@@ -726,8 +731,9 @@ class Engine:
                                  batch=B, sA=(g.T * nh * hd, 0), sB=(Lp * hd, 0), sC=(L * nh * Lp, 0))
                     ops.attn_softmax_bwd(Pm, dP, Lp, tc, dS, Lp, B * L * nh, L, 1.0 / math.sqrt(hd), 50.0)
                 # dQ = dS K ; dK = dS^T Q ; dV = sum_g P_g^T dO_g
-                ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
-                         sB=(Lp * hd, 0), sC=(L * nh * hd, 0))
+                if not dq_done:
+                    ops.gemm(L * nh, hd, Lp, dS, Lp, True, Kj, hd, False, dQ, hd, batch=B, sA=(L * nh * Lp, 0),
+                             sB=(Lp * hd, 0), sC=(L * nh * hd, 0))
                 ops.gemm(Lp, hd, L * nh, dS, Lp, False, Qj, hd, False, dK, hd, batch=B, sA=(L * nh * Lp, 0),
                          sB=(L * nh * hd, 0), sC=(Lp * hd, 0))
                 first = True

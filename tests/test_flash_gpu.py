@@ -202,6 +202,15 @@ def test_flash_bwd_ds_matches_softmax_backward(skip_action):
     ref[..., L:] = 0
     close(dS, ref, rtol=2e-2, atol=2e-2 * ref.abs().max().item() / 8)
     assert (dS[..., L:] == 0).all()
+    # with dq: the same dS plus dQ = dS K (the bf16 dS the batched dQ GEMM would read)
+    dS2 = torch.full_like(Pm, float("nan"))
+    dQ = torch.full_like(Q, float("nan"))
+    a = ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0), groups,
+                       0, None, 1 / math.sqrt(hd), dgroups=dgroups, dq=dQ, **kw)
+    ops.flash_bwd_ds(a, Pm, tc, dS2, Lp)
+    assert torch.equal(dS2, dS)
+    refq = dS.float() @ K.float()
+    close(dQ, refq, rtol=2e-2, atol=2e-2 * refq.abs().max().item() / 8)
 
 
 

@@ -43,6 +43,9 @@ struct GemmP {
   // split-K (batch-1 only): blockIdx.y = split index; raw fp32 partials -> ws[z][M][ldw]
   float* ws;
   int64_t ksplit, ldw;
+  // batched 128-tile launches (gemm_kernel, batch % 8 == 0, no split-K): 1-D grid, the tiles of one batch
+  // entry on one XCD so its operand panels are shared in that XCD's L2 (batch_xcd = number of batch entries)
+  int batch_xcd;
   // 8-phase split tail (batch-1 only, tail_s > 0): work units [0, dp_tiles) are whole tiles; unit
   // dp_tiles + u is K-piece (u % tail_s) (tail_kt K-tiles) of tile dp_tiles + u / tail_s, whose raw
   // accumulators go to ws[u] (256 KiB, thread-major) for gemm8p_tail_epilogue.
@@ -432,8 +435,18 @@ __global__ void __launch_bounds__(NT, 2) gemm_kernel(GemmP p) {
 
   const bool geglu = p.epi == PZ_EPI_GEGLU;
   int tm, tn;
-  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
-  const int64_t z = blockIdx.y;
+  int64_t z = blockIdx.y;
+  if (p.batch_xcd) {
+    // workgroups are dealt round-robin over the 8 XCDs: XCD x takes batch entries x, x + 8, ..., each
+    // entry's tiles consecutive in its local order (all resident together, sharing the entry's panels)
+    const int ntile = p.tiles_m * p.tiles_n, xcd = blockIdx.x & 7, local = blockIdx.x >> 3;
+    const int bi = local / ntile, tile = local - bi * ntile;
+    z = (int64_t)bi * 8 + xcd;
+    tm = tile % p.tiles_m;
+    tn = tile / p.tiles_m;
+  } else {
+    tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  }
   const bool split = p.ksplit > 0;
   const int64_t zo = split ? 0 : z / p.batch_inner, zi = split ? 0 : z % p.batch_inner;
   const bf16_t* A = p.A + zo * p.sAo + zi * p.sAi;
@@ -2163,6 +2176,18 @@ static int launch_tile(const GemmP& p, int64_t batch, hipStream_t st) {
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr_set = true;
+  }
+  static int xb = -1;  // PZ_GEMM_BATCH_XCD=0: 2-D grid (A/B; read once)
+  if (xb < 0) {
+    const char* e = getenv("PZ_GEMM_BATCH_XCD");
+    xb = !(e && e[0] == '0');
+  }
+  if (xb && p.ksplit == 0 && batch >= 8 && batch % 8 == 0 && (int64_t)p.tiles_m * p.tiles_n * batch < (1LL << 31)) {
+    GemmP q = p;
+    q.batch_xcd = (int)batch;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * p.tiles_n * batch)), dim3(NT), smem, st, q);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
   }
   dim3 grid(p.tiles_m * p.tiles_n, (unsigned)batch);
   hipLaunchKernelGGL(kern, grid, dim3(NT), smem, st, p);

@@ -83,6 +83,50 @@ def test_all_four_layouts_batched_fp32_out():
             close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_batched_xcd_grouped_layouts(xcd):
+    """batch % 8 == 0 launches of the 128-tile kernel take the XCD-grouped 1-D grid (a batch entry's tiles
+    on one XCD; PZ_GEMM_BATCH_XCD=0 = the 2-D grid): every layout, the joint-attention dK shape, fp32 and
+    bf16 outputs, beta accumulation -- run in a subprocess because the switch is read once per process"""
+    import subprocess
+    import sys
+
+    code = r"""
+import torch, sys
+sys.path.insert(0, 'open-pi-zero_amd')
+import pizero_native
+from pizero_native import ops
+pizero_native.lib()
+torch.manual_seed(0)
+dev = 'cuda'
+for (Bt, M, N, K) in ((16, 288, 256, 200), (8, 96, 80, 104)):
+    A = (torch.randn(Bt, M, K, device=dev) * 0.5).to(torch.bfloat16)
+    Bm = (torch.randn(Bt, N, K, device=dev) * 0.5).to(torch.bfloat16)
+    ref = A.float() @ Bm.float().transpose(1, 2)
+    for akc in (True, False):
+        for bkc in (True, False):
+            Aop = A if akc else A.transpose(1, 2).contiguous()
+            Bop = Bm if bkc else Bm.transpose(1, 2).contiguous()
+            C = torch.zeros(Bt, M, N, device=dev)
+            ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, C, N, batch=Bt, batch_inner=1,
+                     sA=(M * K, 0), sB=(N * K, 0), sC=(M * N, 0))
+            assert (C - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-3, (Bt, M, N, K, akc, bkc)
+            Cb = torch.empty(Bt, M, N, device=dev, dtype=torch.bfloat16)
+            ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, Cb, N, batch=Bt, batch_inner=1,
+                     sA=(M * K, 0), sB=(N * K, 0), sC=(M * N, 0))
+            ops.gemm(M, N, K, Aop, K if akc else M, akc, Bop, K if bkc else N, bkc, Cb, N, batch=Bt, batch_inner=1,
+                     sA=(M * K, 0), sB=(N * K, 0), sC=(M * N, 0), beta=True)
+            assert ((Cb.float() - 2 * ref).abs() <= 2e-2 * (2 * ref).abs() + 2e-2).all(), (Bt, M, N, K, akc, bkc)
+print('OK')
+"""
+    import os
+
+    env = dict(os.environ, PZ_GEMM_BATCH_XCD=xcd)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("K", [1024, 4304, 40])
 @pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True), (False, False)])
 def test_gemm256_layouts_with_tails(akc, bkc, K):

@@ -1656,6 +1656,16 @@ constexpr int FR_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FA_KB * FaDims
 // resident operand is staged once per unit, every LDS fragment read feeds two MFMAs (two 16-row
 // blocks), and the dK/dV pass takes its K/V fragments straight from global memory into registers
 // (no K/V image, no query-half reduction).  Grid = Z * H workgroups (1024 per micro-batch layer).
+// unit of this workgroup: the H heads of one image on one XCD (workgroups are dealt round-robin over
+// the 8 XCDs), so the 128-B lines that adjacent heads' 144-B q / k / v / O / dO segments share are fetched
+// into one L2 (the default order puts consecutive heads on different XCDs); Z % 8 != 0: linear
+__device__ __forceinline__ int64_t fa_unit_of(const pz_flash_args& a) {
+  const int64_t id = blockIdx.x;
+  if (a.Z % 8 != 0) return id;
+  const int64_t xcd = id & 7, local = id >> 3;
+  return ((local / a.H) * 8 + xcd) * a.H + local % a.H;
+}
+
 constexpr int FU_NW = 8;
 
 // PLAIN (no mask, no soft-cap: SigLIP): the element-wise softmax in the log2 domain with the scale
@@ -1671,7 +1681,7 @@ __global__ void __launch_bounds__(FU_NW * 64) flash_fwd_unit_kernel(pz_flash_arg
   bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
   bf16_t* Vall = Kall + FR_MAX * D::ROW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const int64_t zh = fa_unit_of(a), b = zh / a.H, h = zh % a.H;
   const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
   const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
   const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
@@ -1809,7 +1819,7 @@ __global__ void __launch_bounds__(FU_NW * 64) flash_bwd_q_unit_kernel(pz_flash_a
   bf16_t* Kall = reinterpret_cast<bf16_t*>(fa_smem);
   bf16_t* Vall = Kall + FR_MAX * D::ROW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const int64_t zh = fa_unit_of(a), b = zh / a.H, h = zh % a.H;
   const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
   const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
   const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
@@ -1942,7 +1952,7 @@ __global__ void __launch_bounds__(FU_NW * 64) flash_bwd_kv_unit_kernel(pz_flash_
   float* lse_all = reinterpret_cast<float*>(Dall + FR_MAX * D::ROW);
   float* del_all = lse_all + FR_MAX;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int64_t zh = blockIdx.x, b = zh / a.H, h = zh % a.H;
+  const int64_t zh = fa_unit_of(a), b = zh / a.H, h = zh % a.H;
   const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
   const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
   const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;

@@ -217,6 +217,9 @@ def main():
     ap.add_argument("--no-infer", action="store_true")
     ap.add_argument("--optim-bits", type=int, default=8, choices=(8, 32))
     ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--force-ddp", action="store_true",
+                    help="run the data-parallel path (process group + PiZeroDDP bucketed RCCL all-reduce on the "
+                         "comm stream) even at world size 1 (single-GPU check of the N>1 code path)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -227,7 +230,12 @@ def main():
     backend = os.environ.get("PZ_DIST_BACKEND", "nccl")
     torch.cuda.set_device(dev_idx)
     dev = torch.device(f"cuda:{dev_idx}")
-    if world > 1:
+    ddp = world > 1 or args.force_ddp
+    if ddp:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -247,7 +255,7 @@ def main():
     model.tie_action_proprio_weights()
     model.freeze_unused_weights()
     model.train()
-    meta = PiZeroDDP(model) if world > 1 else model
+    meta = PiZeroDDP(model, force_reduce=args.force_ddp) if ddp else model
     # the reference's optimizer is bnb AdamW8bit (train.py:171-175,194-198): blockwise 8-bit state
     opt_a = FusedAdamW(model.action_expert_parameters, lr=cfg.action_lr, weight_decay=cfg.action_weight_decay,
                        state_bits=args.optim_bits)
@@ -266,7 +274,7 @@ def main():
         for i in range(accum):
             b = batches[i % len(batches)]
             last = i == accum - 1
-            ctx = meta.no_sync() if (world > 1 and not last) else torch.enable_grad()
+            ctx = meta.no_sync() if (ddp and not last) else torch.enable_grad()
             with ctx:
                 loss = meta(**b)
                 (loss / accum).backward()
@@ -280,27 +288,27 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if ddp:
         dist.barrier()
     # live probe of the dominant kernel: the vlm GeGLU gate|up GEMM (M = mb*276, N = 2*16384, K = 2048)
     d = model._engine().d
     Mg, Ng, Kg = mb * d.P, 2 * d.gI, d.gH
     probe = ops.set_probe(lambda M, N, K, epi, batch: (M, N, K, epi) == (Mg, Ng, Kg, ops.PZ_EPI_GEGLU))
     torch.cuda.synchronize()
-    if world > 1:
+    if ddp:
         dist.barrier()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if world > 1:
+    if ddp:
         dist.all_reduce(loss_acc)
     torch.cuda.synchronize()
-    if world > 1:
+    if ddp:
         dist.barrier()
     el = time.perf_counter() - t1
     ops.set_probe(None)
     elt = torch.tensor([el], device=dev)
-    if world > 1:
+    if ddp:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
     durs = [a.elapsed_time(b) for a, b in probe]
@@ -368,6 +376,10 @@ def main():
                        "model": "pi0 (SigLIP-So400m/14 + Gemma-2B + 0.3B action expert)", "global_batch": gb,
                        "micro_batch": mb, "grad_accum": accum, "seq_len": d.L,
                        "parallelism": f"dp{world}"},
+            "ddp": None if not ddp else {
+                "backend": dist.get_backend(), "buckets_reduced_per_step": sum(1 for _ in meta.reducer.log) / max(
+                    1, args.steps + args.warmup), "async_rccl_buckets": sum(1 for a, _ in meta.reducer.log if a),
+                "forced_at_world_1": bool(args.force_ddp and world == 1)},
             "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
             "roofline": {"bound": "mfma", "kernel": kname + " (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,
@@ -384,7 +396,7 @@ def main():
                           "state_gb": (opt_a.state_bytes() + opt_v.state_bytes()) / 1e9},
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if ddp:
         dist.destroy_process_group()
 
 

@@ -133,7 +133,10 @@ __global__ void __launch_bounds__(256) adamw8_kernel(pz_adamw8_args a) {
   for (int k = 0; k < 4; ++k) {
     // the oracle divides (m / absmax); a reciprocal multiply would differ by an ulp at code midpoints
     const float x1 = mx1 > 0.f ? __fdiv_rn(m[k], mx1) : 0.f, x2 = mx2 > 0.f ? __fdiv_rn(v[k], mx2) : 0.f;
-    c1 |= quantize8(q1, x1, true) << (8 * k);
+    unsigned k1 = quantize8(q1, x1, true);
+    // bnb's sign fix: the m code keeps m's sign bit (a tiny negative m does not collapse to +0)
+    if (signbit(q1[k1]) != signbit(m[k])) k1 = m[k] > 0.f ? k1 + 1 : k1 - 1;
+    c1 |= (k1 & 255u) << (8 * k);
     c2 |= quantize8(q2, x2, false) << (8 * k);
   }
   if (nv == 4) {

@@ -29,6 +29,9 @@ class GradReducer:
         self.group = group
         self.enabled = True
         self.stream = torch.cuda.Stream() if arena.data.is_cuda else None
+        # (async, elements) per launched bucket since construction: "async" = the RCCL branch (event on the
+        # compute stream, all_reduce(AVG) enqueued on the communication stream)
+        self.log = []
         self._reset()
 
     def _reset(self):
@@ -42,12 +45,17 @@ class GradReducer:
             # gloo (CPU tests / single-GPU rehearsal): synchronous SUM then scale
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
             g.mul_(1.0 / dist.get_world_size(self.group))
+            self.log.append((False, hi - lo))
             return
         ev = torch.cuda.Event()
         ev.record()
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev)
             dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group)
+            # the arena slice is produced on the compute stream and consumed here: keep the caching
+            # allocator from recycling it before the collective ran
+            g.record_stream(self.stream)
+        self.log.append((True, hi - lo))
 
     def notify(self, stage, layer):
         if not self.enabled:
@@ -109,8 +117,11 @@ def region_marks(model):
 class PiZeroDDP(torch.nn.Module):
     """DistributedDataParallel-compatible wrapper (``.module``, ``no_sync()``, forward -> loss)."""
 
-    def __init__(self, module, bucket_bytes=256 << 20, group=None, broadcast=True):
+    def __init__(self, module, bucket_bytes=256 << 20, group=None, broadcast=True, force_reduce=False):
+        """force_reduce: reduce even in a world of one rank (an RCCL world_size=1 group exercises the
+        overlapped communication-stream path on a single GPU; AVG over one rank is the identity)."""
         super().__init__()
+        self.force_reduce = force_reduce
         self.module = module
         module._ddp_wrapper = self
         module.use_ddp = True
@@ -132,7 +143,7 @@ class PiZeroDDP(torch.nn.Module):
 
     def forward(self, *args, **kwargs):
         eng = self.module._engine()
-        if self._sync and dist.is_initialized() and dist.get_world_size(self.reducer.group) > 1:
+        if self._sync and dist.is_initialized() and (dist.get_world_size(self.reducer.group) > 1 or self.force_reduce):
             self.reducer.enabled = True
             eng.hook = self.reducer.notify
             eng.post_backward = self.reducer.finish

@@ -194,6 +194,7 @@ class Engine:
         self.split_dact = os.environ.get("PZ_SPLIT_DACT", "1") == "1"
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
+        self.f8_version = None
         if self.d.nkv != 1:
             raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
 
@@ -223,8 +224,10 @@ class Engine:
         mixture and the action expert (BASELINE.json configs[4]: fp8 attention / MLP GEMMs).  Prefill
         GEMMs (>= 65 rows) run W8A8 on the fp8 MFMA with per-row activation scales; denoise rows
         (<= 64) run W8A16 (codes expanded to bf16 in registers, RMSNorm still fused).  Taken from the
-        current weights: call again after the weights change."""
+        current weights; the codes carry the arena's weight version (``weights_version``) and every
+        inference entry point re-quantises them when the weights changed since (fp8_refresh)."""
         d = self.d
+        self.f8_version = self.weights_version()
         vt = "vision_tower.vision_model.encoder.layers."
         keys = []
         for i in range(d.vL):
@@ -246,6 +249,20 @@ class Engine:
             ops.fp8_quant_tensor(W, q, sc)
             f8[k[1]] = (q, sc)
         self.f8 = f8
+
+    def weights_version(self):
+        """Version of the weight arena: the shared version counter of arena.data, which torch bumps for
+        every in-place write through a parameter view (load_state_dict, load_pretrained_weights,
+        ``p.copy_``) and FusedAdamW.step bumps after its raw-pointer kernel writes."""
+        return self.ar.data._version
+
+    def fp8_refresh(self):
+        """Re-quantise the fp8 weight copies if the weights changed after prepare_fp8 (stale
+        e4m3 codes after an optimizer step / checkpoint load).  Returns True if it re-quantised."""
+        if self.f8 is None or self.f8_version == self.weights_version():
+            return False
+        self.prepare_fp8()
+        return True
 
     def lin(self, x, key, W, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, aux=None, norm=None):
         """ops.linear, or its fp8 form when prepare_fp8() holds codes for ``key`` (the weight name; the
@@ -329,7 +346,11 @@ class Engine:
         kc = d.kcols
         cols = torch.empty(M, kc, device=dev, dtype=BF16)
         ops.patchify(pix, cols, d.ps)
-        wpad = torch.zeros(d.vH, kc, device=dev, dtype=BF16)
+        # patch-embedding weight with its K padded to a multiple of 32 columns: an engine-owned buffer whose
+        # pad columns are zeroed once; the weight columns are refreshed by every forward (weights change)
+        wpad = self._ws.get(("wpad", dev))
+        if wpad is None:
+            wpad = self._ws[("wpad", dev)] = torch.zeros(d.vH, kc, device=dev, dtype=BF16)
         wpatch = self.w(vt + "embeddings.patch_embedding.weight").view(d.vH, -1)
         ops.copy_rows(wpatch, wpatch.shape[1], 0, wpad, kc, 0, 1, d.vH, wpatch.shape[1])
         x = torch.empty(M, d.vH, device=dev, dtype=BF16)
@@ -814,7 +835,7 @@ class Engine:
         ya = torch.empty_like(Xl)
         ra = torch.empty(Xl.shape[0], device=dev, dtype=F32)
         ops.rmsnorm(Xl, self.w("joint_model.mixtures.action.norm.weight"), ya, ra, d.rms_eps)
-        v = torch.zeros(B * Tg, 8, device=dev, dtype=BF16)
+        v = torch.empty(B * Tg, 8, device=dev, dtype=BF16)  # columns 0..A-1 written and read (8: 16-B rows)
         ops.small_linear(ya, self.w("action_decoder.weight"), v, bias=self.w("action_decoder.bias"))
         loss = torch.empty(1, device=dev, dtype=F32)
         ops.flow_loss(v[aoff:], 8, Tg * 8, x0, actions, loss, None, None, B, d.H, d.A, d.sig_min)
@@ -1051,6 +1072,7 @@ class Engine:
         dev = ids.device
         nh, hd = d.nh, d.hd
         Lcap = kc.shape[2]
+        self.fp8_refresh()
         nk = start + q
         table = self.w("embed_tokens.weight")
         img = table if pix is None else self.siglip_forward(pix, None)
@@ -1204,6 +1226,7 @@ class Engine:
     def infer_action(self, ids, pix, cnt, vpos, ppos, apos, proprios, noise, kcache, vcache, clip=True):
         d = self.d
         B = ids.shape[0]
+        self.fp8_refresh()
         self.prefill(ids, pix, cnt, vpos, ppos, proprios, kcache, vcache)
         action = noise.clone()
         t = torch.zeros(B, device=pix.device, dtype=F32)

@@ -35,6 +35,7 @@ class InferenceGraph:
         self.k, self.v = model._kv_buffers(bsz)
         self.graph = None
         self.out = None
+        self._f8 = None
 
     def _run(self):
         s = self.static
@@ -53,6 +54,7 @@ class InferenceGraph:
         s["noise"].copy_(noise.reshape(s["noise"].shape))
 
     def capture(self):
+        self._f8 = self.m._engine().f8
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -67,5 +69,11 @@ class InferenceGraph:
         return self
 
     def replay(self):
+        # bf16 weights are read in place (an optimizer step / checkpoint load is seen by the next replay);
+        # fp8 codes and their per-tensor scales are baked into the captured launches, so a weight change
+        # since the capture re-quantises them (Engine.fp8_refresh) and re-captures the graph
+        e = self.m._engine()
+        if e.f8 is not self._f8 or e.fp8_refresh():
+            self.capture()
         self.graph.replay()
         return self.out

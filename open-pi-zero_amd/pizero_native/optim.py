@@ -30,6 +30,7 @@ partial-sum order), so clipping -- and training -- is bitwise reproducible.
 from __future__ import annotations
 
 import torch
+from torch.autograd.graph import increment_version
 
 from . import ops
 from ._lib import PZ_SUMSQ_PARTS
@@ -39,17 +40,19 @@ MIN_8BIT_SIZE = 4096  # bnb Optimizer8bit min_8bit_size: smaller tensors keep fp
 
 
 def create_dynamic_map(signed=True, max_exponent_bits=7, total_bits=8):
-    """bitsandbytes' dynamic (tree) quantisation map: 256 sorted float32 values."""
+    """bitsandbytes' dynamic (tree) quantisation map: 256 sorted float32 values, built with the same
+    float32 torch arithmetic as bnb's functional.create_dynamic_map (float32 linspace, float32 means and
+    scale products), so the entries match bnb's saved qmap1 / qmap2 to the bit."""
     data = []
     nsb = total_bits - 1
     for i in range(max_exponent_bits):
         n = 2 ** (i + nsb - max_exponent_bits) + 1 if signed else 2 ** (i + nsb - max_exponent_bits + 1) + 1
-        b = torch.linspace(0.1, 1.0, n, dtype=torch.float64)
-        means = ((b[:-1] + b[1:]) / 2.0).tolist()
-        sc = 10.0 ** (-(max_exponent_bits - 1) + i)
-        data += [sc * x for x in means]
+        b = torch.linspace(0.1, 1, n)
+        means = (b[:-1] + b[1:]) / 2.0
+        sc = 10 ** (-(max_exponent_bits - 1) + i)
+        data += (sc * means).tolist()
         if signed:
-            data += [-sc * x for x in means]
+            data += (-sc * means).tolist()
     data += [0.0, 1.0]
     data += [0.0] * (2 ** total_bits - len(data))
     return torch.tensor(sorted(data), dtype=torch.float32)
@@ -126,6 +129,9 @@ class FusedAdamW(torch.optim.Optimizer):
         rows, blocks, n32, info = [], 0, 0, {}
         for p in sorted(r["params"], key=lambda q: q.data_ptr()):
             o = (p.data_ptr() - base) // es
+            if o % 4:  # pz_adamw8bit loads 4 codes / 4 bf16 elements per access from a segment start
+                raise ValueError(f"FusedAdamW(state_bits=8): parameter segment at element offset {o} is not "
+                                 "4-element aligned (arena parameters are 8-aligned; pass arena views)")
             nb = (p.numel() + BLOCK8 - 1) // BLOCK8
             if p.numel() >= MIN_8BIT_SIZE:
                 rows.append([o, p.numel(), blocks, -1])
@@ -225,6 +231,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 else:
                     ops.adamw8bit(r, g, self._qmap1, self._qmap2, group["lr"], b1, b2, group["eps"],
                                   group["weight_decay"], t, self._gscale)
+                # the kernels write through raw pointers: bump the parameters' (shared arena) version
+                # counter so weight-derived caches (the fp8 inference codes) see the change
+                increment_version(r["params"][0])
         self._gscale = None
 
     def zero_grad(self, set_to_none: bool = True):
@@ -263,6 +272,14 @@ class FusedAdamW(torch.optim.Optimizer):
             g["params"] = ids
             groups.append(g)
         return {"state": state, "param_groups": groups}
+
+    def _same_qmaps(self, s):
+        """True if a saved 8-bit state's maps equal this optimizer's (else its codes are dequantised with
+        the SAVED maps and requantised into ours)."""
+        for k, q in (("qmap1", self._qmap1), ("qmap2", self._qmap2)):
+            if k in s and not torch.equal(s[k].to(q.device, torch.float32).reshape(-1), q):
+                return False
+        return True
 
     @staticmethod
     def _fp32_moments(s, p, dev):
@@ -312,7 +329,8 @@ class FusedAdamW(torch.optim.Optimizer):
                     m, v = self._fp32_moments(s, p, dst["state1"].device)
                     dst["state1"].copy_(m)
                     dst["state2"].copy_(v)
-                elif "absmax1" in s and s["state1"].dtype == torch.uint8:  # same 8-bit layout
+                elif ("absmax1" in s and s["state1"].dtype == torch.uint8
+                      and self._same_qmaps(s)):  # same 8-bit layout and maps: codes copied as they are
                     for k in ("state1", "state2", "absmax1", "absmax2"):
                         dst[k].copy_(s[k].to(dst[k].device).reshape(dst[k].shape))
                 else:  # fp32 moments -> codes with a per-block absmax

@@ -42,25 +42,28 @@ class EvalAgent:
     def infer_chunk(self, input_ids, attention_mask, pixel_values, proprios, noise=None):
         """Tokenized observation -> [B, horizon, action_dim] normalised actions (eval.py:99-125)."""
         m = self.model
-        mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids(attention_mask, self.dtype)
-        itp, amask = m.split_full_mask_into_submasks(mask)
         dev = self.device
+        # masks are built on the device once per call: the block pattern built from the attention mask is
+        # known (its prefix counts are remembered), so no per-call validation or host sync follows
+        mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids(attention_mask.to(dev), self.dtype)
+        itp, amask = m.split_full_mask_into_submasks(mask)
         B = input_ids.shape[0]
         if noise is None:
             noise = torch.randn(B, m.horizon_steps, m.action_dim, device=dev)
         if not self.use_graph:
-            return m(input_ids.to(dev), pixel_values.to(dev, self.dtype), itp.to(dev), amask.to(dev), vpos.to(dev),
-                     ppos.to(dev), apos.to(dev), proprios.to(dev, self.dtype), noise=noise)
+            return m(input_ids.to(dev), pixel_values.to(dev, self.dtype), itp, amask, vpos, ppos, apos,
+                     proprios.to(dev, self.dtype), noise=noise)
         from pizero_native.graph import InferenceGraph
 
+        cnt = m.block_prefix_counts(itp, amask)
+        args = (input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), cnt, vpos, ppos, apos,
+                proprios.to(dev, torch.float32), noise)
         g = self._graphs.get(B)
         if g is None:
             g = self._graphs[B] = InferenceGraph(m, B)
-            g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m.block_prefix_counts(itp, amask),
-                   vpos.to(dev), ppos.to(dev), apos.to(dev), proprios.to(dev, torch.float32), noise)
+            g.load(*args)
             g.capture()
-        g.load(input_ids.to(dev), pixel_values.to(dev, torch.bfloat16), m.block_prefix_counts(itp, amask), vpos.to(dev),
-               ppos.to(dev), apos.to(dev), proprios.to(dev, torch.float32), noise)
+        g.load(*args)
         return g.replay().to(self.dtype)
 
     def run(self):

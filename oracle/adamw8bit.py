@@ -19,8 +19,11 @@ Algorithm (per parameter tensor with >= 4096 elements -- smaller tensors keep fp
     m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g*g;
     p += -lr*sqrt(1-b2^t)/(1-b1^t) * m / (sqrt(v) + eps*sqrt(1-b2^t));  then p *= 1 - lr*wd;
     absmax = max |.| over the block of the NEW m / v; codes = quantise(m/absmax), quantise(v/absmax)
-    by the 7-step binary search over the sorted map with midpoint rounding.
-All arithmetic is float32 (the kernel's), including the map values.
+    by the 7-step binary search over the sorted map with midpoint rounding; the m code then keeps
+    m's sign (bnb's sign fix: a code whose map entry has the other sign bit moves one step toward m).
+All arithmetic is float32 (the kernel's), including the map values (built by bnb's float32 torch
+arithmetic).  Still unpinned against bnb itself: its exact kernel launch shape (the block-local
+order of the absmax reduction does not change a max) and its handling of non-finite gradients.
 """
 
 from __future__ import annotations
@@ -32,23 +35,27 @@ MIN_8BIT_SIZE = 4096
 
 
 def create_dynamic_map(signed: bool = True, max_exponent_bits: int = 7, total_bits: int = 8) -> np.ndarray:
-    """The 256 sorted float32 values of the dynamic (tree) quantisation map."""
+    """The 256 sorted float32 values of the dynamic (tree) quantisation map, in bnb's own float32 torch
+    arithmetic (functional.create_dynamic_map: torch.linspace(0.1, 1, n) in float32, float32 means, the
+    python-float scale multiplied in float32), so each entry equals bnb's saved qmap entry to the bit."""
+    import torch
+
     data = []
     non_sign_bits = total_bits - 1
     additional_items = 2 ** (non_sign_bits - max_exponent_bits) - 1
     for i in range(max_exponent_bits):
         n = int(2 ** (i + non_sign_bits - max_exponent_bits) + 1 if signed
                 else 2 ** (i + non_sign_bits - max_exponent_bits + 1) + 1)
-        b = np.linspace(0.1, 1.0, n, dtype=np.float64)
+        b = torch.linspace(0.1, 1, n)
         means = (b[:-1] + b[1:]) / 2.0
-        scale = 10.0 ** (-(max_exponent_bits - 1) + i)
+        scale = 10 ** (-(max_exponent_bits - 1) + i)
         data += (scale * means).tolist()
         if signed:
             data += (-scale * means).tolist()
     if additional_items > 0:
-        b = np.linspace(0.1, 1.0, additional_items + 1, dtype=np.float64)
+        b = torch.linspace(0.1, 1, additional_items + 1)
         means = (b[:-1] + b[1:]) / 2.0
-        scale = 10.0 ** (-(max_exponent_bits - 1) + max_exponent_bits - 1)
+        scale = 10 ** (-(max_exponent_bits - 1) + max_exponent_bits - 1)
         data += (scale * means).tolist()
         if signed:
             data += (-scale * means).tolist()
@@ -116,7 +123,17 @@ def step_8bit(p, g, c1, c2, absmax1, absmax2, qmap1, qmap2, lr, b1, b2, eps, wd,
     am2 = np.abs(np.concatenate([v, np.zeros(pad, f)])).reshape(nb, BLOCK).max(1).astype(f)
     d1 = np.where(am1[blk] > 0, m / np.where(am1[blk] > 0, am1[blk], 1), 0).astype(f)
     d2 = np.where(am2[blk] > 0, v / np.where(am2[blk] > 0, am2[blk], 1), 0).astype(f)
-    return bf16_round(pn), quantize(d1, qmap1, True), quantize(d2, qmap2, False), am1, am2
+    return bf16_round(pn), sign_fix(quantize(d1, qmap1, True), m, qmap1), quantize(d2, qmap2, False), am1, am2
+
+
+def sign_fix(c1: np.ndarray, m: np.ndarray, qmap1: np.ndarray) -> np.ndarray:
+    """bnb's blockwise 2-state kernel keeps the sign of the first moment through quantisation: when the
+    chosen map entry's sign bit differs from m's (a tiny negative m rounded to the +0 entry), the code
+    moves one step toward m's sign (+1 if m > 0, else -1)."""
+    c = c1.astype(np.int64)
+    flip = np.signbit(qmap1[c]) != np.signbit(np.asarray(m, dtype=np.float32))
+    c = np.where(flip, np.where(m > 0, c + 1, c - 1), c)
+    return c.astype(np.uint8)
 
 
 def step_32bit(p, g, m, v, lr, b1, b2, eps, wd, t, gscale=1.0):

@@ -24,12 +24,30 @@ def build_gpu_model(d, dtype=torch.bfloat16):
     return m
 
 
-def gpu_inputs(m, d, bsz, ragged=True, repeat=1):
-    """Fixture inputs of batch ``bsz`` on the device; ``repeat`` tiles the batch (the loss is a mean
-    over samples, so a batch of r copies has the same loss and gradients -- batch invariance)."""
+def dealias_orders(bsz, repeat):
+    """``repeat`` different row orders of the ``bsz`` fixture samples: copy c is a distinct permutation
+    (identity, reversed, rotated by 6, reversed + rotated by 6), so for an even bsz (16) no slot holds the
+    same sample in two copies (even rotations: 2i = odd has no solution mod an even bsz) -- a batch-stride
+    error that aliases rows of different copies changes the loss / gradients."""
+    base = np.arange(bsz)
+    out = []
+    for c in range(repeat):
+        o = base[::-1] if c % 2 else base
+        out.append(np.roll(o, (c // 2) * 6))
+    return out
+
+
+def gpu_inputs(m, d, bsz, ragged=True, repeat=1, select=None):
+    """Fixture inputs of batch ``bsz`` on the device.  ``repeat`` tiles the batch with a different row
+    order per copy (dealias_orders; the loss is a mean over samples, so the r-fold batch has the same
+    loss and gradients -- batch invariance); ``select`` keeps only those fixture samples (e.g. [0]:
+    one sample of the fixture at B=1 -- samples are independent, so its outputs are that sample's)."""
     inp = synth_inputs(d, bsz, seed=0, ragged=ragged)
     if repeat > 1:
-        inp = {k: np.concatenate([v] * repeat, axis=0) for k, v in inp.items()}
+        orders = dealias_orders(bsz, repeat)
+        inp = {k: np.concatenate([v[o] for o in orders], axis=0) for k, v in inp.items()}
+    if select is not None:
+        inp = {k: v[list(select)] for k, v in inp.items()}
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
     am = T(inp["attention_mask"])
     mask, vpos, ppos, apos = m.build_causal_mask_and_position_ids(am, torch.bfloat16)

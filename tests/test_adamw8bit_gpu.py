@@ -148,3 +148,61 @@ def test_adamw8bit_state_dict_roundtrip_and_conversion():
     m4 = o4.state_dict()["state"][1]
     m4d = m4["qmap1"][m4["state1"].reshape(-1).long()] * m4["absmax1"][blk]
     assert float((m4d - m).abs().max()) <= 0.02 * float(m.abs().max())
+
+
+def test_adamw8bit_sign_fix_bit_exact():
+    """bnb's sign fix of the first-moment code: a block whose absmax is set by one large
+    gradient holds tiny negative m that quantise to the +0 entry; bnb moves their code one step to the
+    smallest negative entry.  Kernel == oracle (which restates the fix), and the fix is exercised."""
+    from oracle import adamw8bit as O8
+    from pizero_native.optim import FusedAdamW
+
+    n = 4096 + 256
+    w = torch.zeros(n, device="cuda", dtype=torch.bfloat16)
+    p = torch.nn.Parameter(w)
+    g = torch.full((n,), -1e-9, dtype=torch.float32)
+    g[::256] = 100.0
+    g[1::512] = 1e-9  # tiny positives stay on +0 (same sign bit)
+    p.grad = g.to("cuda", torch.bfloat16)
+    opt = FusedAdamW([p], lr=1e-3, state_bits=8)
+    opt.step()
+    torch.cuda.synchronize()
+    q1, q2 = O8.create_dynamic_map(True), O8.create_dynamic_map(False)
+    nb = n // 256
+    gg = p.grad.float().cpu().numpy()
+    rp, c1, c2, a1, a2 = O8.step_8bit(np.zeros(n, np.float32), gg, np.zeros(n, np.uint8), np.zeros(n, np.uint8),
+                                      np.zeros(nb, np.float32), np.zeros(nb, np.float32), q1, q2, 1e-3, 0.9, 0.999,
+                                      1e-8, 0.0, 1, 1.0)
+    st = opt.state_dict()["state"][0]
+    k1 = st["state1"].cpu().numpy().reshape(-1)
+    np.testing.assert_array_equal(k1, c1)
+    np.testing.assert_array_equal(st["state2"].cpu().numpy().reshape(-1), c2)
+    zero = int(np.nonzero(q1 == 0.0)[0][0])
+    assert (k1[2:256] == zero - 1).all(), np.unique(k1[2:256])  # tiny negatives: the smallest negative code
+    assert k1[1] == zero and q1[zero - 1] < 0
+
+
+def test_adamw8bit_load_foreign_qmap_requantises():
+    """a saved 8-bit state whose maps differ from ours is dequantised with the SAVED maps and requantised
+    (ADVICE r2), not read against our map"""
+    from pizero_native.optim import FusedAdamW
+
+    ps, w = _arena(7)
+    o = FusedAdamW(ps, lr=1e-3, state_bits=8)
+    gf = torch.randn(w.numel(), device="cuda").to(torch.bfloat16)
+    for p in ps:
+        off = (p.data_ptr() - w.data_ptr()) // 2
+        p.grad = gf[off:off + p.numel()].view(p.shape)
+    o.step()
+    sd = o.state_dict()
+    st = sd["state"][1]
+    foreign = st["qmap1"].clone() * 0.5  # a different (scaled) map
+    st["qmap1"] = foreign
+    blk = torch.arange(ps[1].numel(), device="cuda") // 256
+    want = foreign[st["state1"].reshape(-1).long()] * st["absmax1"][blk]
+    o2 = FusedAdamW(_arena(7)[0], lr=1e-3, state_bits=8)
+    o2.load_state_dict(sd)
+    s2 = o2.state_dict()["state"][1]
+    got = s2["qmap1"][s2["state1"].reshape(-1).long()] * s2["absmax1"][blk]
+    assert float((got - want).abs().max()) <= 0.02 * float(want.abs().max())
+    assert not torch.equal(s2["state1"], st["state1"])

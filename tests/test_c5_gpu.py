@@ -10,7 +10,9 @@ same embeddings (pz_fill_uniform reproduces oracle/synth.py bit-exactly) in bf16
 Tolerance: action hidden rel-L2 <= max(3x the reference's own bf16-vs-fp32 deviation, 3e-2); the
 input-embedding gradients and EVERY JointModel parameter gradient pass the probe gate of
 tests/pizero_gpu_helpers.py (sample rel-L2 <= 8 %, cosine >= 0.995, whole-tensor projections).
-Precision: bf16 (the fp8 variant of C5 is not built).  Both joint-attention kernels are checked.
+Precision: bf16 training-shape JointModel (C5's fp8 path is an inference path: its full-shape chunk is
+checked in tests/test_c5_pizero_gpu.py and its bridge-size reference gate in
+tests/test_pizero_gpu.py::test_full_actions_fp8).  Both joint-attention kernels are checked.
 """
 
 import types

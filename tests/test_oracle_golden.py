@@ -102,3 +102,28 @@ def test_infer_text_matches_reference():
     np.testing.assert_allclose(lg[:, :q].numpy(), pre, rtol=0, atol=1e-4 * scale)
     np.testing.assert_allclose(lg[:, q:].numpy(), steps, rtol=0, atol=1e-4 * scale)
     assert torch.equal(lg[:, q - 1:].argmax(-1), toks)
+
+
+def test_adamw8bit_maps_match_between_oracle_and_optimizer():
+    """the optimizer's device maps and the oracle's are the same float32 values (bnb's float32 torch
+    construction in both)"""
+    from oracle import adamw8bit as O8
+    from pizero_native.optim import create_dynamic_map
+
+    for s in (True, False):
+        a = O8.create_dynamic_map(s)
+        b = create_dynamic_map(s).numpy()
+        assert a.shape == (256,) and (a == b).all()
+        assert (np.diff(a) >= 0).all() and a[-1] == 1.0
+
+
+def test_adamw8bit_oracle_sign_fix():
+    from oracle import adamw8bit as O8
+
+    q1 = O8.create_dynamic_map(True)
+    zero = int(np.nonzero(q1 == 0.0)[0][0])
+    m = np.array([-1e-12, 1e-12, 0.0, -0.5], np.float32)
+    c = O8.quantize(m / np.float32(1.0), q1, True)
+    f = O8.sign_fix(c, m, q1)
+    assert c[0] == zero and f[0] == zero - 1  # tiny negative: off the +0 entry
+    assert f[1] == c[1] == zero and f[2] == zero and f[3] == c[3]

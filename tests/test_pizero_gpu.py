@@ -45,10 +45,13 @@ def _check_grads(g, m, label):
     return check_grads_probe(g, dict(m.named_parameters()), label=label)
 
 
-def _check_actions(g, a, key):
+def _check_actions(g, a, key, sel=None):
     ref = g[f"fp32/{key}"]
     rb = g[f"bf16/{key}"]
+    if sel is not None:  # a sub-batch of the fixture's samples (samples are independent)
+        ref, rb = ref[list(sel)], rb[list(sel)]
     a = a.float().cpu().numpy()
+    assert a.shape == ref.shape, (a.shape, ref.shape)
     dev = np.abs(rb - ref)
     err = np.abs(a - ref)
     assert err.mean() <= max(3 * dev.mean(), 5e-3), (err.mean(), dev.mean())
@@ -141,6 +144,32 @@ def test_full_actions_hipgraph(full):
     assert torch.equal(a.float(), eager.float()), float((a.float() - eager.float()).abs().max())
 
 
+@pytest.mark.parametrize("sample", [0, 1])
+def test_full_actions_b1_benched_config(full_model, sample):
+    """Config C4 as benched (bench.py: B=1, eager infer_action AND the hipGraph replay it times) against
+    the reference: sample ``sample`` of full.npz run alone must reproduce the fixture's actions for that
+    sample (pizero.py:416-490 treats samples independently).  B=1 routes the prefill's 256-row SigLIP and
+    276-row Gemma GEMMs and the 4-row denoise GEMVs through other kernels / split counts than B=2."""
+    from pizero_native.graph import InferenceGraph
+
+    d = O.FULL_DIMS
+    g = load_golden("full")
+    m = full_model
+    gi = gpu_inputs(m, d, int(g["bsz"]), select=[sample])
+    assert gi["input_ids"].shape[0] == 1
+    a = run_infer(m, gi, clip=False)
+    _check_actions(g, a, "actions_unclipped", sel=[sample])
+    ig = InferenceGraph(m, 1, clip=False)
+    ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"], gi["ppos"],
+            gi["apos"], gi["proprios"].float(), gi["noise"])
+    ig.capture()
+    for _ in range(2):
+        ag = ig.replay()
+    torch.cuda.synchronize()
+    _check_actions(g, ag.clone(), "actions_unclipped", sel=[sample])
+    assert torch.equal(ag.float(), a.float()), float((ag.float() - a.float()).abs().max())
+
+
 def test_full_actions_fp8(full):
     """Config C5's fp8 inference (PiZero.use_fp8_inference: e4m3 weights with per-tensor scales; prefill
     GEMMs W8A8 on the fp8 MFMA with per-row activation scales, denoise rows W8A16) at bridge size
@@ -173,6 +202,51 @@ def test_full_actions_fp8(full):
         m.use_fp8_inference(False)
 
 
+def test_fp8_codes_follow_weight_changes(full):
+    """the fp8 weight copies are re-quantised when the weights change after use_fp8_inference
+    (an in-place write through a parameter, e.g. load_state_dict; FusedAdamW.step bumps the same version
+    counter after its raw-pointer kernel writes): eager and hipGraph inference then equal a fresh
+    prepare on the new weights, never the stale codes."""
+    from pizero_native.graph import InferenceGraph
+    from pizero_native.optim import FusedAdamW
+
+    d, g, m, gi = full
+    B = int(g["bsz"])
+    name = "joint_model.mixtures.action.layers.3.mlp.down_proj.weight"
+    p = dict(m.named_parameters())[name]
+    keep = p.detach().clone()
+    try:
+        m.use_fp8_inference(True)
+        a0 = run_infer(m, gi, clip=False)
+        ig = InferenceGraph(m, B, clip=False)
+        ig.load(gi["input_ids"], gi["pixel_values"], m.block_prefix_counts(gi["itp"], gi["amask"]), gi["vpos"],
+                gi["ppos"], gi["apos"], gi["proprios"].float(), gi["noise"])
+        ig.capture()
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            p.mul_(-3.0)  # a large change of one fp8-served weight
+        a1 = run_infer(m, gi, clip=False)
+        ag = ig.replay().clone()
+        torch.cuda.synchronize()
+        m.use_fp8_inference(True)  # fresh codes of the new weights
+        a2 = run_infer(m, gi, clip=False)
+        assert not torch.equal(a0, a2)
+        assert torch.equal(a1, a2), float((a1.float() - a2.float()).abs().max())
+        assert torch.equal(ag.float(), a2.float()), float((ag.float() - a2.float()).abs().max())
+        # the optimizer's kernel writes bump the arena's weight version
+        v0 = m._engine().weights_version()
+        opt = FusedAdamW([p], lr=1e-3, state_bits=32)
+        p.grad = torch.ones_like(p)
+        opt.step()
+        p.grad = None
+        assert m._engine().weights_version() != v0
+    finally:
+        with torch.no_grad():
+            p.copy_(keep)
+        m.use_fp8_inference(False)
+        m.zero_grad(set_to_none=True)
+
+
 @pytest.fixture(scope="module")
 def b16(full_model):
     d = O.FULL_DIMS
@@ -191,8 +265,16 @@ def test_b16_loss_and_grads(b16):
 
 
 def test_microbatch64_batch_invariance(b16):
-    """The bench's micro-batch 64 = the 16 fixture samples x 4: same loss / gradients as B=16."""
+    """The bench's micro-batch 64 = the 16 fixture samples x 4 in 4 DIFFERENT row orders
+    (pizero_gpu_helpers.dealias_orders): same loss / gradients as B=16.  Copy c is a distinct
+    permutation, so an error that aliases sample i with sample i + 16c (a batch-stride bug in the
+    64-way batched attention GEMMs / kernels) changes the result."""
+    from tests.pizero_gpu_helpers import dealias_orders
+
     d, g, m = b16
+    orders = dealias_orders(16, 4)
+    assert all(not np.array_equal(orders[a], orders[b]) for a in range(4) for b in range(a))
+    assert all((orders[a] != orders[b]).all() for a in range(4) for b in range(a))  # no sample at the same slot
     gi = gpu_inputs(m, d, 16, repeat=4)
     assert gi["input_ids"].shape[0] == 64
     loss = run_loss(m, gi)

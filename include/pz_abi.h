@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 13
+#define PZ_ABI_VERSION 14
 
 enum {
   PZ_OK = 0,
@@ -163,6 +163,13 @@ typedef struct pz_qkv_rope_args {
   int64_t T, nh, hd, Lq, qoff, Lk, koff;
 } pz_qkv_rope_args;
 int pz_gemv_qkv_rope(const pz_qkv_rope_args* a, void* stream);
+/* The same fused projection + RoPE + scatter for MANY rows (training / prefill, mixture.py:162-215,
+ * utils.py:4-16, joint_model.py:170-257): one 8-phase 256-tile MFMA GEMM whose epilogue rounds each head's
+ * projection to bf16, rotates Q / K and writes Q / K / V straight into the joint buffers (no [M, N] qkv
+ * tensor, no pz_qkv_rope_split launch; bit-identical to that pair).  hd = 256, q_out required, norm_w NULL.
+ * Returns PZ_ERR_UNSUPPORTED when the shape does not take the 8-phase kernel (too few rows): the caller
+ * runs pz_gemm + pz_qkv_rope_split instead.  (ABI 14) */
+int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream);
 /* backward of the above: writes d(qkv) (un-rotates dQ/dK, copies dV).  dq NULL -> zero dQ part */
 int pz_qkv_rope_split_bwd(const void* dq, const void* dk, const void* dv, const int64_t* pos,
                           const float* cs, void* dqkv, int64_t B, int64_t T, int64_t nh, int64_t nkv,

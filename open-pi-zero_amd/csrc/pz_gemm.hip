@@ -55,6 +55,16 @@ struct GemmP {
   float neps;
   // fp8 W8A8 (gemm8p_f8_kernel): per-row activation scales [M] or NULL
   const float* rs;
+  // measurement knob (PZ_GEMM_DBG, read per call): 1 = the 8-phase kernels skip their epilogue stores
+  // (tools/epi_probe.py: main-loop time alone); 0 in every product run
+  int dbg;
+  // fused q|k|v RoPE epilogue (pz_gemm_qkv_rope; 8-phase kernel, head_dim 256 = one column tile per head):
+  // the bf16-rounded projection of head n0/256 is rotated at rpos[m] (table rcs) and scattered into the
+  // joint Q / K / V buffers like pz_qkv_rope_split; C is not written.  rcs == NULL: off.
+  const int64_t* rpos;
+  const float* rcs;
+  bf16_t *rq, *rk, *rv;
+  int64_t rT, rnh, rLq, rqoff, rLk, rkoff;
 };
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -1155,9 +1165,67 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
   }
 }
 
+// fused RoPE + Q / K / V scatter (pz_gemm_qkv_rope): the tile (256 rows x one head of 256 columns) is
+// rounded to bf16 into two LDS images (columns 0..127 | 128..255 = the two halves of every rotation pair,
+// utils.py:4-16 rotate_half), then each thread rotates 16-B chunk pairs (i..i+7 with i+128..i+135) and
+// writes them to the joint buffers -- the arithmetic of qkv_rope_split_kernel on the same bf16 inputs.
+__device__ __forceinline__ void epi8p_rope(const GemmP& p, int64_t m0, int64_t n0, int wr, int wc, int lane,
+                                           const f32x4 (&acc)[8][4], char* smem) {
+  const int g4 = 4 * (lane >> 4), rl = lane & 15;
+  char* img = smem + (wc >> 1) * 65536;
+#pragma unroll
+  for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha;
+      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+    }
+  lds_sync();
+  const int64_t h = n0 >> 8;  // head: 0..nh-1 query, nh key, nh+1 value
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int c = threadIdx.x + it * NT2, row = c >> 4, ch = c & 15;
+    const int64_t m = m0 + row;
+    if (m >= p.M) continue;
+    const int off = (ch ^ (row & 15)) << 4;
+    const u32x4 w1 = *reinterpret_cast<const u32x4*>(smem + row * 256 + off);
+    const u32x4 w2 = *reinterpret_cast<const u32x4*>(smem + 65536 + row * 256 + off);
+    const int64_t b = m / p.rT, t = m - b * p.rT;
+    if (h == p.rnh + 1) {  // value head: copied
+      bf16_t* dv = p.rv + (b * p.rLk + p.rkoff + t) * 256 + ch * 8;
+      *reinterpret_cast<u32x4*>(dv) = w1;
+      *reinterpret_cast<u32x4*>(dv + 128) = w2;
+      continue;
+    }
+    float x1[8], x2[8], o1[8], o2[8];
+    unpack8(w1, x1);
+    unpack8(w2, x2);
+    const float4* cs = reinterpret_cast<const float4*>(p.rcs + p.rpos[m] * 256 + 16 * ch);  // (cos, sin) x 8
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c2 = cs[q];
+      const float co0 = c2.x, si0 = c2.y, co1 = c2.z, si1 = c2.w;
+      o1[2 * q] = x1[2 * q] * co0 - x2[2 * q] * si0;
+      o2[2 * q] = x2[2 * q] * co0 + x1[2 * q] * si0;
+      o1[2 * q + 1] = x1[2 * q + 1] * co1 - x2[2 * q + 1] * si1;
+      o2[2 * q + 1] = x2[2 * q + 1] * co1 + x1[2 * q + 1] * si1;
+    }
+    bf16_t* d = h < p.rnh ? p.rq + (b * p.rLq + p.rqoff + t) * (p.rnh * 256) + h * 256 + ch * 8
+                          : p.rk + (b * p.rLk + p.rkoff + t) * 256 + ch * 8;
+    *reinterpret_cast<u32x4*>(d) = pack8v(o1);
+    *reinterpret_cast<u32x4*>(d + 128) = pack8v(o2);
+  }
+}
+
 template <bool GEGLU>
 __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m0, int64_t n0,
                                            int wr, int wc, int lane, const f32x4 (&acc)[8][4], char* smem) {
+  if (!GEGLU && p.rcs) {
+    epi8p_rope(p, m0, n0, wr, wc, lane, acc, smem);
+    return;
+  }
   const int g4 = 4 * (lane >> 4), rl = lane & 15;
   if (GEGLU) {
     if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
@@ -1263,6 +1331,10 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL, bool F8>
 __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (p.dbg >= 2 && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
+    const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {  // split tail: one K-piece of a leftover tile
@@ -1490,6 +1562,7 @@ __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
     }
   }
 
+  if (p.dbg == 1) return;
   if (piece >= 0) {  // split tail: raw partial sums, summed + epilogued by gemm8p_tail_epilogue
     f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)piece * (32 * NT2);
 #pragma unroll
@@ -1567,6 +1640,10 @@ __device__ __forceinline__ bf16x8 kh_frag(const char* opbase, int h, int rb, int
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (p.dbg >= 2 && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
+    const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
+    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {
@@ -2650,6 +2727,10 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.nw = (const bf16_t*)a->norm_w;
   p.neps = a->norm_eps;
   p.rs = a->fp8_mode == 1 ? a->a_row_scale : nullptr;
+  {
+    const char* e = getenv("PZ_GEMM_DBG");
+    p.dbg = e ? atoi(e) : 0;
+  }
   hipStream_t st = (hipStream_t)stream;
 
   const Plan pl = make_plan(a);
@@ -2728,6 +2809,48 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   if (a->a_kcontig && !a->b_kcontig) return launch_tile_any<true, false, 2, 0>(p, pl, a->batch, st);
   if (!a->a_kcontig && a->b_kcontig) return launch_tile_any<false, true, 2, 0>(p, pl, a->batch, st);
   return launch_tile_any<false, false, 2, 0>(p, pl, a->batch, st);
+}
+
+// q|k|v projection + RoPE + joint Q / K / V scatter in one 8-phase GEMM launch (training / prefill rows:
+// mixture.py:162-215 + utils.py:4-16 + joint_model.py:170-257).  PZ_ERR_UNSUPPORTED (no error text) when the
+// shape does not take the 8-phase 256-tile kernel: the caller then runs pz_gemm + pz_qkv_rope_split.
+extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
+  PZ_CHECK_ARG(a && a->x && a->W && a->pos && a->cs && a->k_out && a->v_out && a->M > 0 && a->K > 0,
+               "gemm_qkv_rope: bad args");
+  PZ_CHECK_ARG(a->hd == BT && a->nh >= 1 && a->q_out && a->N == (a->nh + 2) * a->hd && a->T > 0 && a->M % a->T == 0 &&
+                   !a->norm_w,
+               "gemm_qkv_rope: head_dim 256, N = (nh + 2) * 256, q_out set, M %% T == 0, no fused norm");
+  PZ_CHECK_ARG(PZ_ALIGNED(a->x, 16) && PZ_ALIGNED(a->W, 16) && a->ldx % 8 == 0 && a->ldw % 8 == 0 && a->K % 8 == 0 &&
+                   PZ_ALIGNED(a->q_out, 16) && PZ_ALIGNED(a->k_out, 16) && PZ_ALIGNED(a->v_out, 16),
+               "gemm_qkv_rope: 16-byte alignment");
+  pz_gemm_args g;
+  memset(&g, 0, sizeof(g));
+  g.M = a->M; g.N = a->N; g.K = a->K;
+  g.A = a->x; g.lda = a->ldx; g.a_kcontig = 1;
+  g.B = a->W; g.ldb = a->ldw; g.b_kcontig = 1;
+  g.C = a->q_out; g.ldc = a->N;
+  g.batch = 1; g.batch_inner = 1;
+  g.alpha = 1.f;
+  const Plan pl = make_plan(&g);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
+  if (!use_8phase() || pl.kind != PATH_256) return PZ_ERR_UNSUPPORTED;
+  GemmP p;
+  memset(&p, 0, sizeof(p));
+  p.A = (const bf16_t*)a->x;
+  p.B = (const bf16_t*)a->W;
+  p.C = a->q_out;
+  p.M = a->M; p.N = a->N; p.K = a->K;
+  p.lda = a->ldx; p.ldb = a->ldw; p.ldc = a->N;
+  p.batch_inner = 1;
+  p.alpha = 1.f;
+  p.tiles_m = (int)pl.tiles_m;
+  p.tiles_n = (int)pl.tiles_n;
+  p.rpos = a->pos;
+  p.rcs = a->cs;
+  p.rq = (bf16_t*)a->q_out;
+  p.rk = (bf16_t*)a->k_out;
+  p.rv = (bf16_t*)a->v_out;
+  p.rT = a->T; p.rnh = a->nh; p.rLq = a->Lq; p.rqoff = a->qoff; p.rLk = a->Lk; p.rkoff = a->koff;
+  return launch8p<true, true, false>(p, 1, (hipStream_t)stream);
 }
 
 extern "C" int pz_gemm_small(const pz_small_gemm_args* a, void* stream) {

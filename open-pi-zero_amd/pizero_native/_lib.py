@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 13  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 14  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -126,6 +126,7 @@ SIGNATURES = {
     "pz_qkv_rope_split": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
     "pz_qkv_rope_split_bwd": [vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, i64, i64, i64, vp],
     "pz_gemv_qkv_rope": [C.POINTER(QkvRopeArgs), vp],
+    "pz_gemm_qkv_rope": [C.POINTER(QkvRopeArgs), vp],
     "pz_decode_attn": [C.POINTER(DecodeAttnArgs), vp],
     "pz_decode_attn_ws_bytes": [i64, i64, i64],
     "pz_attn_softmax": [C.POINTER(SoftmaxArgs), vp],

@@ -123,7 +123,9 @@ class PiZeroDDP(torch.nn.Module):
         super().__init__()
         self.force_reduce = force_reduce
         self.module = module
-        module._ddp_wrapper = self
+        # a plain attribute, not a registered submodule (module -> wrapper -> module would make
+        # .train() / .eval() / .modules() recurse forever)
+        module.__dict__["_ddp_wrapper"] = self
         module.use_ddp = True
         self._sync = True
         ar = module._arena

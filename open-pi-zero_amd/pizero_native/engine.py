@@ -192,6 +192,9 @@ class Engine:
         # vectorised elementwise pass; "0" = fused into the dgrad GEMM's epilogue, which the 8-phase kernel
         # cannot overlap with its main loop (measured: "1" +0.7 % samples/s)
         self.split_dact = os.environ.get("PZ_SPLIT_DACT", "1") == "1"
+        # q|k|v GEMM with the RoPE + Q/K/V scatter in its epilogue (pz_gemm_qkv_rope) where the 8-phase kernel
+        # runs; PZ_FUSE_QKV_ROPE=0: GEMM + pz_qkv_rope_split (A/B, bit-identical)
+        self.fuse_qkv_rope = os.environ.get("PZ_FUSE_QKV_ROPE", "1") == "1"
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
         self.f8_version = None
@@ -600,11 +603,16 @@ class Engine:
                 h = torch.empty_like(x)
                 r = torch.empty(M, device=dev, dtype=F32)
                 ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, r, d.rms_eps)
-                W = (nh + 2) * hd
-                qkv = torch.empty(M, W, device=dev, dtype=BF16)
-                ops.linear(h, self.qkv_w(p), qkv)
-                ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L, g.off,
-                                   Lp, g.off)
+                # q|k|v projection + RoPE + joint scatter: one 8-phase GEMM whose epilogue rotates and writes
+                # Q / K / V (N1: no [M, 2560] qkv tensor, no split launch); rows too few for the 8-phase
+                # kernel (the action expert's 320) take GEMM + qkv_rope_split (same bits)
+                if not (self.fuse_qkv_rope and ops.gemm_qkv_rope(h, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta),
+                                                                 Qj, Kj, Vj, g.T, nh, hd, L, g.off, Lp, g.off)):
+                    W = (nh + 2) * hd
+                    qkv = torch.empty(M, W, device=dev, dtype=BF16)
+                    ops.linear(h, self.qkv_w(p), qkv)
+                    ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L,
+                                       g.off, Lp, g.off)
                 st["g"][g.name] = {"x": x, "h": h, "r": r}
             Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
             if self.joint_flash and not isinstance(cnt, GeneralMask):
@@ -1030,11 +1038,15 @@ class Engine:
                     ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), None, Kj, Vj, B, g.T, nh, 1, hd, L1,
                                        g.off, Lp, g.off)
                     continue
+                hs[g.name] = h
+                if self.fuse_qkv_rope and not (self.f8 and (p + "self_attn.q_proj.weight") in self.f8) and \
+                        ops.gemm_qkv_rope(h, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, g.T, nh, hd,
+                                          L1, g.off, Lp, g.off):
+                    continue  # many rows (B >= 16): projection + RoPE + scatter in one 8-phase GEMM
                 qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
                 self.lin(h, p + "self_attn.q_proj.weight", self.qkv_w(p), qkv)
                 ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, B, g.T, nh, 1, hd, L1, g.off,
                                    Lp, g.off)
-                hs[g.name] = h
             if last:
                 break
             if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over the L1 prefix keys

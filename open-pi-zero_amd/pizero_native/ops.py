@@ -26,6 +26,7 @@ from ._lib import (
     FlashArgs,
     GemmArgs,
     SmallGemmArgs,
+    NativeError,
     SoftmaxArgs,
     call,
     lib,
@@ -335,6 +336,28 @@ def gemv_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, k
     a.q_out, a.k_out, a.v_out = _p(q_out), _p(k_out), _p(v_out)
     a.T, a.nh, a.hd, a.Lq, a.qoff, a.Lk, a.koff = T, nh, hd, Lq, qoff, Lk, koff
     call("pz_gemv_qkv_rope", C.byref(a), _st())
+
+
+PZ_ERR_UNSUPPORTED = 3  # include/pz_abi.h
+
+
+def gemm_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, koff):
+    """Many-row q|k|v projection with RoPE and the joint Q / K / V scatter fused into the 8-phase GEMM's
+    epilogue (pz_gemm_qkv_rope).  Returns False (nothing launched) when the shape does not take the
+    8-phase kernel -- the caller then runs linear + qkv_rope_split (same bits)."""
+    a = QkvRopeArgs()
+    a.x, a.ldx = _p(x), x.stride(0)
+    a.W, a.ldw = _p(W), W.stride(0)
+    a.M, a.N, a.K = x.shape[0], W.shape[0], x.shape[1]
+    a.pos, a.cs = _p(pos), _p(cs)
+    a.q_out, a.k_out, a.v_out = _p(q_out), _p(k_out), _p(v_out)
+    a.T, a.nh, a.hd, a.Lq, a.qoff, a.Lk, a.koff = T, nh, hd, Lq, qoff, Lk, koff
+    rc = lib().pz_gemm_qkv_rope(C.byref(a), _st())
+    if rc == PZ_ERR_UNSUPPORTED:
+        return False
+    if rc != 0:
+        raise NativeError(f"pz_gemm_qkv_rope failed (rc={rc}): {lib().pz_last_error().decode(errors='replace')}")
+    return True
 
 
 def decode_attn(q, Lq, qoff, k, v, o, B, nh, T, nk, scale, cap, cnt, prefix, cond, qtok0):

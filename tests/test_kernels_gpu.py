@@ -709,3 +709,38 @@ def test_decode_attn_matches_reference(B, T, cnts, P):
     s = s.masked_fill(~allowed[:, None, None, :], float("-inf"))
     ref = torch.einsum("bhtj,bjd->bthd", torch.softmax(s, -1), v.float()[:, :nk]).reshape(B * T, nh * hd)
     close(o, ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("B,T,off", [(16, 276, 0), (64, 276, 0), (16, 5, 276)])
+def test_gemm_qkv_rope_bit_identical_to_gemm_plus_split(B, T, off):
+    """pz_gemm_qkv_rope (q|k|v GEMM with RoPE + joint Q/K/V scatter in the 8-phase epilogue, N1) against
+    pz_gemm + pz_qkv_rope_split on the same bf16 inputs: bit-identical joint buffers, incl. a partial last
+    row tile (B=16: 4416 rows) and the benched micro-batch (17664 rows).  Shapes the 8-phase kernel does
+    not take (B=16 x 5 expert rows) return False and launch nothing."""
+    from pizero_native import ops
+
+    nh, hd, K = 8, 256, 2048
+    L, Lp = 281, 288
+    M = B * T
+    x, W = bf(M, K), bf((nh + 2) * hd, K, scale=K ** -0.5)
+    pos = (torch.arange(T, device=dev) + 1 + off).repeat(B).contiguous()
+    cs = torch.empty((L + 9) * hd, device=dev, dtype=torch.float32)
+    ops.rope_table(cs, L + 8, hd, 10000.0)
+    outs = []
+    for fused in (True, False):
+        Q = torch.full((B, L, nh * hd), 7.0, device=dev, dtype=torch.bfloat16)
+        Kj = torch.full((B, Lp, hd), 7.0, device=dev, dtype=torch.bfloat16)
+        Vj = torch.full((B, Lp, hd), 7.0, device=dev, dtype=torch.bfloat16)
+        done = fused and ops.gemm_qkv_rope(x, W, pos, cs, Q, Kj, Vj, T, nh, hd, L, off, Lp, off)
+        if fused and T < 256:
+            assert not done  # 80 rows: not an 8-phase shape
+        if not done:
+            qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, qkv)
+            ops.qkv_rope_split(qkv, pos, cs, Q, Kj, Vj, B, T, nh, 1, hd, L, off, Lp, off)
+        outs.append((Q, Kj, Vj))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), float((a.float() - b.float()).abs().max())
+    if T >= 256:  # the rows the fused epilogue did not own are untouched
+        assert (outs[0][0][:, T + off:] == 7.0).all() and (outs[0][1][:, T + off:] == 7.0).all()

@@ -212,8 +212,8 @@ def test_fp8_codes_follow_weight_changes(full):
 
     d, g, m, gi = full
     B = int(g["bsz"])
-    name = "joint_model.mixtures.action.layers.3.mlp.down_proj.weight"
-    p = dict(m.named_parameters())[name]
+    name = "joint_model.mixtures.action.layers.0.mlp.down_proj.weight"
+    p = m._param(name)  # (tied: named_parameters() may list it under the proprio alias)
     keep = p.detach().clone()
     try:
         m.use_fp8_inference(True)

@@ -40,8 +40,10 @@ __global__ void qkv_rope_split_kernel(const bf16_t* __restrict__ qkv, const int6
       const int h = e / half, i = e % half;
       const float x1 = bf2f(src[h * hd + i]), x2 = bf2f(src[h * hd + i + half]);
       const float co = c[2 * i], si = c[2 * i + 1];
-      dq[h * hd + i] = f2bf(x1 * co - x2 * si);
-      dq[h * hd + i + half] = f2bf(x2 * co + x1 * si);
+      float o1, o2;
+      rope_pair(x1, x2, co, si, o1, o2);
+      dq[h * hd + i] = f2bf(o1);
+      dq[h * hd + i + half] = f2bf(o2);
     }
   }
   bf16_t* dk = k_out + (b * Lk + koff + t) * (int64_t)(nkv * hd);
@@ -52,8 +54,10 @@ __global__ void qkv_rope_split_kernel(const bf16_t* __restrict__ qkv, const int6
     const int h = e / half, i = e % half;
     const float x1 = bf2f(sk[h * hd + i]), x2 = bf2f(sk[h * hd + i + half]);
     const float co = c[2 * i], si = c[2 * i + 1];
-    dk[h * hd + i] = f2bf(x1 * co - x2 * si);
-    dk[h * hd + i + half] = f2bf(x2 * co + x1 * si);
+    float o1, o2;
+    rope_pair(x1, x2, co, si, o1, o2);
+    dk[h * hd + i] = f2bf(o1);
+    dk[h * hd + i + half] = f2bf(o2);
   }
   for (int e = threadIdx.x; e < nkv * hd; e += blockDim.x) dv[e] = sv[e];
 }

@@ -898,7 +898,7 @@ __device__ __forceinline__ bf16x8 frag_tr_asm(const char* lds, int rb, int kk, i
 // Edge tiles use the general per-group store_out4_rt.
 enum FastMode { FM_STORE = 0, FM_BF16 = 1, FM_F32 = 2, FM_DACT = 3, FM_DGEGLU = 4 };
 
-__device__ __forceinline__ int fast_mode(const GemmP& p) {
+__host__ __device__ __forceinline__ int fast_mode(const GemmP& p) {
   if (p.epi == PZ_EPI_DGEGLU) return FM_DGEGLU;
   if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) return FM_DACT;
   if (p.c_fp32) return FM_F32;
@@ -1207,10 +1207,8 @@ __device__ __forceinline__ void epi8p_rope(const GemmP& p, int64_t m0, int64_t n
     for (int q = 0; q < 4; ++q) {
       const float4 c2 = cs[q];
       const float co0 = c2.x, si0 = c2.y, co1 = c2.z, si1 = c2.w;
-      o1[2 * q] = x1[2 * q] * co0 - x2[2 * q] * si0;
-      o2[2 * q] = x2[2 * q] * co0 + x1[2 * q] * si0;
-      o1[2 * q + 1] = x1[2 * q + 1] * co1 - x2[2 * q + 1] * si1;
-      o2[2 * q + 1] = x2[2 * q + 1] * co1 + x1[2 * q + 1] * si1;
+      rope_pair(x1[2 * q], x2[2 * q], co0, si0, o1[2 * q], o2[2 * q]);
+      rope_pair(x1[2 * q + 1], x2[2 * q + 1], co1, si1, o1[2 * q + 1], o2[2 * q + 1]);
     }
     bf16_t* d = h < p.rnh ? p.rq + (b * p.rLq + p.rqoff + t) * (p.rnh * 256) + h * 256 + ch * 8
                           : p.rk + (b * p.rLk + p.rkoff + t) * 256 + ch * 8;
@@ -1583,6 +1581,290 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_kernel(GemmP p) {
 template <bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8p_f8_kernel(GemmP p) {
   gemm8p_body<true, true, GEGLU, KTAIL, true>(p);
+}
+
+// ---- persistent 8-phase kernel (k-contiguous A and B: the forward NT GEMMs) --------------------
+// The epilogue of the one-shot kernel is not overlapped with anything: its stores must drain before the
+// workgroup exits and frees the 128 KiB of LDS, and only then does the next tile's workgroup start its
+// prologue DMA (measured, tools/epi_probe.py: the vlm GeGLU GEMM 2.26 ms with stores vs 1.70 without; a
+// staggered first round did not help, so it is this per-CU serialisation, not a chip-wide write burst).
+// Here one workgroup per CU walks the work units blockIdx.x, +G, +2G, ... (whole tiles, then the
+// split-tail K-pieces) as ONE stream of K-steps: the LDS-DMA of the next unit's first two K-steps is
+// issued during the current unit's last two (the steady-state schedule, unchanged), and the epilogue
+// stores go straight from the accumulators to global memory (no LDS staging: both buffers are filling)
+// while those loads are in flight.  vmcnt retires in issue order, so the waits of the first K-step after
+// an epilogue count its memory ops as younger (+adj: a lower bound of the ops it issued); the second
+// K-step's waits then also retire the stores, one K-step after they were issued.
+#define PZ_WVM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+__device__ __forceinline__ void wait_vm10(int adj) {
+  if (adj >= 48) PZ_WVM(58);
+  else if (adj >= 32) PZ_WVM(42);
+  else if (adj >= 16) PZ_WVM(26);
+  else PZ_WVM(10);
+}
+__device__ __forceinline__ void wait_vm8(int adj) {
+  if (adj >= 48) PZ_WVM(56);
+  else if (adj >= 32) PZ_WVM(40);
+  else if (adj >= 16) PZ_WVM(24);
+  else PZ_WVM(8);
+}
+__device__ __forceinline__ void wait_vm2(int adj) {
+  if (adj >= 48) PZ_WVM(50);
+  else if (adj >= 32) PZ_WVM(34);
+  else if (adj >= 16) PZ_WVM(18);
+  else PZ_WVM(2);
+}
+
+struct Unit8 {
+  int64_t m0, n0;
+  int kt0, nk, piece;  // piece < 0: a whole tile
+};
+
+template <bool GEGLU>
+__device__ __forceinline__ Unit8 unit8_of(const GemmP& p, int u, int nk_all) {
+  Unit8 r;
+  int lid = u;
+  r.piece = -1;
+  r.kt0 = 0;
+  r.nk = nk_all;
+  if (p.tail_s && lid >= p.dp_tiles) {
+    const int v = lid - p.dp_tiles;
+    r.piece = v;
+    lid = p.dp_tiles + v / p.tail_s;
+    r.kt0 = (v % p.tail_s) * p.tail_kt;
+    r.nk = min(nk_all - r.kt0, p.tail_kt);
+  }
+  int tm, tn;
+  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  r.m0 = (int64_t)tm * BT;
+  r.n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
+  return r;
+}
+
+template <bool GEGLU, bool KTAIL, int FM>  // FM: interior epilogue class (FM_STORE | FM_BF16; GEGLU: unused)
+__global__ void __launch_bounds__(NT2, 1) gemm8q_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nk_all = (int)((p.K + 63) / 64);
+  const int T = p.tiles_m * p.tiles_n;
+  const int U = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
+  const int G = gridDim.x;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = wave >> 2, wc = wave & 3;
+  const int g4 = 4 * (lane >> 4), rl = lane & 15;
+  // thread constants of the k-contiguous LDS images (p8_src): region row (t >> 3) + 64 i, 16-B chunk
+  const int trow = t >> 3;
+  const int colofs = 8 * ((t & 7) ^ ((t >> 4) & 7));
+  const int krem = KTAIL ? (int)(p.K - (int64_t)(nk_all - 1) * 64) : 64;  // valid k of the last K-tile
+  constexpr int lds_off[4] = {0, 2 * P8_REG, 3 * P8_REG, P8_REG};
+
+  int ucur = blockIdx.x;
+  Unit8 cur = unit8_of<GEGLU>(p, ucur, nk_all);
+  int unxt = ucur + G;
+  const bool has_nxt0 = unxt < U;
+  Unit8 nxt = has_nxt0 ? unit8_of<GEGLU>(p, unxt, nk_all) : cur;
+  bool has_nxt = has_nxt0;
+  int cur_start = 0, cur_end = cur.nk;  // global K-steps [cur_start, cur_end) belong to cur
+
+  // LDS-DMA of one piece (0 = A region 0, 1 = B region 0, 2 = B region 1, 3 = A region 1) of global
+  // K-step `step` (which belongs to cur or, from cur_end on, to nxt)
+  auto issue = [&](int piece, int step) {
+    const bool in_cur = step < cur_end;
+    const int64_t row0 = in_cur ? (piece == 0 || piece == 3 ? cur.m0 : cur.n0) : (piece == 0 || piece == 3 ? nxt.m0 : nxt.n0);
+    const int kt = in_cur ? cur.kt0 + (step - cur_start) : nxt.kt0 + (step - cur_end);
+    char* dst = smem + (step & 1) * P8_BUF + lds_off[piece] + wave * 1024;
+    const bool isA = piece == 0 || piece == 3;
+    const int region = (piece == 3 || piece == 2) ? 1 : 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      int64_t g;
+      if (isA) {
+        g = row0 + i * 128 + region * 64 + trow;
+        g = g < p.M ? g : p.M - 1;
+      } else if (GEGLU) {
+        const int v = region * 128 + i * 64 + trow;
+        g = row0 + (v >> 6) * 32 + (v & 31);
+        g = g < p.geglu_I ? g : p.geglu_I - 1;
+        if ((v >> 5) & 1) g += p.geglu_I;
+      } else {
+        g = row0 + region * 128 + i * 64 + trow;
+        g = g < p.N ? g : p.N - 1;
+      }
+      const bf16_t* src = (isA ? p.A + g * p.lda : p.B + g * p.ldb) + colofs + (int64_t)kt * 64;
+      if (KTAIL && krem < 64 && kt == nk_all - 1 && colofs >= krem) src -= colofs - (krem - 8);
+      glds16(src, dst + i * 8192);
+    }
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bf[2][2][2];
+  auto read_a = [&](const char* buf, int ah) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<true>(buf + ah * P8_REG, wr * 4 + i, kk, lane);
+  };
+  auto read_b = [&](const char* buf, int bh) {
+    const char* reg = buf + 2 * P8_REG + (wc >> 1) * P8_REG;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) bf[bh][j][kk] = frag<true>(reg, (wc & 1) * 4 + bh * 2 + j, kk, lane);
+  };
+  auto mask_tail_a = [&](int kt) {
+    if (KTAIL && krem < 64 && kt == nk_all - 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          if (kk * 32 + 8 * (lane >> 4) >= krem) af[i][kk] = bf16x8{};
+    }
+  };
+  auto mfma_quad = [&](int ah, int bh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ah * 4 + i][bh * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[bh][j][kk], af[i][kk], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: global K-steps 0 (all pieces) and 1 (A0, B0, B1); every unit has >= 2 K-steps
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  const bool two = cur.nk > 1 || has_nxt;
+  if (two) {
+    issue(0, 1);
+    issue(1, 1);
+    issue(2, 1);
+    PZ_WAIT_VM(8);
+  } else {
+    PZ_WAIT_VM(2);
+  }
+  PZ_RAW_BARRIER();
+  if (wr == 1) PZ_RAW_BARRIER();  // stagger: row-1 waves run one barrier behind
+
+  int s = 0;    // global K-step
+  int adj = 0;  // memory ops of the epilogue just before this K-step (lower bound; 0: none)
+  while (true) {
+    const int kt = cur.kt0 + (s - cur_start);
+    const char* buf = smem + (s & 1) * P8_BUF;
+    const bool n1 = s + 1 < cur_end || has_nxt, n2 = s + 2 < cur_end || has_nxt;
+    // phase 0: quadrant (0,0)
+    if (n1) issue(3, s + 1);
+    read_a(buf, 0);
+    read_b(buf, 0);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mask_tail_a(kt);
+    mfma_quad(0, 0);
+    PZ_RAW_BARRIER();
+    // phase 1: quadrant (0,1); retire A region 1 of this K-step
+    if (n2) issue(0, s + 2);
+    read_b(buf, 1);
+    if (n2) wait_vm10(adj);
+    else if (n1) wait_vm8(adj);
+    else PZ_WAIT_VM(0);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mfma_quad(0, 1);
+    PZ_RAW_BARRIER();
+    // phase 2: quadrant (1,1)
+    if (n2) issue(1, s + 2);
+    read_a(buf, 1);
+    PZ_WAIT_LGKM0();
+    PZ_RAW_BARRIER();
+    mask_tail_a(kt);
+    mfma_quad(1, 1);
+    PZ_RAW_BARRIER();
+    // phase 3: quadrant (1,0); retire the next K-step's phase-0 operands
+    if (n2) issue(2, s + 2);
+    if (n2) wait_vm8(adj);
+    else if (n1) wait_vm2(adj);
+    PZ_RAW_BARRIER();
+    mfma_quad(1, 0);
+    PZ_RAW_BARRIER();
+    adj = 0;
+    ++s;
+    if (s < cur_end) continue;
+
+    // ---- unit done: epilogue straight from the accumulators (no LDS), then the next unit ----
+    const bool last = !has_nxt;
+    if (last && wr == 0) PZ_RAW_BARRIER();
+    if (p.dbg != 1) {
+      if (cur.piece >= 0) {  // split tail: raw partial sums (gemm8p_tail_epilogue merges them)
+        f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)cur.piece * (32 * NT2);
+#pragma unroll
+        for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) W[(rb * 4 + cb) * NT2 + t] = acc[rb][cb];
+        adj = 32;
+      } else if (GEGLU) {
+        if (cur.m0 + BT <= p.M && cur.n0 + BT / 2 <= p.geglu_I && p.aux) {
+#pragma unroll
+          for (int rb = 0; rb < 8; ++rb) {
+            const int64_t m = cur.m0 + wr * 128 + rb * 16 + rl;
+            bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + cur.n0 + wc * 32 + g4;
+            bf16_t* Xr = p.aux + m * p.ld_aux + cur.n0 + wc * 32 + g4;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              float gg[4], uu[4], hh[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                gg[r] = acc[rb][j][r] * p.alpha;
+                uu[r] = acc[rb][2 + j][r] * p.alpha;
+                hh[r] = gelu_tanh(gg[r]) * uu[r];
+              }
+              *reinterpret_cast<u32x2*>(Cr + j * 16) = pk4(hh);
+              *reinterpret_cast<u32x2*>(Xr + j * 16) = pk4(gg);
+              *reinterpret_cast<u32x2*>(Xr + p.geglu_I + j * 16) = pk4(uu);
+            }
+          }
+          adj = 48;
+        } else {
+#pragma unroll
+          for (int rb = 0; rb < 8; ++rb) {
+            const int64_t m = cur.m0 + wr * 128 + rb * 16 + rl;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              store_geglu4(p, 0, m, cur.n0 + wc * 32 + j * 16 + g4, acc[rb][j], acc[rb][2 + j]);
+          }
+        }
+      } else {
+        const int64_t m = cur.m0 + wr * 128 + rl, nb = cur.n0 + wc * 64 + g4;
+        if (cur.m0 + BT <= p.M && cur.n0 + BT <= p.N) {
+          epi8p_fast<FM>(p, 0, 0, m, nb, acc);
+          adj = 32;
+        } else {
+#pragma unroll
+          for (int rb = 0; rb < 8; ++rb)
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) store_out4_rt(p, 0, 0, m + rb * 16, nb + cb * 16, acc[rb][cb]);
+        }
+      }
+    }
+    if (last) break;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    cur = nxt;
+    cur_start = cur_end;
+    cur_end = cur_start + cur.nk;
+    unxt += G;
+    has_nxt = unxt < U;
+    if (has_nxt) nxt = unit8_of<GEGLU>(p, unxt, nk_all);
+  }
 }
 
 // ---- k-half variant of the ping-pong kernel -----------------------------------
@@ -2615,9 +2897,50 @@ static void launch_tail(const GemmP& p, int T, hipStream_t st) {
     hipLaunchKernelGGL((gemm8p_tail_epilogue<GEGLU, 8>), dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
 }
 
+// persistent 8-phase kernel (gemm8q_kernel) for k-contiguous A and B: batch 1, no fused RoPE epilogue
+// (its LDS staging), every work unit >= 2 K-steps; PZ_GEMM_PERSIST=0 keeps the one-shot kernel (A/B)
+static bool use_persist(const GemmP& p, int64_t batch, bool geglu) {
+  const char* e = getenv("PZ_GEMM_PERSIST");
+  if (e && e[0] == '0') return false;
+  if (batch != 1 || p.rcs) return false;
+  if (!geglu && fast_mode(p) != FM_STORE && fast_mode(p) != FM_BF16) return false;
+  const int nk = (int)((p.K + 63) / 64);
+  if (nk < 2) return false;
+  if (p.tail_s && nk - (p.tail_s - 1) * p.tail_kt < 2) return false;  // a 1-step last K-piece
+  return true;
+}
+
+template <bool GEGLU, bool KTAIL, int FM>
+static int launch8q(const GemmP& p, hipStream_t st) {
+  const int smem = 2 * P8_BUF;
+  auto kern = gemm8q_kernel<GEGLU, KTAIL, FM>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  const int T = p.tiles_m * p.tiles_n;
+  const int U = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
+  const int G = device_cus();
+  hipLaunchKernelGGL(kern, dim3((unsigned)(U < G ? U : G)), dim3(NT2), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  if (p.tail_s) {
+    launch_tail<GEGLU>(p, T, st);
+    PZ_CHECK_LAUNCH();
+  }
+  return PZ_OK;
+}
+
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
+  if constexpr (AKC && BKC) {
+    if (use_persist(p, batch, GEGLU)) {
+      if (GEGLU) return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
+      if (fast_mode(p) == FM_STORE) return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
+      return launch8q<GEGLU, KTAIL, FM_BF16>(p, st);
+    }
+  }
   const bool kh = use_khalf(AKC, BKC);
   auto kern = kh ? gemm8k_kernel<AKC, BKC, GEGLU, KTAIL> : gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
   static bool attr_set[2] = {false, false};

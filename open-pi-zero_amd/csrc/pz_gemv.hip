@@ -235,7 +235,8 @@ __global__ void __launch_bounds__(256) gemv_qkv_rope_kernel(GemvP p) {
   }
   const float* cs = p.cs + p.pos[r] * p.hd;
   const float co = cs[2 * i], si = cs[2 * i + 1];
-  const float o1 = y1 * co - y2 * si, o2 = y2 * co + y1 * si;
+  float o1, o2;
+  rope_pair(y1, y2, co, si, o1, o2);
   bf16_t* d = h < p.nh ? p.q + (b * p.Lq + p.qoff + t) * (p.nh * p.hd) + h * p.hd
                        : p.k + (b * p.Lk + p.koff + t) * p.hd;
   d[i] = f2bf(o1);

@@ -744,3 +744,63 @@ def test_gemm_qkv_rope_bit_identical_to_gemm_plus_split(B, T, off):
         assert torch.equal(a, b), float((a.float() - b.float()).abs().max())
     if T >= 256:  # the rows the fused epilogue did not own are untouched
         assert (outs[0][0][:, T + off:] == 7.0).all() and (outs[0][1][:, T + off:] == 7.0).all()
+
+
+@pytest.mark.parametrize("case", ["geglu_4416", "geglu_300", "plain_qkv", "resid_oproj", "sig_fc1_gelu_aux",
+                                  "sig_fc2_ktail_resid", "sig_out_tail_bias_resid", "plain_edge_rows_cols"])
+def test_persistent_8phase_bit_identical_to_one_shot(case, monkeypatch):
+    """gemm8q_kernel (persistent 8-phase: one workgroup per CU walking tiles + split-tail K-pieces as one
+    K-step stream, epilogue stores straight from the accumulators) against the one-shot gemm8p_kernel
+    (PZ_GEMM_PERSIST=0): the same per-tile K order, so every output (C, saved aux) is bit-identical --
+    GeGLU, plain, residual, GELU + bias + saved pre-activation, a K % 64 tail, split-tail shapes and
+    partial edge tiles.  Both are also checked against torch fp32."""
+    from pizero_native import ops
+
+    M, N, K, kw = {
+        "geglu_4416": (4416, 2 * 4096, 2048, dict(geglu=True)),
+        "geglu_300": (300, 2 * 16384, 2048, dict(geglu=True)),
+        "plain_qkv": (4416, 2560, 2048, {}),
+        "resid_oproj": (17664, 2048, 2048, dict(resid=True)),
+        "sig_fc1_gelu_aux": (16384, 4304, 1152, dict(bias=True, gelu=True)),
+        "sig_fc2_ktail_resid": (16384, 1152, 4304, dict(bias=True, resid=True)),
+        "sig_out_tail_bias_resid": (16384, 1152, 1152, dict(bias=True, resid=True)),
+        "plain_edge_rows_cols": (2000, 1000, 1024, {}),
+    }[case]
+    x, W = bf(M, K), bf(N, K, scale=K ** -0.5)
+    b = bf(N) if kw.get("bias") else None
+    r = bf(M, N) if kw.get("resid") else None
+    name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU if kw.get("geglu") else
+                                (ops.PZ_EPI_GELU if kw.get("gelu") else ops.PZ_EPI_NONE), geglu_inter=N // 2)
+    assert name.startswith("gemm8p_kernel"), name  # an 8-phase shape (the persistent kernel replaces it)
+
+    def run():
+        if kw.get("geglu"):
+            out = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
+            aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, out, epi=ops.PZ_EPI_GEGLU, aux=aux)
+            return out, aux
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if kw.get("gelu") else None
+        ops.linear(x, W, out, bias=b, resid=r, epi=ops.PZ_EPI_GELU if kw.get("gelu") else ops.PZ_EPI_NONE, aux=aux)
+        return out, aux
+
+    monkeypatch.setenv("PZ_GEMM_PERSIST", "0")
+    o1, a1 = run()
+    monkeypatch.setenv("PZ_GEMM_PERSIST", "1")
+    o2, a2 = run()
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2), float((o1.float() - o2.float()).abs().max())
+    if a1 is not None:
+        assert torch.equal(a1, a2), float((a1.float() - a2.float()).abs().max())
+    rows = slice(0, min(M, 512))  # fp32 reference on a row slice
+    pre = x[rows].float() @ W.float().t()
+    if kw.get("geglu"):
+        g, u = pre[:, : N // 2], pre[:, N // 2:]
+        close(o2[rows], torch.nn.functional.gelu(g, approximate="tanh") * u, rtol=3e-2, atol=3e-2)
+    else:
+        if b is not None:
+            pre = pre + b.float()
+        ref = torch.nn.functional.gelu(pre, approximate="tanh") if kw.get("gelu") else pre
+        if r is not None:
+            ref = ref + r[rows].float()
+        close(o2[rows], ref, rtol=3e-2, atol=3e-2)

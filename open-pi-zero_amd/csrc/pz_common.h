@@ -103,9 +103,12 @@ void pz_set_error(const char* fmt, ...);
 // RoPE rotation of one pair (utils.py:4-16: x*cos + rotate_half(x)*sin) with every product rounded
 // separately (no FMA contraction): every kernel that applies RoPE (qkv_rope_split, the GEMV and the 8-phase
 // GEMM epilogues) produces the same bits from the same bf16 inputs
+// (__fmul_rn / __fadd_rn alone do not stop hipcc's default -ffp-contract=fast from fusing a product into
+// the add after inlining, differently per call site: contraction is switched off for this scope)
 __device__ __forceinline__ void rope_pair(float x1, float x2, float co, float si, float& o1, float& o2) {
-  o1 = __fsub_rn(__fmul_rn(x1, co), __fmul_rn(x2, si));
-  o2 = __fadd_rn(__fmul_rn(x2, co), __fmul_rn(x1, si));
+#pragma clang fp contract(off)
+  o1 = x1 * co - x2 * si;
+  o2 = x2 * co + x1 * si;
 }
 
 

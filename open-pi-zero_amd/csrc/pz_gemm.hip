@@ -1226,6 +1226,28 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
   }
   const int g4 = 4 * (lane >> 4), rl = lane & 15;
   if (GEGLU) {
+    if (p.dbg == 4 && m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {  // measurement: direct 8-B stores
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb) {
+        const int64_t m = m0 + wr * 128 + rb * 16 + rl;
+        bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n0 + wc * 32 + g4;
+        bf16_t* Xr = p.aux + m * p.ld_aux + n0 + wc * 32 + g4;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float gg[4], uu[4], hh[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gg[r] = acc[rb][j][r] * p.alpha;
+            uu[r] = acc[rb][2 + j][r] * p.alpha;
+            hh[r] = gelu_tanh(gg[r]) * uu[r];
+          }
+          *reinterpret_cast<u32x2*>(Cr + j * 16) = pk4(hh);
+          *reinterpret_cast<u32x2*>(Xr + j * 16) = pk4(gg);
+          *reinterpret_cast<u32x2*>(Xr + p.geglu_I + j * 16) = pk4(uu);
+        }
+      }
+      return;
+    }
     if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
       // pass 1: h (smem) -> C and g (smem + 64 KiB) -> aux[:, :I]; pass 2: u (smem) -> aux[:, I:]
 #pragma unroll
@@ -1666,33 +1688,47 @@ __global__ void __launch_bounds__(NT2, 1) gemm8q_kernel(GemmP p) {
   bool has_nxt = has_nxt0;
   int cur_start = 0, cur_end = cur.nk;  // global K-steps [cur_start, cur_end) belong to cur
 
-  // LDS-DMA of one piece (0 = A region 0, 1 = B region 0, 2 = B region 1, 3 = A region 1) of global
-  // K-step `step` (which belongs to cur or, from cur_end on, to nxt)
-  auto issue = [&](int piece, int step) {
-    const bool in_cur = step < cur_end;
-    const int64_t row0 = in_cur ? (piece == 0 || piece == 3 ? cur.m0 : cur.n0) : (piece == 0 || piece == 3 ? nxt.m0 : nxt.n0);
-    const int kt = in_cur ? cur.kt0 + (step - cur_start) : nxt.kt0 + (step - cur_end);
-    char* dst = smem + (step & 1) * P8_BUF + lds_off[piece] + wave * 1024;
+  // LDS-DMA sources: per piece (0 = A region 0, 1 = B region 0, 2 = B region 1, 3 = A region 1) the two
+  // per-thread pointers of the unit whose first global K-step is pbase[piece] (its kt0 folded in).  A piece
+  // switches to the next unit the first time it is issued for a K-step of that unit (A region 1 one K-step
+  // before the others), so the K loop does one 64-bit add per DMA, like the one-shot kernel.
+  const bf16_t* src[4][2];
+  int pbase[4], plast[4];  // plast: global K-step of the reduction's last (K % 64) tile in that unit, or -1
+  auto set_src = [&](int piece, const Unit8& u, int base) {
     const bool isA = piece == 0 || piece == 3;
     const int region = (piece == 3 || piece == 2) ? 1 : 0;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       int64_t g;
       if (isA) {
-        g = row0 + i * 128 + region * 64 + trow;
+        g = u.m0 + i * 128 + region * 64 + trow;
         g = g < p.M ? g : p.M - 1;
       } else if (GEGLU) {
         const int v = region * 128 + i * 64 + trow;
-        g = row0 + (v >> 6) * 32 + (v & 31);
+        g = u.n0 + (v >> 6) * 32 + (v & 31);
         g = g < p.geglu_I ? g : p.geglu_I - 1;
         if ((v >> 5) & 1) g += p.geglu_I;
       } else {
-        g = row0 + region * 128 + i * 64 + trow;
+        g = u.n0 + region * 128 + i * 64 + trow;
         g = g < p.N ? g : p.N - 1;
       }
-      const bf16_t* src = (isA ? p.A + g * p.lda : p.B + g * p.ldb) + colofs + (int64_t)kt * 64;
-      if (KTAIL && krem < 64 && kt == nk_all - 1 && colofs >= krem) src -= colofs - (krem - 8);
-      glds16(src, dst + i * 8192);
+      src[piece][i] = (isA ? p.A + g * p.lda : p.B + g * p.ldb) + colofs + (int64_t)u.kt0 * 64;
+    }
+    pbase[piece] = base;
+    plast[piece] = (KTAIL && u.kt0 + u.nk == nk_all) ? base + u.nk - 1 : -1;
+  };
+#pragma unroll
+  for (int q = 0; q < 4; ++q) set_src(q, cur, 0);
+  // LDS-DMA of one piece of global K-step `step` (cur's, or from cur_end on nxt's)
+  auto issue = [&](int piece, int step) {
+    if (step >= cur_end && pbase[piece] != cur_end) set_src(piece, nxt, cur_end);
+    const int64_t off = (int64_t)(step - pbase[piece]) * 64;
+    char* dst = smem + (step & 1) * P8_BUF + lds_off[piece] + wave * 1024;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const bf16_t* g = src[piece][i] + off;
+      if (KTAIL && krem < 64 && step == plast[piece] && colofs >= krem) g -= colofs - (krem - 8);
+      glds16(g, dst + i * 8192);
     }
   };
 
@@ -1845,11 +1881,31 @@ __global__ void __launch_bounds__(NT2, 1) gemm8q_kernel(GemmP p) {
         if (cur.m0 + BT <= p.M && cur.n0 + BT <= p.N) {
           epi8p_fast<FM>(p, 0, 0, m, nb, acc);
           adj = 32;
-        } else {
+        } else {  // edge tile (FM_STORE: alpha * acc + bias), bounds-checked stores
+          float bias[4][4];
 #pragma unroll
-          for (int rb = 0; rb < 8; ++rb)
+          for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
-            for (int cb = 0; cb < 4; ++cb) store_out4_rt(p, 0, 0, m + rb * 16, nb + cb * 16, acc[rb][cb]);
+            for (int r = 0; r < 4; ++r) bias[cb][r] = (p.bias && nb + cb * 16 + r < p.N) ? bf2f(p.bias[nb + cb * 16 + r]) : 0.f;
+#pragma unroll
+          for (int rb = 0; rb < 8; ++rb) {
+            if (m + rb * 16 >= p.M) continue;
+            bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + (m + rb * 16) * p.ldc;
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) {
+              const int64_t n = nb + cb * 16;
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[cb][r];
+              if (n + 4 <= p.N) {
+                *reinterpret_cast<u32x2*>(Cr + n) = pk4(v);
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (n + r < p.N) Cr[n + r] = f2bf(v[r]);
+              }
+            }
+          }
         }
       }
     }
@@ -2900,10 +2956,15 @@ static void launch_tail(const GemmP& p, int T, hipStream_t st) {
 // persistent 8-phase kernel (gemm8q_kernel) for k-contiguous A and B: batch 1, no fused RoPE epilogue
 // (its LDS staging), every work unit >= 2 K-steps; PZ_GEMM_PERSIST=0 keeps the one-shot kernel (A/B)
 static bool use_persist(const GemmP& p, int64_t batch, bool geglu) {
+  // opt-in (PZ_GEMM_PERSIST=1): measured SLOWER than the one-shot kernel on every Pi0 NT shape (vlm GeGLU
+  // 2.57 vs 2.12-2.19 ms, its main loop alone 1.83 vs 1.61 ms), kept for A/B runs
   const char* e = getenv("PZ_GEMM_PERSIST");
-  if (e && e[0] == '0') return false;
+  if (!(e && e[0] == '1')) return false;
   if (batch != 1 || p.rcs) return false;
-  if (!geglu && fast_mode(p) != FM_STORE && fast_mode(p) != FM_BF16) return false;
+  // GeGLU and plain / bias-only outputs: the residual / activation epilogues (FM_BF16) round the Linear
+  // output to bf16 first (the reference's Linear -> add order, epi8p_staged) and load side inputs, so they
+  // keep the one-shot kernel
+  if (!geglu && fast_mode(p) != FM_STORE) return false;
   const int nk = (int)((p.K + 63) / 64);
   if (nk < 2) return false;
   if (p.tail_s && nk - (p.tail_s - 1) * p.tail_kt < 2) return false;  // a 1-step last K-piece
@@ -2936,9 +2997,7 @@ static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
   if constexpr (AKC && BKC) {
     if (use_persist(p, batch, GEGLU)) {
-      if (GEGLU) return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
-      if (fast_mode(p) == FM_STORE) return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
-      return launch8q<GEGLU, KTAIL, FM_BF16>(p, st);
+      return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
     }
   }
   const bool kh = use_khalf(AKC, BKC);

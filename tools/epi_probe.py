@@ -44,7 +44,7 @@ def main():
             kname = ops.gemm_kernel_name(M, N, K, epi=epi)
         res = {}
         for tail in ("1", "0"):
-            for dbg in ("0", "1", "2", "3"):
+            for dbg in ("0", "1", "2", "3", "4"):
                 os.environ["PZ_GEMM_TAIL"] = tail
                 os.environ["PZ_GEMM_DBG"] = dbg
                 for _ in range(3):
@@ -64,7 +64,8 @@ def main():
               f"{res[('1', '1')]:.3f} ms ({tf(res[('1', '1')]):.0f}) | no tail {res[('0', '0')]:.3f} ms "
               f"({tf(res[('0', '0')]):.0f}) | no tail, no stores {res[('0', '1')]:.3f} ms ({tf(res[('0', '1')]):.0f})\n"
               f"   first round desynchronised (s_sleep 0..7 x 4.5 us / x 9 us): {res[('1', '2')]:.3f} / "
-              f"{res[('1', '3')]:.3f} ms; no tail {res[('0', '2')]:.3f} / {res[('0', '3')]:.3f} ms", flush=True)
+              f"{res[('1', '3')]:.3f} ms; no tail {res[('0', '2')]:.3f} / {res[('0', '3')]:.3f} ms\n"
+              f"   GeGLU epilogue with direct 8-B stores (no LDS staging): {res[('1', '4')]:.3f} ms", flush=True)
 
     case("geglu", 17664, 32768, 2048, geglu=True)
     case("plainNT", 17664, 32768, 2048)

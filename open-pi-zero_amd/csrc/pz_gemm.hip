@@ -3199,9 +3199,10 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
 extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->x && a->W && a->pos && a->cs && a->k_out && a->v_out && a->M > 0 && a->K > 0,
                "gemm_qkv_rope: bad args");
-  PZ_CHECK_ARG(a->hd == BT && a->nh >= 1 && a->q_out && a->N == (a->nh + 2) * a->hd && a->T > 0 && a->M % a->T == 0 &&
-                   !a->norm_w,
-               "gemm_qkv_rope: head_dim 256, N = (nh + 2) * 256, q_out set, M %% T == 0, no fused norm");
+  PZ_CHECK_ARG(a->nh >= 1 && a->N == (a->nh + 2) * a->hd && a->T > 0 && a->M % a->T == 0,
+               "gemm_qkv_rope: N = (nh + 2) * hd, M %% T == 0");
+  // one 256-column tile per head, Q written, no fused norm: otherwise not this kernel (no error text)
+  if (a->hd != BT || !a->q_out || a->norm_w) return PZ_ERR_UNSUPPORTED;
   PZ_CHECK_ARG(PZ_ALIGNED(a->x, 16) && PZ_ALIGNED(a->W, 16) && a->ldx % 8 == 0 && a->ldw % 8 == 0 && a->K % 8 == 0 &&
                    PZ_ALIGNED(a->q_out, 16) && PZ_ALIGNED(a->k_out, 16) && PZ_ALIGNED(a->v_out, 16),
                "gemm_qkv_rope: 16-byte alignment");

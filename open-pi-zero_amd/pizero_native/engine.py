@@ -194,7 +194,7 @@ class Engine:
         self.split_dact = os.environ.get("PZ_SPLIT_DACT", "1") == "1"
         # q|k|v GEMM with the RoPE + Q/K/V scatter in its epilogue (pz_gemm_qkv_rope) where the 8-phase kernel
         # runs; PZ_FUSE_QKV_ROPE=0: GEMM + pz_qkv_rope_split (A/B, bit-identical)
-        self.fuse_qkv_rope = os.environ.get("PZ_FUSE_QKV_ROPE", "1") == "1"
+        self.fuse_qkv_rope = os.environ.get("PZ_FUSE_QKV_ROPE", "1") == "1" and self.d.hd == 256
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
         self.f8_version = None

@@ -65,6 +65,8 @@ struct GemmP {
   const float* rcs;
   bf16_t *rq, *rk, *rv;
   int64_t rT, rnh, rLq, rqoff, rLk, rkoff;
+  // 8-phase LDS-staged epilogues: non-temporal (streaming) 16-B output stores (PZ_GEMM_NT, read per call)
+  int nt_store;
 };
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -1045,12 +1047,17 @@ __device__ __forceinline__ void img_put(char* img, int row, int col, u32x2 v) {
   const int ch = col >> 3;
   *reinterpret_cast<u32x2*>(img + row * 256 + ((ch ^ (row & 15)) << 4) + ((col >> 2) & 1) * 8) = v;
 }
-__device__ __forceinline__ void img_flush(const char* img, bf16_t* dst, int64_t ld) {
+// 16-B output store; nt: non-temporal (streaming) cache policy (PZ_GEMM_NT=1, A/B)
+__device__ __forceinline__ void st16(bf16_t* dst, const u32x4& v, bool nt) {
+  if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+  else *reinterpret_cast<u32x4*>(dst) = v;
+}
+__device__ __forceinline__ void img_flush(const char* img, bf16_t* dst, int64_t ld, bool nt = false) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int c = threadIdx.x + i * NT2, row = c >> 4, ch = c & 15;
     const u32x4 v = *reinterpret_cast<const u32x4*>(img + row * 256 + ((ch ^ (row & 15)) << 4));
-    *reinterpret_cast<u32x4*>(dst + row * ld + ch * 8) = v;
+    st16(dst + row * ld + ch * 8, v, nt);
   }
 }
 __device__ __forceinline__ void lds_sync() {
@@ -1145,21 +1152,21 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
           dg[e] = v[e] * x1[e] * gelu_tanh_grad(x0[e]);
           du[e] = v[e] * gelu_tanh(x0[e]);
         }
-        *reinterpret_cast<u32x4*>(Cp) = pack8v(dg);
-        *reinterpret_cast<u32x4*>(Cp + p.geglu_I) = pack8v(du);
+        st16(Cp, pack8v(dg), p.nt_store);
+        st16(Cp + p.geglu_I, pack8v(du), p.nt_store);
       } else if (FM == FM_DACT) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] *= gelu ? gelu_tanh_grad(x0[e]) : silu_grad(x0[e]);
-        *reinterpret_cast<u32x4*>(Cp) = pack8v(v);
+        st16(Cp, pack8v(v), p.nt_store);
       } else {
         if (act) {
-          if (p.aux) *reinterpret_cast<u32x4*>(p.aux + (m0 + row) * p.ld_aux + n0 + col) = iv[i];
+          if (p.aux) st16(p.aux + (m0 + row) * p.ld_aux + n0 + col, iv[i], p.nt_store);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu ? gelu_tanh(v[e]) : silu(v[e]);
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += x1[e] + x0[e];  // resid, old C (zeros when absent)
-        *reinterpret_cast<u32x4*>(Cp) = pack8v(v);
+        st16(Cp, pack8v(v), p.nt_store);
       }
     }
   }
@@ -1265,8 +1272,8 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
           img_put(smem + 65536, row, col, u32x2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])});
         }
       lds_sync();
-      img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc);
-      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux);
+      img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc, p.nt_store);
+      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_store);
       lds_sync();
 #pragma unroll
       for (int rb = 0; rb < 8; ++rb)
@@ -1279,7 +1286,7 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
                   u32x2{pack2bf(uu[0], uu[1]), pack2bf(uu[2], uu[3])});
         }
       lds_sync();
-      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux);
+      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux, p.nt_store);
       return;
     }
 #pragma unroll
@@ -1316,8 +1323,8 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
           }
         lds_sync();
         bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0;
-        img_flush(smem, C, p.ldc);
-        img_flush(smem + 65536, C + 128, p.ldc);
+        img_flush(smem, C, p.ldc, p.nt_store);
+        img_flush(smem + 65536, C + 128, p.ldc, p.nt_store);
         break;
       }
       case FM_F32: epi8p_fast<FM_F32>(p, cofs, rofs, m, nb, acc); break;
@@ -3112,6 +3119,8 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   {
     const char* e = getenv("PZ_GEMM_DBG");
     p.dbg = e ? atoi(e) : 0;
+    e = getenv("PZ_GEMM_NT");
+    p.nt_store = e ? atoi(e) : 0;
   }
   hipStream_t st = (hipStream_t)stream;
 

@@ -24,6 +24,7 @@ current stream).  Layout decisions (MI355X-first):
 
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 import weakref
@@ -195,6 +196,10 @@ class Engine:
         # q|k|v GEMM with the RoPE + Q/K/V scatter in its epilogue (pz_gemm_qkv_rope) where the 8-phase kernel
         # runs; PZ_FUSE_QKV_ROPE=0: GEMM + pz_qkv_rope_split (A/B, bit-identical)
         self.fuse_qkv_rope = os.environ.get("PZ_FUSE_QKV_ROPE", "1") == "1" and self.d.hd == 256
+        # backward of the action-expert group (M = B*(C+H) = 320 rows: latency-bound GEMMs) on a second HIP
+        # stream, concurrent with the vlm group's (PZ_EXPERT_STREAM=0: one stream, A/B)
+        self.expert_stream = os.environ.get("PZ_EXPERT_STREAM", "1") == "1"
+        self._side = {}
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
         self.f8_version = None
@@ -334,6 +339,24 @@ class Engine:
                 out.append(Group("action", mp + "action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI,
                                  d.a_theta, False, "action"))
         return out
+
+    # ------------------------------------------------------- second stream --
+    def _side_stream(self, dev):
+        st = self._side.get(dev)
+        if st is None:
+            st = self._side[dev] = torch.cuda.Stream(device=dev)
+        return st
+
+    @staticmethod
+    def _on(side, g):
+        """Context of one group's work: the action-expert group on the side stream with its own GEMM scratch
+        (ops.workspace_slot), the vlm group on the current stream."""
+        if side is None or g.name == "vlm":
+            return contextlib.nullcontext()
+        stack = contextlib.ExitStack()
+        stack.enter_context(torch.cuda.stream(side))
+        stack.enter_context(ops.workspace_slot(1))
+        return stack
 
     # ================================================================ SigLIP ==
     def siglip_forward(self, pix, save):
@@ -672,12 +695,96 @@ class Engine:
         save["joint"] = layers
         return X
 
+    def _mlp_oproj_backward(self, g, gs, p, dX, dO, dXm, beta, rpp, nh, hd, dev):
+        """One group's GeGLU MLP + post-attention RMSNorm + o_proj backward of a joint layer
+        (paligemma/modules.py:86-95, mixture.py:216-242): dX[g] -> dO[g] (the attention output gradient)
+        and dXm[g] (the residual gradient into the input RMSNorm backward)."""
+        dx = dX[g.name]
+        M = dx.shape[0]
+        part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
+        # MLP
+        # dgrad through down_proj with the GeGLU derivative fused into its epilogue:
+        # gu (saved g|u) <- d(gate|up) in place; hm (saved GeGLU output) feeds the down_proj wgrad
+        gu = gs["gu"]
+        if self.split_dact:  # plain dgrad GEMM, then the HBM-bound GeGLU backward in place on gu
+            dh = torch.empty(M, g.inter, device=dev, dtype=BF16)
+            ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dh)
+            ops.geglu_bwd(dh, gu, gu, None, M, g.inter)
+            del dh
+        else:
+            ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), gu, epi=PZ_EPI_DGEGLU, aux=gu)
+        if self.rg(p + "mlp.down_proj.weight"):
+            ops.linear_wgrad(dx, gs["hm"], self.gw(p + "mlp.down_proj.weight"), beta=beta)
+        gs["hm"] = None
+        if self.rg(p + "mlp.gate_proj.weight") and self.rg(p + "mlp.up_proj.weight"):
+            ops.linear_wgrad(gu, gs["h2"], self.ar.grad_span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"),
+                             beta=beta)
+        dh2 = torch.empty(M, g.hid, device=dev, dtype=BF16)
+        ops.linear_dgrad(gu, self.gu_w(p), dh2)
+        dxm = torch.empty_like(dx)
+        ops.rmsnorm_bwd(dh2, gs["xm"], self.w(p + "post_attention_layernorm.weight"), gs["r2"], dxm, dres=dx,
+                        dw_part=part)
+        self._norm_grads(p + "post_attention_layernorm.", part, None, beta)
+        # o_proj
+        if self.rg(p + "self_attn.o_proj.weight"):
+            ops.linear_wgrad(dxm, gs["O"], self.gw(p + "self_attn.o_proj.weight"), beta=beta)
+        o = torch.empty(M, nh * hd, device=dev, dtype=BF16)
+        ops.linear_dgrad(dxm, self.w(p + "self_attn.o_proj.weight"), o)
+        dO[g.name] = o
+        dXm[g.name] = dxm
+
+    def _qkv_backward(self, g, gs, p, dQ, dK, dV, dX, dXm, pos, B, L, Lp, beta, rpp, nh, hd, dev):
+        """One group's q|k|v projection + input RMSNorm backward of a joint layer (mixture.py:162-215,
+        joint_model.py:170-257 + inverse RoPE): dQ / dK / dV rows of the group -> dX[g]."""
+        x = gs["x"]
+        M = x.shape[0]
+        W = (nh + 2) * hd
+        dqkv = torch.empty(M, W, device=dev, dtype=BF16)
+        ops.qkv_rope_split_bwd(None if gs.get("skip") else dQ, dK, dV, pos[g.pos_key], self.rope(g.theta), dqkv,
+                               B, g.T, nh, 1, hd, L, g.off, Lp, g.off)
+        names = [p + f"self_attn.{k}_proj.weight" for k in "qkv"]
+        rgs = [self.rg(n) for n in names]
+        if all(rgs):
+            ops.linear_wgrad(dqkv, gs["h"], self.ar.grad_span(names[0], names[2]), beta=beta)
+        elif rgs[0] and rgs[1]:  # e.g. last-layer vlm v_proj frozen (pizero.py:231)
+            ops.linear_wgrad(dqkv[:, : (nh + 1) * hd], gs["h"], self.ar.grad_span(names[0], names[1]), beta=beta)
+        else:
+            for n, rgk, c0, c1 in zip(names, rgs, (0, nh * hd, (nh + 1) * hd), (nh * hd, (nh + 1) * hd, W)):
+                if rgk:
+                    ops.linear_wgrad(dqkv[:, c0:c1], gs["h"], self.gw(n), beta=beta)
+        dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
+        ops.linear_dgrad(dqkv, self.qkv_w(p), dh)
+        part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
+        dxn = torch.empty(M, g.hid, device=dev, dtype=BF16)
+        ops.rmsnorm_bwd(dh, x, self.w(p + "input_layernorm.weight"), gs["r"], dxn, dres=dXm.get(g.name),
+                        dw_part=part)
+        self._norm_grads(p + "input_layernorm.", part, None, beta)
+        dX[g.name] = dxn
+
     def _joint_layers_backward(self, groups, dX, pos, cnt, B, sv, beta):
         d = self.d
         L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
         dev = next(v for v in dX.values() if v is not None).device
         delta = dP = dS = None
         rpp = ops.rows_per_part()
+        # the non-vlm group (action expert, 320 rows at micro-batch 64) runs its MLP / o_proj / q|k|v backward
+        # on a second stream while the vlm group's run on the main stream; they meet at the joint attention
+        # backward (events both ways).  Tensors one stream allocated and the other reads are record_stream'ed,
+        # so the caching allocator never hands their memory out while the other stream may still read it.
+        main = torch.cuda.current_stream(dev)
+        side = None
+        if self.expert_stream and len(groups) > 1 and dev.type == "cuda":
+            side = self._side_stream(dev)
+            side.wait_stream(main)
+            for st in sv["joint"]:
+                for g in groups:
+                    if g.name != "vlm":
+                        for t in st["g"][g.name].values():
+                            if isinstance(t, torch.Tensor):
+                                t.record_stream(side)
+            for t in dX.values():
+                if t is not None:
+                    t.record_stream(side)
         for l in reversed(range(d.nL)):
             st = sv["joint"][l]
             dQ = torch.empty(B, L, nh * hd, device=dev, dtype=BF16)
@@ -692,39 +799,12 @@ class Engine:
                 if gs.get("skip"):
                     any_skip = True
                     continue
-                dx = dX[g.name]
-                M = dx.shape[0]
-                part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
-                # MLP
-                # dgrad through down_proj with the GeGLU derivative fused into its epilogue:
-                # gu (saved g|u) <- d(gate|up) in place; hm (saved GeGLU output) feeds the down_proj wgrad
-                gu = gs["gu"]
-                if self.split_dact:  # plain dgrad GEMM, then the HBM-bound GeGLU backward in place on gu
-                    dh = torch.empty(M, g.inter, device=dev, dtype=BF16)
-                    ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dh)
-                    ops.geglu_bwd(dh, gu, gu, None, M, g.inter)
-                    del dh
-                else:
-                    ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), gu, epi=PZ_EPI_DGEGLU, aux=gu)
-                if self.rg(p + "mlp.down_proj.weight"):
-                    ops.linear_wgrad(dx, gs["hm"], self.gw(p + "mlp.down_proj.weight"), beta=beta)
-                gs["hm"] = None
-                if self.rg(p + "mlp.gate_proj.weight") and self.rg(p + "mlp.up_proj.weight"):
-                    ops.linear_wgrad(gu, gs["h2"], self.ar.grad_span(p + "mlp.gate_proj.weight", p + "mlp.up_proj.weight"),
-                                     beta=beta)
-                dh2 = torch.empty(M, g.hid, device=dev, dtype=BF16)
-                ops.linear_dgrad(gu, self.gu_w(p), dh2)
-                dxm = torch.empty_like(dx)
-                ops.rmsnorm_bwd(dh2, gs["xm"], self.w(p + "post_attention_layernorm.weight"), gs["r2"], dxm, dres=dx,
-                                dw_part=part)
-                self._norm_grads(p + "post_attention_layernorm.", part, None, beta)
-                # o_proj
-                if self.rg(p + "self_attn.o_proj.weight"):
-                    ops.linear_wgrad(dxm, gs["O"], self.gw(p + "self_attn.o_proj.weight"), beta=beta)
-                o = torch.empty(M, nh * hd, device=dev, dtype=BF16)
-                ops.linear_dgrad(dxm, self.w(p + "self_attn.o_proj.weight"), o)
-                dO[g.name] = o
-                dXm[g.name] = dxm
+                with self._on(side, g):
+                    self._mlp_oproj_backward(g, gs, p, dX, dO, dXm, beta, rpp, nh, hd, dev)
+                if side is not None and g.name != "vlm":
+                    dO[g.name].record_stream(main)
+            if side is not None:
+                main.wait_stream(side)  # the expert dO for the joint attention backward
             if "lse" in st:
                 # fused attention backward (skipped mixtures' outputs reach nothing: dO = 0)
                 for g in groups:
@@ -774,34 +854,22 @@ class Engine:
                     first = False
                 if first:
                     dV.zero_()
+            if side is not None:  # dQ / dK / dV of the joint attention backward feed the expert's q|k|v backward
+                side.wait_stream(main)
+                for t in (dQ, dK, dV):
+                    t.record_stream(side)
             for g in groups:
-                gs = st["g"][g.name]
-                p = f"{g.prefix}{l}."
-                x = gs["x"]
-                M = x.shape[0]
-                W = (nh + 2) * hd
-                dqkv = torch.empty(M, W, device=dev, dtype=BF16)
-                ops.qkv_rope_split_bwd(None if gs.get("skip") else dQ, dK, dV, pos[g.pos_key], self.rope(g.theta), dqkv,
-                                       B, g.T, nh, 1, hd, L, g.off, Lp, g.off)
-                names = [p + f"self_attn.{k}_proj.weight" for k in "qkv"]
-                rgs = [self.rg(n) for n in names]
-                if all(rgs):
-                    ops.linear_wgrad(dqkv, gs["h"], self.ar.grad_span(names[0], names[2]), beta=beta)
-                elif rgs[0] and rgs[1]:  # e.g. last-layer vlm v_proj frozen (pizero.py:231)
-                    ops.linear_wgrad(dqkv[:, : (nh + 1) * hd], gs["h"], self.ar.grad_span(names[0], names[1]), beta=beta)
-                else:
-                    for n, rgk, c0, c1 in zip(names, rgs, (0, nh * hd, (nh + 1) * hd), (nh * hd, (nh + 1) * hd, W)):
-                        if rgk:
-                            ops.linear_wgrad(dqkv[:, c0:c1], gs["h"], self.gw(n), beta=beta)
-                dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
-                ops.linear_dgrad(dqkv, self.qkv_w(p), dh)
-                part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
-                dxn = torch.empty(M, g.hid, device=dev, dtype=BF16)
-                ops.rmsnorm_bwd(dh, x, self.w(p + "input_layernorm.weight"), gs["r"], dxn, dres=dXm.get(g.name),
-                                dw_part=part)
-                self._norm_grads(p + "input_layernorm.", part, None, beta)
-                dX[g.name] = dxn
+                with self._on(side, g):
+                    self._qkv_backward(g, st["g"][g.name], f"{g.prefix}{l}.", dQ, dK, dV, dX, dXm, pos, B, L, Lp, beta,
+                                       rpp, nh, hd, dev)
+            if side is not None and self.hook is not None:
+                main.wait_stream(side)  # DDP buckets are reduced from the main stream: the layer's expert grads first
             self._notify("joint", l)
+        if side is not None:
+            main.wait_stream(side)
+            for t in dX.values():
+                if t is not None:
+                    t.record_stream(main)
         sv.pop("_jkv_token", None)  # the joint K/V buffers are free for the next forward
         return dX
 

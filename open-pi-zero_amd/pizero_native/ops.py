@@ -77,14 +77,34 @@ _WS_BYTES = 64 << 20
 _WS = {}
 
 
+_WS_SLOT = [0]
+
+
+class workspace_slot:
+    """``with workspace_slot(1):`` -- GEMMs enqueued inside use their own split-K / split-tail scratch (the
+    engine's second stream for the action-expert group runs GEMMs concurrently with the main stream's)."""
+
+    def __init__(self, slot):
+        self.slot, self.prev = slot, None
+
+    def __enter__(self):
+        self.prev = _WS_SLOT[0]
+        _WS_SLOT[0] = self.slot
+
+    def __exit__(self, *exc):
+        _WS_SLOT[0] = self.prev
+
+
 def workspace(device=None):
     """Per-device fp32 split-K scratch for pz_gemm (allocated once, before any graph capture
-    reuses it; GEMMs are stream-ordered on the main stream, so one buffer is enough)."""
+    reuses it; GEMMs are stream-ordered within a stream, so one buffer per stream slot is enough:
+    slot 0 = the main stream, slot 1 = the engine's action-expert stream)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    ws = _WS.get(dev)
+    key = (dev, _WS_SLOT[0])
+    ws = _WS.get(key)
     if ws is None:
         ws = torch.empty(_WS_BYTES // 4, dtype=torch.float32, device=dev)
-        _WS[dev] = ws
+        _WS[key] = ws
     return ws
 
 

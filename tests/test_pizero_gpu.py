@@ -344,3 +344,26 @@ def test_interleaved_forwards_keep_their_saved_state(tiny):
     (la + lb).backward()
     torch.cuda.synchronize()
     torch.testing.assert_close(m.action_decoder.weight.grad.float(), ga + gb, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("which", ["full", "b16"])
+def test_expert_stream_backward_bitwise(which, request):
+    """The action-expert group's backward on its own HIP stream (Engine.expert_stream, events and
+    record_stream at the joint attention) gives the SAME gradient arena bits as the single-stream
+    backward (every kernel is deterministic; only the interleaving changes)."""
+    if which == "full":
+        d, g, m, gi = request.getfixturevalue("full")
+    else:
+        d, g, m = request.getfixturevalue("b16")
+        gi = gpu_inputs(m, d, 16)
+    eng = m._engine()
+    prev = eng.expert_stream
+    try:
+        eng.expert_stream = False
+        run_loss(m, gi)
+        ref = m._arena.grad.clone()
+        eng.expert_stream = True
+        run_loss(m, gi)
+        assert torch.equal(m._arena.grad, ref), float((m._arena.grad.float() - ref.float()).abs().max())
+    finally:
+        eng.expert_stream = prev

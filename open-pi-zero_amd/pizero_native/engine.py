@@ -606,6 +606,51 @@ class Engine:
         self._jkv_holder = weakref.ref(tok)
         return kv
 
+    def _pre_attn_train(self, g, l, X, pos, st, Qj, Kj, Vj, dev):
+        """One group's input RMSNorm + q|k|v projection + RoPE + joint Q / K / V scatter of joint layer l
+        (paligemma/modules.py:7-21, mixture.py:162-215, joint_model.py:170-257)."""
+        d = self.d
+        L, Lp, nh, hd = d.L, d.Lp, d.nh, d.hd
+        B = Qj.shape[0]
+        p = f"{g.prefix}{l}."
+        x = X[g.name]
+        M = x.shape[0]
+        h = torch.empty_like(x)
+        r = torch.empty(M, device=dev, dtype=F32)
+        ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, r, d.rms_eps)
+        # q|k|v projection + RoPE + joint scatter: one 8-phase GEMM whose epilogue rotates and writes
+        # Q / K / V (N1: no [M, 2560] qkv tensor, no split launch); rows too few for the 8-phase
+        # kernel (the action expert's 320) take GEMM + qkv_rope_split (same bits)
+        if not (self.fuse_qkv_rope and ops.gemm_qkv_rope(h, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta),
+                                                         Qj, Kj, Vj, g.T, nh, hd, L, g.off, Lp, g.off)):
+            W = (nh + 2) * hd
+            qkv = torch.empty(M, W, device=dev, dtype=BF16)
+            ops.linear(h, self.qkv_w(p), qkv)
+            ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L,
+                               g.off, Lp, g.off)
+        st["g"][g.name] = {"x": x, "h": h, "r": r}
+
+    def _post_attn_train(self, g, l, X, gs, Os, dev):
+        """One group's o_proj (+ residual), post-attention RMSNorm and GeGLU MLP (+ residual) of joint layer l
+        (mixture.py:216-242, paligemma/modules.py:86-95), activations saved in gs for the backward."""
+        d = self.d
+        p = f"{g.prefix}{l}."
+        x = X[g.name]
+        M = x.shape[0]
+        O = Os[g.name]
+        xm = torch.empty_like(x)
+        ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
+        h2 = torch.empty_like(x)
+        r2 = torch.empty(M, device=dev, dtype=F32)
+        ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, r2, d.rms_eps)
+        gu = torch.empty(M, 2 * g.inter, device=dev, dtype=BF16)
+        hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
+        ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU, aux=gu)
+        xn = torch.empty_like(x)
+        ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
+        gs.update(O=O, xm=xm, h2=h2, r2=r2, gu=gu, hm=hm, skip=False)
+        X[g.name] = xn
+
     def _joint_layers_train(self, groups, X, pos, cnt, B, save):
         """joint_model.py:24-304 x nL for the training pass (all mixtures active)."""
         d = self.d
@@ -614,29 +659,28 @@ class Engine:
         S = None
         layers = []
         Kall, Vall = self._joint_kv(B, Lp, dev, save)
+        # the action-expert group's pre- and post-attention work on the second stream, concurrent with the vlm
+        # group's; the streams meet at the joint attention (as in _joint_layers_backward)
+        main = torch.cuda.current_stream(dev)
+        side = None
+        if self.expert_stream and len(groups) > 1 and dev.type == "cuda":
+            side = self._side_stream(dev)
+            side.wait_stream(main)
+            for t in X.values():
+                if t is not None:
+                    t.record_stream(side)
         for l in range(d.nL):
             last = l == d.nL - 1
             Qj = torch.empty(B, L, nh * hd, device=dev, dtype=BF16)
+            if side is not None:
+                Qj.record_stream(side)
             Kj, Vj = Kall[l], Vall[l]
             st = {"Q": Qj, "K": Kj, "V": Vj, "g": {}}
             for g in groups:
-                p = f"{g.prefix}{l}."
-                x = X[g.name]
-                M = x.shape[0]
-                h = torch.empty_like(x)
-                r = torch.empty(M, device=dev, dtype=F32)
-                ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, r, d.rms_eps)
-                # q|k|v projection + RoPE + joint scatter: one 8-phase GEMM whose epilogue rotates and writes
-                # Q / K / V (N1: no [M, 2560] qkv tensor, no split launch); rows too few for the 8-phase
-                # kernel (the action expert's 320) take GEMM + qkv_rope_split (same bits)
-                if not (self.fuse_qkv_rope and ops.gemm_qkv_rope(h, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta),
-                                                                 Qj, Kj, Vj, g.T, nh, hd, L, g.off, Lp, g.off)):
-                    W = (nh + 2) * hd
-                    qkv = torch.empty(M, W, device=dev, dtype=BF16)
-                    ops.linear(h, self.qkv_w(p), qkv)
-                    ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Qj, Kj, Vj, B, g.T, nh, 1, hd, L,
-                                       g.off, Lp, g.off)
-                st["g"][g.name] = {"x": x, "h": h, "r": r}
+                with self._on(side, g):
+                    self._pre_attn_train(g, l, X, pos, st, Qj, Kj, Vj, dev)
+            if side is not None:
+                main.wait_stream(side)  # every group's Q / K / V rows before the joint attention
             Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
             if self.joint_flash and not isinstance(cnt, GeneralMask):
                 # fused joint attention (joint_model.py:259-292): soft-cap, block mask from cnt, O rows
@@ -669,29 +713,30 @@ class Engine:
                         ops.gemm(g.T * nh, hd, Lp, Pm[:, g.off * nh:], Lp, True, Vj, hd, False, Os[g.name], hd, batch=B,
                                  sA=(L * nh * Lp, 0), sB=(Lp * hd, 0), sC=(g.T * nh * hd, 0))
                 st["O"] = Os
+            if side is not None:
+                side.wait_stream(main)  # the attention outputs
+                for t in Os.values():
+                    t.record_stream(side)
             for g in groups:
                 gs = st["g"][g.name]
-                p = f"{g.prefix}{l}."
-                x = X[g.name]
-                M = x.shape[0]
                 if last and g.skip_last:
                     X[g.name] = None
                     gs["skip"] = True
                     continue
-                O = Os[g.name]
-                xm = torch.empty_like(x)
-                ops.linear(O, self.w(p + "self_attn.o_proj.weight"), xm, resid=x)
-                h2 = torch.empty_like(x)
-                r2 = torch.empty(M, device=dev, dtype=F32)
-                ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, r2, d.rms_eps)
-                gu = torch.empty(M, 2 * g.inter, device=dev, dtype=BF16)
-                hm = torch.empty(M, g.inter, device=dev, dtype=BF16)
-                ops.linear(h2, self.gu_w(p), hm, epi=PZ_EPI_GEGLU, aux=gu)
-                xn = torch.empty_like(x)
-                ops.linear(hm, self.w(p + "mlp.down_proj.weight"), xn, resid=xm)
-                gs.update(O=O, xm=xm, h2=h2, r2=r2, gu=gu, hm=hm, skip=False)
-                X[g.name] = xn
+                with self._on(side, g):
+                    self._post_attn_train(g, l, X, gs, Os, dev)
             layers.append(st)
+        if side is not None:  # the expert output and its saved activations are read on the main stream later
+            main.wait_stream(side)
+            for t in X.values():
+                if t is not None:
+                    t.record_stream(main)
+            for st in layers:
+                for g in groups:
+                    if g.name != "vlm":
+                        for t in st["g"][g.name].values():
+                            if isinstance(t, torch.Tensor):
+                                t.record_stream(main)
         save["joint"] = layers
         return X
 

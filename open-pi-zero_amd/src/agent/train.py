@@ -200,10 +200,14 @@ class TrainAgent:
                 self.cnt_update += 1
                 if self.cnt_update % self.save_model_freq == 0 or self.cnt_update == self.n_updates:
                     self.save_training(self.cnt_update, self.cnt_batch)
-            if self.multi_gpu:
-                torch.distributed.all_reduce(loss, op=torch.distributed.ReduceOp.SUM)
-                loss = loss / self.world
             if self.cnt_batch % self.log_freq == 0:
+                # the rank-mean of this micro-batch's loss, as the reference logs it (train.py:381-384) -- but
+                # all-reduced only on the batches that are logged (every rank has the same cnt_batch, so all
+                # of them enter the collective), not once per micro-batch
+                if self.multi_gpu:
+                    loss = loss.detach().clone()
+                    torch.distributed.all_reduce(loss, op=torch.distributed.ReduceOp.SUM)
+                    loss = loss / self.world
                 loss_deque.append(loss.item())
                 if self.main_rank:
                     log.info("Batch %d Update %d: loss %.4f | action lr %.8f", self.cnt_batch, self.cnt_update,

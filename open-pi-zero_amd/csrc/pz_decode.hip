@@ -227,6 +227,167 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
   *out = f2bf(l > 0.f ? o / l : 0.f);
 }
 
+// ---- one-workgroup decode attention (C4 / text decode: few row tiles) --------------------------------
+// grid (B * rtiles), 256 threads: workgroup = (sample b, 32-row tile) walks EVERY 32-key chunk with an online
+// softmax and writes O itself -- no partials, no merge launch.  Per chunk: S^T = K Q^T on the MFMA (K straight
+// from global), soft-cap + block mask, online (m, l) per row, P (bf16) into LDS, and O^T += V^T P^T on the MFMA
+// with V staged in LDS as a [key][256-dim] image read transposed (ds_read_b64_tr_b16); the next chunk's K
+// fragments and V rows are loaded while the current chunk is processed.
+__device__ __forceinline__ int da_sw(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
+
+// A fragment of the MFMA from the k-strided [32 key][256 dim] V image: rows (dims) 16 * dt .. + 15, k = keys
+// 8 (lane >> 4) .. + 7 (the transposed-read layout of pz_gemm.hip's k-strided operands)
+__device__ __forceinline__ bf16x8 da_vfrag(const char* img, int dt, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  s16x8 out;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = 8 * (lane >> 4) + 4 * t + q;
+    const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) s16x4*)(img + k * 512 + (((4 * dt + p) ^ da_sw(k)) << 3)));
+    out[4 * t + 0] = v[0];
+    out[4 * t + 1] = v[1];
+    out[4 * t + 2] = v[2];
+    out[4 * t + 3] = v[3];
+  }
+  return __builtin_bit_cast(bf16x8, out);
+}
+
+__global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
+  __shared__ float S[DA_R][DA_KC + 1];
+  __shared__ __attribute__((aligned(16))) bf16_t Pm[DA_R][DA_KC + 8];  // bf16 probabilities [row][key]
+  __shared__ __attribute__((aligned(16))) char Vimg[DA_KC * 512];       // one chunk of V, transposed reads
+  __shared__ float alpha_s[DA_R];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
+  const int rtiles = (R + DA_R - 1) / DA_R;
+  const int b = blockIdx.x / rtiles, rt = blockIdx.x % rtiles, r0 = rt * DA_R;
+  const bool masked = a.cnt != nullptr;
+  const int cnt = masked ? a.cnt[b] : nk;
+  const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
+  const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
+  const int nchunks = (nk + DA_KC - 1) / DA_KC;
+  const int g = lane >> 4;
+  // S^T tile of this wave: key tile kt (16 keys) x row block rb (16 rows)
+  const int kt = wave & 1, rb = wave >> 1;
+  const int row = r0 + rb * 16 + (lane & 15);
+  const bool rok = row < R;
+  const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
+  const int qt = (int)a.qtok0 + t;
+  bf16x8 qf[8];
+  {
+    const bf16_t* qp = (const bf16_t*)a.q + ((int64_t)b * a.Lq + a.qoff + t) * a.ldq + (int64_t)h * DA_HD + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 8; ++dc) qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
+  }
+  // V staging: thread = 4 (key, 16-B dim chunk) pairs of the 32 x 32 chunks
+  auto load_k = [&](int c, bf16x8 (&kf)[8]) {
+    const int key = min(c * DA_KC + kt * 16 + (lane & 15), nk - 1);
+    const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
+#pragma unroll
+    for (int dc = 0; dc < 8; ++dc) kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
+  };
+  auto load_v = [&](int c, u32x4 (&vv)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + i * 256, kr = e >> 5, ch = e & 31;
+      vv[i] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(c * DA_KC + kr, nk - 1) * DA_HD + 8 * ch);
+    }
+  };
+  const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
+  f32x4 acc[4][2];  // O^T tiles: dim tile 4 * wave + i, row tile j (lane: dims 4 (lane >> 4) .. + 3, row lane & 15)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;  // threads < 32: row threadIdx.x
+  bf16x8 kf[8], kn[8];
+  u32x4 vv[4], vn[4];
+  load_k(0, kf);
+  load_v(0, vv);
+  for (int c = 0; c < nchunks; ++c) {
+    const int j0 = c * DA_KC;
+    // V(c) -> LDS image (the previous chunk's P.V reads ended at the loop-closing barrier)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = threadIdx.x + i * 256, kr = e >> 5, ch = e & 31;
+      *reinterpret_cast<u32x4*>(Vimg + kr * 512 + (((2 * ch) ^ da_sw(kr)) << 3)) = vv[i];
+    }
+    {  // S^T tile
+      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int dc = 0; dc < 8; ++dc) s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], s, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int kl = kt * 16 + 4 * g + e;
+        float x = s[e] * a.scale;
+        if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
+        const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
+        S[row - r0][kl] = ok ? x : -INFINITY;
+      }
+    }
+    if (c + 1 < nchunks) {  // next chunk's K fragments and V rows in flight during this chunk's softmax / P.V
+      load_k(c + 1, kn);
+      load_v(c + 1, vn);
+    }
+    __syncthreads();
+    if (threadIdx.x < DA_R) {  // online softmax of row threadIdx.x
+      const int r = threadIdx.x;
+      float m = m_run;
+#pragma unroll
+      for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
+      const float al = m_run == -INFINITY ? 0.f : __expf(m_run - m);
+      float l = 0.f;
+#pragma unroll
+      for (int k = 0; k < DA_KC; k += 2) {
+        const float p0 = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
+        const float p1 = m == -INFINITY ? 0.f : __expf(S[r][k + 1] - m);
+        l += p0 + p1;
+        *reinterpret_cast<unsigned*>(&Pm[r][k]) = pack2bf(p0, p1);
+      }
+      l_run = l_run * al + l;
+      m_run = m;
+      alpha_s[r] = al;
+    }
+    __syncthreads();
+    {  // O^T += V^T P^T (rows rescaled by alpha first)
+      bf16x8 pb[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) pb[j] = *reinterpret_cast<const bf16x8*>(&Pm[j * 16 + (lane & 15)][8 * g]);
+      const float al0 = alpha_s[lane & 15], al1 = alpha_s[16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bf16x8 vf = da_vfrag(Vimg, 4 * wave + i, lane);
+        acc[i][0] *= al0;
+        acc[i][1] *= al1;
+        acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[0], acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pb[1], acc[i][1], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int dc = 0; dc < 8; ++dc) kf[dc] = kn[dc];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) vv[i] = vn[i];
+    __syncthreads();  // S, P, alpha and the V image are rewritten by the next chunk
+  }
+  if (threadIdx.x < DA_R) alpha_s[threadIdx.x] = l_run > 0.f ? 1.f / l_run : 0.f;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rr = r0 + j * 16 + (lane & 15);
+    if (rr >= R) continue;
+    const float il = alpha_s[j * 16 + (lane & 15)];
+    const int tt = rr / nh, hh = rr % nh;
+    bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int d0 = (4 * wave + i) * 16 + 4 * g;
+      *reinterpret_cast<u32x2*>(out + d0) =
+          u32x2{pack2bf(acc[i][j][0] * il, acc[i][j][1] * il), pack2bf(acc[i][j][2] * il, acc[i][j][3] * il)};
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int64_t pz_decode_attn_ws_bytes(int64_t B, int64_t rows, int64_t nk) {
@@ -246,6 +407,17 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
   PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
+  // one workgroup per (sample, row tile) walking every key chunk (no merge launch) when that grid is small
+  // (C4 at B=1: one workgroup, 9 chunks); PZ_DECODE_ONE = 0 | 1 forces the split / one-workgroup path (A/B)
+  {
+    const char* e1 = getenv("PZ_DECODE_ONE");
+    const bool one = e1 ? e1[0] == '1' : (a->B * rtiles <= 16 && nchunks <= 16);
+    if (one && PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0) {
+      hipLaunchKernelGGL(decode_attn_one, dim3((unsigned)(a->B * rtiles)), dim3(256), 0, st, *a);
+      PZ_CHECK_LAUNCH();
+      return PZ_OK;
+    }
+  }
   // chunks per workgroup: one (C4: 9 workgroups) until the (chunk, row tile) grid passes 256 workgroups,
   // then groups of nch chunks (fewer partial rows for the merge)
   const int64_t wg1 = (int64_t)nchunks * a->B * rtiles;

@@ -227,7 +227,7 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
   *out = f2bf(l > 0.f ? o / l : 0.f);
 }
 
-// ---- one-workgroup decode attention (C4 / text decode: few row tiles) --------------------------------
+// ---- one-workgroup decode attention (opt-in A/B: PZ_DECODE_ONE=1; measured slower for C4) ---------------
 // grid (B * rtiles), 256 threads: workgroup = (sample b, 32-row tile) walks EVERY 32-key chunk with an online
 // softmax and writes O itself -- no partials, no merge launch.  Per chunk: S^T = K Q^T on the MFMA (K straight
 // from global), soft-cap + block mask, online (m, l) per row, P (bf16) into LDS, and O^T += V^T P^T on the MFMA
@@ -407,11 +407,12 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
   PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
-  // one workgroup per (sample, row tile) walking every key chunk (no merge launch) when that grid is small
-  // (C4 at B=1: one workgroup, 9 chunks); PZ_DECODE_ONE = 0 | 1 forces the split / one-workgroup path (A/B)
+  // one workgroup per (sample, row tile) walking every key chunk (no merge launch): opt-in, PZ_DECODE_ONE=1 --
+  // measured SLOWER for C4 (chunk 16.2 vs 13.8 ms: its per-chunk S -> softmax -> P.V chain is latency-bound
+  // in one workgroup, ~2.9 us per 32 keys, while the split kernel runs the 9 chunks on 9 CUs at once)
   {
     const char* e1 = getenv("PZ_DECODE_ONE");
-    const bool one = e1 ? e1[0] == '1' : (a->B * rtiles <= 16 && nchunks <= 16);
+    const bool one = e1 && e1[0] == '1';
     if (one && PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0) {
       hipLaunchKernelGGL(decode_attn_one, dim3((unsigned)(a->B * rtiles)), dim3(256), 0, st, *a);
       PZ_CHECK_LAUNCH();

@@ -691,9 +691,9 @@ def test_time_embed_modes_match_reference():
 def test_decode_attn_matches_reference(B, T, cnts, P, one, monkeypatch):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
     with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
-    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  one = "1": the
-    one-workgroup kernel (every key chunk in one workgroup, MFMA P.V, no merge launch; C4's default),
-    "0": the key-split kernel + fixed-order merge"""
+    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  one = "0": the
+    key-split kernel + fixed-order merge (default); "1": the opt-in one-workgroup kernel (every key chunk
+    in one workgroup, MFMA P.V, no merge launch)"""
     from pizero_native import ops
 
     monkeypatch.setenv("PZ_DECODE_ONE", one)

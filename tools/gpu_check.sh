@@ -36,6 +36,11 @@ PY
     infprof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/infprof" -o infer \
         -- python3 tools/infer_bench.py --iters 20 > "$OUT/infprof.log" 2>&1 ;;
+    c5prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5prof" -o c5 \
+        -- python3 tools/c5_bench.py --iters 20 > "$OUT/c5prof.log" 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     flashbench)
       timeout -k 10 300 python -u tools/flash_bench.py > "$OUT/flash_bench.log" 2>&1 ;;
     gemmbench)

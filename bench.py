@@ -65,9 +65,9 @@ def synthetic_batch(model, B, device, gen):
 
 def pmc_traffic(kname, shape):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (profiles/r02/pmc_dominant.json, tools/pmc_dominant.sh + tools/pmc_summary.py): FETCH_SIZE x2
+    (profiles/r03/pmc_dominant.json, tools/pmc_dominant.sh + tools/pmc_summary.py): FETCH_SIZE x2
     (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another kernel/shape."""
-    path = os.path.join(ROOT, "profiles", "r02", "pmc_dominant.json")
+    path = os.path.join(ROOT, "profiles", "r03", "pmc_dominant.json")
     try:
         with open(path) as f:
             pm = json.load(f)
@@ -76,7 +76,7 @@ def pmc_traffic(kname, shape):
     if not kname.startswith(pm.get("kernel", "?")) or list(pm.get("shape_MNK", [])) != list(shape):
         return {"traffic": None}
     return {"traffic": pm["traffic_bytes"], "traffic_unit": "bytes/launch",
-            "traffic_algorithmic": pm["algorithmic_bytes"], "traffic_source": "profiles/r02/pmc_dominant.json"}
+            "traffic_algorithmic": pm["algorithmic_bytes"], "traffic_source": "profiles/r03/pmc_dominant.json"}
 
 
 def cpu_baseline(seconds_budget=25.0):

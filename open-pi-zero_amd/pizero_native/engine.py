@@ -199,6 +199,10 @@ class Engine:
         # backward of the action-expert group (M = B*(C+H) = 320 rows: latency-bound GEMMs) on a second HIP
         # stream, concurrent with the vlm group's (PZ_EXPERT_STREAM=0: one stream, A/B)
         self.expert_stream = os.environ.get("PZ_EXPERT_STREAM", "1") == "1"
+        # ... and in the forward (PZ_EXPERT_STREAM_FWD=1): measured no faster than backward-only (bench 238.9 vs
+        # 239.3 samples/s), and its expert GEMMs then share the CUs with the vlm GeGLU GEMM (the dominant
+        # kernel: live roofline 2.32 vs 2.19 ms per launch), so off by default
+        self.expert_stream_fwd = os.environ.get("PZ_EXPERT_STREAM_FWD", "0") == "1"
         self._side = {}
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
@@ -663,7 +667,7 @@ class Engine:
         # group's; the streams meet at the joint attention (as in _joint_layers_backward)
         main = torch.cuda.current_stream(dev)
         side = None
-        if self.expert_stream and len(groups) > 1 and dev.type == "cuda":
+        if self.expert_stream and self.expert_stream_fwd and len(groups) > 1 and dev.type == "cuda":
             side = self._side_stream(dev)
             side.wait_stream(main)
             for t in X.values():

@@ -357,13 +357,14 @@ def test_expert_stream_backward_bitwise(which, request):
         d, g, m = request.getfixturevalue("b16")
         gi = gpu_inputs(m, d, 16)
     eng = m._engine()
-    prev = eng.expert_stream
+    prev = eng.expert_stream, eng.expert_stream_fwd
     try:
         eng.expert_stream = False
         run_loss(m, gi)
         ref = m._arena.grad.clone()
-        eng.expert_stream = True
-        run_loss(m, gi)
-        assert torch.equal(m._arena.grad, ref), float((m._arena.grad.float() - ref.float()).abs().max())
+        for fwd in (False, True):  # backward-only (default) and forward + backward on the second stream
+            eng.expert_stream, eng.expert_stream_fwd = True, fwd
+            run_loss(m, gi)
+            assert torch.equal(m._arena.grad, ref), (fwd, float((m._arena.grad.float() - ref.float()).abs().max()))
     finally:
-        eng.expert_stream = prev
+        eng.expert_stream, eng.expert_stream_fwd = prev

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 14
+#define PZ_ABI_VERSION 15
 
 enum {
   PZ_OK = 0,
@@ -355,6 +355,10 @@ int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float o
  * (the sqrt(hidden) embedding scaling of joint_model.py:348-355 for proprio/action rows) */
 int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t dld, int64_t dbs, int64_t B,
                  int64_t rows, int64_t D, float scale, int32_t beta, void* stream);
+/* read [p, p + bytes) once into the caches (MALL / L2) and discard it: the inference engine warms the next
+ * action-expert layer's weights on a side stream while the current layer's latency-bound GEMV chain runs
+ * (replaces nothing in the reference: the weight reads of pizero.py:461-481's denoise Linears) */
+int pz_prefetch(const void* p, int64_t bytes, int32_t workgroups, void* stream);
 /* bf16 <-> fp32 copies / scaled adds */
 int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);

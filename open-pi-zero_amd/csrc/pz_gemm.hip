@@ -22,52 +22,13 @@
 
 #include <type_traits>
 
-#include "pz_common.h"
+#include "pz_gemm_epi.h"
 
 namespace {
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile image in LDS
 
-struct GemmP {
-  const bf16_t* A;
-  const bf16_t* B;
-  void* C;
-  const bf16_t* bias;
-  const bf16_t* resid;
-  bf16_t* aux;
-  int64_t M, N, K, lda, ldb, ldc, ld_resid, ld_aux, geglu_I;
-  int64_t batch_inner, sAo, sAi, sBo, sBi, sCo, sCi, sRo, sRi;
-  int tiles_m, tiles_n, epi, c_fp32, beta;
-  float alpha;
-  // split-K (batch-1 only): blockIdx.y = split index; raw fp32 partials -> ws[z][M][ldw]
-  float* ws;
-  int64_t ksplit, ldw;
-  // batched 128-tile launches (gemm_kernel, batch % 8 == 0, no split-K): 1-D grid, the tiles of one batch
-  // entry on one XCD so its operand panels are shared in that XCD's L2 (batch_xcd = number of batch entries)
-  int batch_xcd;
-  // 8-phase split tail (batch-1 only, tail_s > 0): work units [0, dp_tiles) are whole tiles; unit
-  // dp_tiles + u is K-piece (u % tail_s) (tail_kt K-tiles) of tile dp_tiles + u / tail_s, whose raw
-  // accumulators go to ws[u] (256 KiB, thread-major) for gemm8p_tail_epilogue.
-  int dp_tiles, tail_s, tail_kt;
-  // fused Gemma RMSNorm of the A rows (skinny path only): bf16 (1 + w) weights [K] or NULL
-  const bf16_t* nw;
-  float neps;
-  // fp8 W8A8 (gemm8p_f8_kernel): per-row activation scales [M] or NULL
-  const float* rs;
-  // measurement knob (PZ_GEMM_DBG, read per call): 1 = the 8-phase kernels skip their epilogue stores
-  // (tools/epi_probe.py: main-loop time alone); 0 in every product run
-  int dbg;
-  // fused q|k|v RoPE epilogue (pz_gemm_qkv_rope; 8-phase kernel, head_dim 256 = one column tile per head):
-  // the bf16-rounded projection of head n0/256 is rotated at rpos[m] (table rcs) and scattered into the
-  // joint Q / K / V buffers like pz_qkv_rope_split; C is not written.  rcs == NULL: off.
-  const int64_t* rpos;
-  const float* rcs;
-  bf16_t *rq, *rk, *rv;
-  int64_t rT, rnh, rLq, rqoff, rLk, rkoff;
-  // 8-phase LDS-staged epilogues: non-temporal (streaming) 16-B output stores (PZ_GEMM_NT, read per call)
-  int nt_store;
-};
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 // two bf16-shaped fragments (8 x 16 bit each = 16 fp8 codes) -> one 32-code f8f6f4 operand
@@ -154,286 +115,6 @@ __device__ __forceinline__ bf16x8 frag(const char* lds, int rb, int kk, int lane
   }
 }
 
-// bijective XCD-aware remap + grouped (super-row) tile order
-__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
-  const int xcd = bid & 7, local = bid >> 3;
-  const int q = nwg >> 3, r = nwg & 7;
-  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-  constexpr int GROUP = 8;
-  const int per_group = GROUP * tiles_n;
-  const int g = wg / per_group;
-  const int first_m = g * GROUP;
-  const int gsize = min(tiles_m - first_m, GROUP);
-  const int in = wg - g * per_group;
-  tm = first_m + in % gsize;
-  tn = in / gsize;
-}
-
-// ---- epilogue: one lane owns C[m][n..n+3] (swapped-operand MFMA layout) -------
-// Side inputs of the epilogue (residual, saved activations, old C for beta accumulation, bias) are
-// loaded by epi_load4 into raw registers and consumed by epi_store4.  Kernels that own many output
-// groups per lane issue the loads of the next groups before the stores of the current ones: the
-// pointers may alias C (resid == C, DGEGLU in place), so the compiler cannot hoist a load above an
-// earlier store by itself and would otherwise pay one memory round trip per 4-column group.
-struct Side {
-  u32x4 w;  // .xy: aux (DGELU/DSILU pre-activation, DGEGLU g) or old bf16 C (beta); .zw: resid or DGEGLU u
-            // (fp32 C with beta: all four lanes hold the old fp32 values)
-};
-
-__device__ __forceinline__ u32x2 ld4bf(const bf16_t* X, bool full, int64_t n, int64_t N) {
-  if (full) return *reinterpret_cast<const u32x2*>(X);
-  unsigned h[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) h[r] = n + r < N ? (unsigned)X[r] : 0u;
-  return u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-}
-__device__ __forceinline__ void unpack4(u32x2 w, float (&o)[4]) {
-  o[0] = __uint_as_float(w[0] << 16); o[1] = __uint_as_float(w[0] & 0xffff0000u);
-  o[2] = __uint_as_float(w[1] << 16); o[3] = __uint_as_float(w[1] & 0xffff0000u);
-}
-__device__ __forceinline__ void store4(bf16_t* X, bool full, int64_t n, int64_t N, const float (&v)[4]) {
-  if (full) {
-    *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < N) X[r] = f2bf(v[r]);
-  }
-}
-
-__device__ __forceinline__ u32x2 epi_load_bias(const GemmP& p, int64_t n) {
-  if (!p.bias || n >= p.N) return u32x2{0u, 0u};
-  return ld4bf(p.bias + n, n + 4 <= p.N, n, p.N);
-}
-
-// epilogue classes (compile-time, so each fully unrolled 8-phase epilogue carries one class's code)
-enum EpiMode { EM_BF16 = 0, EM_F32 = 1, EM_DACT = 2, EM_DGEGLU = 3 };
-
-template <int EM>
-__device__ __forceinline__ void epi_load4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                          Side& s) {
-  s.w = u32x4{0u, 0u, 0u, 0u};
-  if (m >= p.M || n >= p.N) return;
-  const bool full = n + 4 <= p.N;
-  if constexpr (EM == EM_DGEGLU) {
-    const bf16_t* X = p.aux + m * p.ld_aux + n;
-    const u32x2 g = ld4bf(X, full, n, p.N), u = ld4bf(X + p.geglu_I, full, n, p.N);
-    s.w = u32x4{g[0], g[1], u[0], u[1]};
-  } else if constexpr (EM == EM_DACT) {
-    const u32x2 x = ld4bf(p.aux + m * p.ld_aux + n, full, n, p.N);
-    s.w = u32x4{x[0], x[1], 0u, 0u};
-  } else if constexpr (EM == EM_F32) {
-    if (p.beta) {
-      const float* Cp = reinterpret_cast<const float*>(p.C) + cofs + m * p.ldc + n;
-      if (full) {
-        s.w = *reinterpret_cast<const u32x4*>(Cp);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) s.w[r] = n + r < p.N ? __float_as_uint(Cp[r]) : 0u;
-      }
-    } else if (p.resid) {
-      const u32x2 x = ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N);
-      s.w = u32x4{0u, 0u, x[0], x[1]};
-    }
-  } else {
-    u32x2 x0{0u, 0u}, x1{0u, 0u};
-    if (p.resid) x1 = ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N);
-    if (p.beta) x0 = ld4bf(reinterpret_cast<const bf16_t*>(p.C) + cofs + m * p.ldc + n, full, n, p.N);
-    s.w = u32x4{x0[0], x0[1], x1[0], x1[1]};
-  }
-}
-
-template <int EM>
-__device__ __forceinline__ void epi_store4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                           const f32x4& acc, const Side& s, u32x2 bias) {
-  if (m >= p.M || n >= p.N) return;
-  const bool full = n + 4 <= p.N;
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = acc[r] * p.alpha;
-  float x0[4], x1[4];
-  unpack4(u32x2{s.w[0], s.w[1]}, x0);
-  unpack4(u32x2{s.w[2], s.w[3]}, x1);
-  bf16_t* Cb = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-  if constexpr (EM == EM_DGEGLU) {  // GeGLU backward from saved [g | u]: two outputs, nothing else applies
-    float dg[4], du[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dg[r] = v[r] * x1[r] * gelu_tanh_grad(x0[r]);
-      du[r] = v[r] * gelu_tanh(x0[r]);
-    }
-    store4(Cb, full, n, p.N, dg);
-    store4(Cb + p.geglu_I, full, n, p.N, du);
-  } else if constexpr (EM == EM_DACT) {  // activation backward from the saved pre-activation
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= p.epi == PZ_EPI_DGELU ? gelu_tanh_grad(x0[r]) : silu_grad(x0[r]);
-    store4(Cb, full, n, p.N, v);
-  } else {
-    if (p.bias) {
-      float b[4];
-      unpack4(bias, b);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += b[r];
-    }
-    if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
-      if (p.aux) store4(p.aux + m * p.ld_aux + n, full, n, p.N, v);
-      if (p.epi == PZ_EPI_GELU) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_tanh(v[r]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = silu(v[r]);
-      }
-    }
-    if constexpr (EM == EM_F32) {
-      if (p.beta) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += __uint_as_float(s.w[r]);
-      } else if (p.resid) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += x1[r];
-      }
-      float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
-      if (full) {
-        *reinterpret_cast<f32x4*>(Cp) = f32x4{v[0], v[1], v[2], v[3]};
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (n + r < p.N) Cp[r] = v[r];
-      }
-    } else {
-      if (p.resid) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += x1[r];
-      }
-      if (p.beta) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += x0[r];
-      }
-      store4(Cb, full, n, p.N, v);
-    }
-  }
-}
-
-__device__ __forceinline__ int epi_mode(const GemmP& p) {
-  if (p.epi == PZ_EPI_DGEGLU) return EM_DGEGLU;
-  if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) return EM_DACT;
-  return p.c_fp32 ? EM_F32 : EM_BF16;
-}
-
-template <int EM>
-__device__ __forceinline__ void store_out4_m(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                             const f32x4& acc) {
-  Side s;
-  epi_load4<EM>(p, cofs, rofs, m, n, s);
-  epi_store4<EM>(p, cofs, rofs, m, n, acc, s, epi_load_bias(p, n));
-}
-
-// one group, runtime-general (edge tiles of the 8-phase kernel: one compact copy per group)
-__device__ __forceinline__ void store_out4_rt(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                              const f32x4& acc) {
-  if (m >= p.M || n >= p.N) return;
-  const bool full = n + 4 <= p.N;
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = acc[r] * p.alpha;
-  if (p.epi == PZ_EPI_DGEGLU) {
-    float g[4], u[4], dg[4], du[4];
-    const bf16_t* X = p.aux + m * p.ld_aux + n;
-    unpack4(ld4bf(X, full, n, p.N), g);
-    unpack4(ld4bf(X + p.geglu_I, full, n, p.N), u);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dg[r] = v[r] * u[r] * gelu_tanh_grad(g[r]);
-      du[r] = v[r] * gelu_tanh(g[r]);
-    }
-    bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-    store4(Cp, full, n, p.N, dg);
-    store4(Cp + p.geglu_I, full, n, p.N, du);
-    return;
-  }
-  if (p.epi == PZ_EPI_DGELU || p.epi == PZ_EPI_DSILU) {
-    float x[4];
-    unpack4(ld4bf(p.aux + m * p.ld_aux + n, full, n, p.N), x);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] *= p.epi == PZ_EPI_DGELU ? gelu_tanh_grad(x[r]) : silu_grad(x[r]);
-  }
-  if (p.bias) {
-    float b[4];
-    unpack4(ld4bf(p.bias + n, full, n, p.N), b);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += b[r];
-  }
-  if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
-    if (p.aux) store4(p.aux + m * p.ld_aux + n, full, n, p.N, v);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = p.epi == PZ_EPI_GELU ? gelu_tanh(v[r]) : silu(v[r]);
-  }
-  if (p.resid) {
-    float x[4];
-    unpack4(ld4bf(p.resid + rofs + m * p.ld_resid + n, full, n, p.N), x);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += x[r];
-  }
-  if (p.c_fp32) {
-    float* Cp = reinterpret_cast<float*>(p.C) + cofs + m * p.ldc + n;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (full || n + r < p.N) Cp[r] = p.beta ? Cp[r] + v[r] : v[r];
-  } else {
-    bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-    if (p.beta) {
-      float o[4];
-      unpack4(ld4bf(Cp, full, n, p.N), o);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += o[r];
-    }
-    store4(Cp, full, n, p.N, v);
-  }
-}
-
-// run f(std::integral_constant<int, EM>) for the epilogue class of p (one branch per launch, outside
-// the unrolled per-group loops)
-template <class F>
-__device__ __forceinline__ void epi_dispatch(const GemmP& p, F&& f) {
-  switch (epi_mode(p)) {
-    case EM_DGEGLU: f(std::integral_constant<int, EM_DGEGLU>{}); break;
-    case EM_DACT: f(std::integral_constant<int, EM_DACT>{}); break;
-    case EM_F32: f(std::integral_constant<int, EM_F32>{}); break;
-    default: f(std::integral_constant<int, EM_BF16>{}); break;
-  }
-}
-
-// one group, loads then stores (kernels with few groups per lane)
-__device__ __forceinline__ void store_out4(const GemmP& p, int64_t cofs, int64_t rofs, int64_t m, int64_t n,
-                                           const f32x4& acc) {
-  switch (epi_mode(p)) {
-    case EM_DGEGLU: store_out4_m<EM_DGEGLU>(p, cofs, rofs, m, n, acc); break;
-    case EM_DACT: store_out4_m<EM_DACT>(p, cofs, rofs, m, n, acc); break;
-    case EM_F32: store_out4_m<EM_F32>(p, cofs, rofs, m, n, acc); break;
-    default: store_out4_m<EM_BF16>(p, cofs, rofs, m, n, acc); break;
-  }
-}
-
-// GeGLU: gate and up accumulators of the same (m, n..n+3) -> h = gelu_tanh(g) * u (+ saved g|u)
-__device__ __forceinline__ void store_geglu4(const GemmP& p, int64_t cofs, int64_t m, int64_t n, const f32x4& ga,
-                                             const f32x4& ua) {
-  if (m >= p.M || n >= p.geglu_I) return;
-  float h[4], g[4], u[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    g[r] = ga[r] * p.alpha;
-    u[r] = ua[r] * p.alpha;
-    h[r] = gelu_tanh(g[r]) * u[r];
-  }
-  bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
-  *reinterpret_cast<u32x2*>(Cp) = u32x2{pack2bf(h[0], h[1]), pack2bf(h[2], h[3])};
-  if (p.aux) {
-    bf16_t* X = p.aux + m * p.ld_aux + n;
-    *reinterpret_cast<u32x2*>(X) = u32x2{pack2bf(g[0], g[1]), pack2bf(g[2], g[3])};
-    *reinterpret_cast<u32x2*>(X + p.geglu_I) = u32x2{pack2bf(u[0], u[1]), pack2bf(u[2], u[3])};
-  }
-}
 
 // TAG only separates kernel symbols (profiling): 1 = the Gemma-2B MLP gate|up GeGLU GEMM (M >= 2048 rows)
 template <bool AKC, bool BKC, int WM, int TAG>
@@ -1160,7 +841,7 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
         st16(Cp, pack8v(v), p.nt_store);
       } else {
         if (act) {
-          if (p.aux) st16(p.aux + (m0 + row) * p.ld_aux + n0 + col, iv[i], p.nt_store);
+          if (p.aux) st16(p.aux + (m0 + row) * p.ld_aux + n0 + col, iv[i], p.nt_aux);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = gelu ? gelu_tanh(v[e]) : silu(v[e]);
         }
@@ -1273,7 +954,7 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
         }
       lds_sync();
       img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc, p.nt_store);
-      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_store);
+      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_aux);
       lds_sync();
 #pragma unroll
       for (int rb = 0; rb < 8; ++rb)
@@ -1286,7 +967,7 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
                   u32x2{pack2bf(uu[0], uu[1]), pack2bf(uu[2], uu[3])});
         }
       lds_sync();
-      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux, p.nt_store);
+      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux, p.nt_aux);
       return;
     }
 #pragma unroll
@@ -2635,13 +2316,14 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64 };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
   int wm, tag, skinny_w, skinny_nc, skinny_mb, splits;
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
+  int rows_w, rows_tnb;           // row-slab kernel: waves, 16-column blocks per tile
 };
 
 // compute units of the current device (the "wave" of resident 8-phase workgroups: 1 per CU)
@@ -2683,6 +2365,38 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   pl.dp_tiles = (int)(q * G);
   pl.tail_s = (int)s;
   pl.tail_kt = (int)kt;
+}
+
+// row-slab kernel (64 < M <= PZ_ROWS_MAXM, default 512; k-contiguous A and B, batch 1, forward
+// epilogues): whole-K 64-row tiles, 16 / 32 / 64 columns wide so the tiles cover >= 128 workgroups;
+// 8 waves split K when it has >= 16 chunks (4 for GeGLU).  Taken where it measured faster than the
+// 128-tile + split-K pair or the 256-tile kernel (tools/rows_bench.py, profiles/r03/rows_bench.log):
+// K <= 2048 and <= 4096 output columns -- B = 1 SigLIP q|k|v 20.9 -> 12.0 us, o 14.6 -> 9.0 us, Gemma
+// q|k|v / o at 276 rows 19.8 -> 18.1 us, action expert (320 rows) q|k|v 17.5 -> 11.0, o 16.0 -> 13.4,
+// gate|up + GeGLU 32.9 -> 25.8 us; the long-K / wide ones (SigLIP fc1 / fc2, 4096-K down projections,
+// the 32768-wide Gemma gate|up) stay on the tile kernels.  PZ_GEMM_ROWS=0: never; =1: any 64 < M <= maxm
+// (A/B runs; read per call)
+bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
+  const char* er = getenv("PZ_GEMM_ROWS");
+  const char* em = getenv("PZ_ROWS_MAXM");
+  const int64_t maxm = em ? atoll(em) : 512;
+  if ((er && er[0] == '0') || a->M <= 64 || a->M > maxm || !pl.akc || !pl.bkc || a->batch != 1 ||
+      a->epilogue >= PZ_EPI_DGELU || a->norm_w)
+    return false;
+  if (!(er && er[0] == '1') && (a->K > 2048 || ncols > 4096)) return false;
+  const int64_t tm = (a->M + 63) / 64;
+  int tnb = pl.geglu ? 2 : 4;
+  while (tnb > 1 && tm * ((ncols + 16 * tnb - 1) / (16 * tnb)) < 128) tnb /= 2;
+  pl.kind = PATH_ROWS;
+  pl.rows_w = (a->K + 63) / 64 >= 16 && !pl.geglu ? 8 : 4;
+  const char* ew = getenv("PZ_ROWS_W");  // A/B overrides (read per call): waves 4 | 8, column blocks
+  if (ew && (atoi(ew) == 4 || atoi(ew) == 8)) pl.rows_w = atoi(ew);
+  const char* et = getenv("PZ_ROWS_TNB");
+  if (et && (atoi(et) == 1 || atoi(et) == 2 || (atoi(et) == 4 && !pl.geglu))) tnb = atoi(et);
+  pl.rows_tnb = tnb;
+  pl.tiles_m = tm;
+  pl.tiles_n = (ncols + 16 * tnb - 1) / (16 * tnb);
+  return true;
 }
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
@@ -2770,6 +2484,12 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
+  // the row-slab kernel before the 256-tile kernels (action-expert gate|up at 320 rows); PZ_ROWS_FIRST=1 for
+  // every shape it takes (A/B runs; read per call)
+  {
+    const char* ef = getenv("PZ_ROWS_FIRST");
+    if ((pl.geglu || (ef && ef[0] == '1')) && plan_rows(pl, a, ncols)) return pl;
+  }
   // rows from which the 256-tile kernels are tried: 256 for the GeGLU GEMM and long-K GEMMs (prefill
   // at B=1, 276 rows: 64 vs 78 us and 51 vs 56 us measured), 512 otherwise (narrow prefill GEMMs
   // are faster on 128-row tiles); PZ_GEMM_256_MINM overrides (A/B runs)
@@ -2787,6 +2507,7 @@ Plan make_plan(const pz_gemm_args* a) {
     const char* mu = getenv("PZ_GEMM_256_MINUNITS");  // A/B: workgroups the 256-tile path must reach
     if (units >= (mu ? atoll(mu) : 160)) return cand;
   }
+  if (plan_rows(pl, a, ncols)) return pl;
   pl.kind = PATH_TILE;
   pl.tiles_m = (a->M + BM - 1) / BM;
   pl.tiles_n = (ncols + (pl.geglu ? BN / 2 : BN) - 1) / (pl.geglu ? BN / 2 : BN);
@@ -2847,6 +2568,9 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
     case PATH_TILE:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
+      break;
+    case PATH_ROWS:
+      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, 4, %d, %s>", pl.rows_w, pl.rows_tnb, bstr(pl.geglu));
       break;
     case PATH_SPLIT:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
@@ -3121,6 +2845,8 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
     p.dbg = e ? atoi(e) : 0;
     e = getenv("PZ_GEMM_NT");
     p.nt_store = e ? atoi(e) : 0;
+    e = getenv("PZ_GEMM_NT_AUX");
+    p.nt_aux = p.nt_store || (e && atoi(e) != 0);
   }
   hipStream_t st = (hipStream_t)stream;
 
@@ -3160,6 +2886,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
+  if (pl.kind == PATH_ROWS) return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, pl.geglu, st);
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {
       p.ws = (float*)a->workspace;

@@ -429,6 +429,30 @@ extern "C" int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst
   return PZ_OK;
 }
 
+// Cache warm-up read (denoise weight prefetch): every thread reads 16-B chunks of [p, p + n16 * 16) in
+// strided order, 8 loads in flight, and keeps nothing -- the values are pinned live by an empty asm so the
+// loads are not removed; the bytes land in the MALL (and the reading XCD's L2) for the kernels that
+// stream them next.  Writes nothing.
+__global__ void __launch_bounds__(256) prefetch_kernel(const u32x4* __restrict__ p, int64_t n16) {
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += 8 * stride) {
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = i + u * stride < n16 ? p[i + u * stride] : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < 8; ++u) asm volatile("" ::"v"(v[u]));
+  }
+}
+
+extern "C" int pz_prefetch(const void* p, int64_t bytes, int32_t workgroups, void* stream) {
+  PZ_CHECK_ARG(p && bytes >= 0 && workgroups > 0 && PZ_ALIGNED(p, 16), "prefetch: bad args");
+  const int64_t n16 = bytes / 16;
+  if (n16 == 0) return PZ_OK;
+  hipLaunchKernelGGL(prefetch_kernel, dim3((unsigned)workgroups), dim3(256), 0, ST, (const u32x4*)p, n16);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
 extern "C" int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream) {
   PZ_CHECK_ARG(x && n > 0, "clamp: bad args");
   hipLaunchKernelGGL(clamp_kernel, dim3(nblk(n)), dim3(256), 0, ST, x, n, lo, hi);

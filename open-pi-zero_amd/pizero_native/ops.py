@@ -540,6 +540,11 @@ def copy_rows(src, sld, sbs, dst, dld, dbs, B, rows, D, scale=1.0, beta=False):
     call("pz_copy_rows", _p(src), sld, sbs, _p(dst), dld, dbs, B, rows, D, float(scale), int(beta), _st())
 
 
+def prefetch(t, workgroups=64):
+    """read the bytes of t once into the caches (pz_prefetch), on the current stream"""
+    call("pz_prefetch", _p(t), t.numel() * t.element_size(), int(workgroups), _st())
+
+
 def clamp_(x, lo, hi):
     call("pz_clamp", _p(x), x.numel(), float(lo), float(hi), _st())
 

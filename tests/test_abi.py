@@ -44,3 +44,19 @@ def test_error_path_without_gpu():
     rc = pizero_native.lib().pz_gemm(ctypes.byref(a), None)
     assert rc == 1
     assert b"bad dims" in pizero_native.lib().pz_last_error()
+
+
+def test_gemm_planner_routes_without_gpu():
+    """pz_gemm_kernel_name is host logic (no device needed): the row-slab kernel takes the measured-faster
+    64 < M <= 512 forward shapes (pz_gemm.hip plan_rows), the tile kernels keep the rest."""
+    from pizero_native import ops
+
+    geglu = ops.PZ_EPI_GEGLU
+    assert ops.gemm_kernel_name(256, 3456, 1152).startswith("gemm_rows_kernel<8, 4, 4")  # B=1 SigLIP q|k|v
+    assert ops.gemm_kernel_name(320, 8192, 1024, epi=geglu, geglu_inter=4096).startswith("gemm_rows_kernel<4")
+    assert not ops.gemm_kernel_name(256, 4304, 1152).startswith("gemm_rows")  # SigLIP fc1
+    assert not ops.gemm_kernel_name(256, 1152, 4304).startswith("gemm_rows")  # SigLIP fc2
+    assert not ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_rows")
+    assert not ops.gemm_kernel_name(64, 1024, 1024).startswith("gemm_rows")  # few-row paths keep M <= 64
+    assert not ops.gemm_kernel_name(17664, 2560, 2048).startswith("gemm_rows")  # training rows: 8-phase
+    assert not ops.gemm_kernel_name(320, 1024, 2048, a_kc=False).startswith("gemm_rows")  # k-strided A

@@ -271,10 +271,12 @@ def test_epilogues_gelu_resid_geglu_silu():
 
 
 @pytest.mark.parametrize("M,N,K", [(256, 1152, 4304), (276, 2048, 16384), (100, 300, 1024), (276, 2560, 2048)])
-def test_split_k_forward_epilogues(M, N, K):
+def test_split_k_forward_epilogues(M, N, K, monkeypatch):
     """Few-tile batch-1 GEMMs (B=1 prefill) run split-K + epilogue pass (or, long K, the 256-tile
-    kernel's K-pieces + tail epilogue); same results as one pass."""
+    kernel's K-pieces + tail epilogue) when the row-slab kernel is off; same results as one pass."""
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_GEMM_ROWS", "0")
 
     name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GELU)
     assert "splitk" in name or "tail" in name, name
@@ -296,6 +298,53 @@ def test_split_k_forward_epilogues(M, N, K):
         gu = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I)
         assert "splitk" in name or "tail" in name, name
+        ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+        raw = x.float() @ W.float().t()
+        close(gu, raw)
+        close(h, torch.nn.functional.gelu(raw[:, :I], approximate="tanh") * raw[:, I:])
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 3456, 1152), (256, 1152, 4304), (276, 2048, 2048), (320, 1024, 4096),
+                                   (100, 300, 1032), (512, 520, 200), (65, 2560, 1024)])
+@pytest.mark.parametrize("variant", ["auto", "w4", "w8", "tnb1", "tnb2", "tnb4"])
+def test_rows_kernel_forward_epilogues(M, N, K, variant, monkeypatch):
+    """Row-slab GEMM (64 < M <= 512, whole K per workgroup, no split-K pass): every forward epilogue, K tails
+    (K % 64 != 0), row / column edges, each wave count and tile width."""
+    from pizero_native import ops
+
+    monkeypatch.setenv("PZ_GEMM_ROWS", "1")  # every 64 < M <= 512 shape (default: K <= 2048, <= 4096 columns)
+    knob = {"w4": ("PZ_ROWS_W", "4"), "w8": ("PZ_ROWS_W", "8"), "tnb1": ("PZ_ROWS_TNB", "1"),
+            "tnb2": ("PZ_ROWS_TNB", "2"), "tnb4": ("PZ_ROWS_TNB", "4")}.get(variant)
+    if knob:
+        monkeypatch.setenv(*knob)
+    assert ops.gemm_kernel_name(M, N, K).startswith("gemm_rows_kernel"), ops.gemm_kernel_name(M, N, K)
+    x, W, b, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(N), bf(M, N)
+    ref = x.float() @ W.float().t() + b.float()
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, W, out, bias=b, resid=r)
+    close(out, ref + r.float(), atol=2e-2)
+    ops.linear(x, W, out, bias=b, epi=ops.PZ_EPI_GELU, aux=pre)
+    close(pre, ref)
+    close(out, torch.nn.functional.gelu(ref, approximate="tanh"))
+    ops.linear(x, W, out, bias=b, epi=ops.PZ_EPI_SILU)
+    close(out, torch.nn.functional.silu(ref))
+    out32 = torch.ones(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(M, N, K, x, K, True, W, K, True, out32, N, beta=True)
+    close(out32, 1.0 + x.float() @ W.float().t(), rtol=1e-3, atol=1e-3)
+    # row-strided views (ld > K / ld > N), as the engine passes them
+    xs = bf(M, K + 8)[:, :K]
+    xs.copy_(x)
+    outs = torch.empty(M, N + 4, device=dev, dtype=torch.bfloat16)[:, :N]
+    ops.linear(xs, W, outs, bias=b)
+    close(outs, ref)
+    I = N // 2 // 4 * 4
+    if I * 2 == N:
+        monkeypatch.setenv("PZ_ROWS_FIRST", "1")  # GeGLU shapes that the 256-tile path would otherwise take
+        name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I)
+        assert name.startswith("gemm_rows_kernel") and name.endswith("true>"), name
+        h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+        gu = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
         raw = x.float() @ W.float().t()
         close(gu, raw)

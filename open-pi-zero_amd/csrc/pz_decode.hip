@@ -14,6 +14,7 @@
 // The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of once per head.
 // Deterministic (no atomics).
 #include <stdlib.h>
+#include <string.h>
 
 #include "pz_common.h"
 
@@ -227,12 +228,14 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
   *out = f2bf(l > 0.f ? o / l : 0.f);
 }
 
-// ---- one-workgroup decode attention (opt-in A/B: PZ_DECODE_ONE=1; measured slower for C4) ---------------
-// grid (B * rtiles), 256 threads: workgroup = (sample b, 32-row tile) walks EVERY 32-key chunk with an online
-// softmax and writes O itself -- no partials, no merge launch.  Per chunk: S^T = K Q^T on the MFMA (K straight
-// from global), soft-cap + block mask, online (m, l) per row, P (bf16) into LDS, and O^T += V^T P^T on the MFMA
-// with V staged in LDS as a [key][256-dim] image read transposed (ds_read_b64_tr_b16); the next chunk's K
-// fragments and V rows are loaded while the current chunk is processed.
+// ---- MFMA decode attention (default): P.V on the matrix cores --------------------------------------------
+// grid (ngroups, B * rtiles), 256 threads: workgroup = (group of nch consecutive 32-key chunks, sample b, 32-row
+// tile) with an online softmax over its chunks; ngroups == 1 writes O itself (no merge launch), otherwise fp32
+// (O, m, l) partials in decode_attn_part's workspace layout for decode_attn_combine.  Per chunk: V(c) staged
+// into an LDS image read transposed (ds_read_b64_tr_b16), S^T = K Q^T on the MFMA (K fragments straight from
+// global), soft-cap + block mask into LDS, the softmax of each row by 8 lanes (4 keys each, shuffle max / sum,
+// online (m, l) kept in all 8 lanes), bf16 P, and O^T += V^T P^T on the MFMA (16 per chunk instead of the VALU
+// kernel's 1024 FMAs per thread); chunk c + 1's K fragments and V rows are loaded during chunk c.
 __device__ __forceinline__ int da_sw(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 2; }
 
 // A fragment of the MFMA from the k-strided [32 key][256 dim] V image: rows (dims) 16 * dt .. + 15, k = keys
@@ -253,20 +256,22 @@ __device__ __forceinline__ bf16x8 da_vfrag(const char* img, int dt, int lane) {
   return __builtin_bit_cast(bf16x8, out);
 }
 
-__global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
+__global__ void __launch_bounds__(256) decode_attn_mfma(pz_decode_attn_args a, int nch) {
   __shared__ float S[DA_R][DA_KC + 1];
   __shared__ __attribute__((aligned(16))) bf16_t Pm[DA_R][DA_KC + 8];  // bf16 probabilities [row][key]
   __shared__ __attribute__((aligned(16))) char Vimg[DA_KC * 512];       // one chunk of V, transposed reads
   __shared__ float alpha_s[DA_R];
+  __shared__ float ml_s[DA_R][2];  // final (m, l) per row
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
-  const int rtiles = (R + DA_R - 1) / DA_R;
-  const int b = blockIdx.x / rtiles, rt = blockIdx.x % rtiles, r0 = rt * DA_R;
+  const int rtiles = (R + DA_R - 1) / DA_R, Rpad = rtiles * DA_R;
+  const int grp = blockIdx.x, b = blockIdx.y / rtiles, rt = blockIdx.y % rtiles, r0 = rt * DA_R;
   const bool masked = a.cnt != nullptr;
   const int cnt = masked ? a.cnt[b] : nk;
   const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
   const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
   const int nchunks = (nk + DA_KC - 1) / DA_KC;
+  const int c0 = grp * nch, c1 = min(nchunks, c0 + nch);
   const int g = lane >> 4;
   // S^T tile of this wave: key tile kt (16 keys) x row block rb (16 rows)
   const int kt = wave & 1, rb = wave >> 1;
@@ -280,13 +285,13 @@ __global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
 #pragma unroll
     for (int dc = 0; dc < 8; ++dc) qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
   }
-  // V staging: thread = 4 (key, 16-B dim chunk) pairs of the 32 x 32 chunks
   auto load_k = [&](int c, bf16x8 (&kf)[8]) {
     const int key = min(c * DA_KC + kt * 16 + (lane & 15), nk - 1);
     const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
 #pragma unroll
     for (int dc = 0; dc < 8; ++dc) kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
   };
+  // V staging: thread = 4 (key, 16-B dim chunk) pairs of the 32 x 32 chunks
   auto load_v = [&](int c, u32x4 (&vv)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -300,12 +305,16 @@ __global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;  // threads < 32: row threadIdx.x
+  // softmax ownership: row sr = threadIdx.x >> 3, keys 4 sq .. 4 sq + 3; (m, l) replicated in the row's 8 lanes
+  const int sr = threadIdx.x >> 3, sq = threadIdx.x & 7;
+  float m_run = -INFINITY, l_run = 0.f;
   bf16x8 kf[8], kn[8];
   u32x4 vv[4], vn[4];
-  load_k(0, kf);
-  load_v(0, vv);
-  for (int c = 0; c < nchunks; ++c) {
+  if (c0 < c1) {
+    load_k(c0, kf);
+    load_v(c0, vv);
+  }
+  for (int c = c0; c < c1; ++c) {
     const int j0 = c * DA_KC;
     // V(c) -> LDS image (the previous chunk's P.V reads ended at the loop-closing barrier)
 #pragma unroll
@@ -314,40 +323,44 @@ __global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
       *reinterpret_cast<u32x4*>(Vimg + kr * 512 + (((2 * ch) ^ da_sw(kr)) << 3)) = vv[i];
     }
     {  // S^T tile
-      f32x4 s = {0.f, 0.f, 0.f, 0.f};
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int dc = 0; dc < 8; ++dc) s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], s, 0, 0, 0);
+      for (int dc = 0; dc < 8; ++dc) sv = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], sv, 0, 0, 0);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int kl = kt * 16 + 4 * g + e;
-        float x = s[e] * a.scale;
+        float x = sv[e] * a.scale;
         if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
         const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
         S[row - r0][kl] = ok ? x : -INFINITY;
       }
     }
-    if (c + 1 < nchunks) {  // next chunk's K fragments and V rows in flight during this chunk's softmax / P.V
+    if (c + 1 < c1) {  // next chunk's K fragments and V rows in flight during this chunk's softmax / P.V
       load_k(c + 1, kn);
       load_v(c + 1, vn);
     }
     __syncthreads();
-    if (threadIdx.x < DA_R) {  // online softmax of row threadIdx.x
-      const int r = threadIdx.x;
-      float m = m_run;
+    {  // online softmax: 8 lanes per row
+      float x[4];
 #pragma unroll
-      for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
+      for (int i = 0; i < 4; ++i) x[i] = S[sr][4 * sq + i];
+      float m = fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3]));
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      m = fmaxf(m, m_run);
       const float al = m_run == -INFINITY ? 0.f : __expf(m_run - m);
-      float l = 0.f;
+      float p[4], l = 0.f;
 #pragma unroll
-      for (int k = 0; k < DA_KC; k += 2) {
-        const float p0 = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
-        const float p1 = m == -INFINITY ? 0.f : __expf(S[r][k + 1] - m);
-        l += p0 + p1;
-        *reinterpret_cast<unsigned*>(&Pm[r][k]) = pack2bf(p0, p1);
+      for (int i = 0; i < 4; ++i) {
+        p[i] = m == -INFINITY ? 0.f : __expf(x[i] - m);
+        l += p[i];
       }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) l += __shfl_xor(l, o, 64);
       l_run = l_run * al + l;
       m_run = m;
-      alpha_s[r] = al;
+      *reinterpret_cast<u32x2*>(&Pm[sr][4 * sq]) = u32x2{pack2bf(p[0], p[1]), pack2bf(p[2], p[3])};
+      if (sq == 0) alpha_s[sr] = al;
     }
     __syncthreads();
     {  // O^T += V^T P^T (rows rescaled by alpha first)
@@ -370,20 +383,37 @@ __global__ void __launch_bounds__(256) decode_attn_one(pz_decode_attn_args a) {
     for (int i = 0; i < 4; ++i) vv[i] = vn[i];
     __syncthreads();  // S, P, alpha and the V image are rewritten by the next chunk
   }
-  if (threadIdx.x < DA_R) alpha_s[threadIdx.x] = l_run > 0.f ? 1.f / l_run : 0.f;
+  if (sq == 0) {
+    ml_s[sr][0] = m_run;
+    ml_s[sr][1] = l_run;
+  }
   __syncthreads();
+  const bool direct = gridDim.x == 1;
+  float* ws = direct ? nullptr : a.ws + (((int64_t)b * gridDim.x + grp) * Rpad + r0) * DA_RS;
+  if (!direct && threadIdx.x < DA_R) {
+    ws[threadIdx.x * DA_RS + DA_HD] = ml_s[threadIdx.x][0];
+    ws[threadIdx.x * DA_RS + DA_HD + 1] = ml_s[threadIdx.x][1];
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int rr = r0 + j * 16 + (lane & 15);
+    const int rl = j * 16 + (lane & 15), rr = r0 + rl;
     if (rr >= R) continue;
-    const float il = alpha_s[j * 16 + (lane & 15)];
-    const int tt = rr / nh, hh = rr % nh;
-    bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD;
+    if (direct) {
+      const float l = ml_s[rl][1], il = l > 0.f ? 1.f / l : 0.f;
+      const int tt = rr / nh, hh = rr % nh;
+      bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int d0 = (4 * wave + i) * 16 + 4 * g;
-      *reinterpret_cast<u32x2*>(out + d0) =
-          u32x2{pack2bf(acc[i][j][0] * il, acc[i][j][1] * il), pack2bf(acc[i][j][2] * il, acc[i][j][3] * il)};
+      for (int i = 0; i < 4; ++i) {
+        const int d0 = (4 * wave + i) * 16 + 4 * g;
+        *reinterpret_cast<u32x2*>(out + d0) =
+            u32x2{pack2bf(acc[i][j][0] * il, acc[i][j][1] * il), pack2bf(acc[i][j][2] * il, acc[i][j][3] * il)};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int d0 = (4 * wave + i) * 16 + 4 * g;
+        *reinterpret_cast<f32x4*>(ws + rl * DA_RS + d0) = acc[i][j];
+      }
     }
   }
 }
@@ -407,31 +437,31 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
   PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
-  // one workgroup per (sample, row tile) walking every key chunk (no merge launch): opt-in, PZ_DECODE_ONE=1 --
-  // measured SLOWER for C4 (chunk 16.2 vs 13.8 ms: its per-chunk S -> softmax -> P.V chain is latency-bound
-  // in one workgroup, ~2.9 us per 32 keys, while the split kernel runs the 9 chunks on 9 CUs at once)
-  {
-    const char* e1 = getenv("PZ_DECODE_ONE");
-    const bool one = e1 && e1[0] == '1';
-    if (one && PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0) {
-      hipLaunchKernelGGL(decode_attn_one, dim3((unsigned)(a->B * rtiles)), dim3(256), 0, st, *a);
-      PZ_CHECK_LAUNCH();
-      return PZ_OK;
-    }
-  }
+  // PZ_DECODE_ONE=1: one workgroup per (sample, row tile) walking every key chunk (no merge launch) -- measured
+  // SLOWER for C4 (chunk 16.2 vs 13.8 ms with the VALU P.V: the per-chunk chain is latency-bound in one
+  // workgroup, ~2.9 us per 32 keys, while the split kernels run the 9 chunks on 9 CUs at once); A/B only
+  const char* e1 = getenv("PZ_DECODE_ONE");
+  const bool one = e1 && e1[0] == '1';
   // chunks per workgroup: one (C4: 9 workgroups) until the (chunk, row tile) grid passes 256 workgroups,
   // then groups of nch chunks (fewer partial rows for the merge)
   const int64_t wg1 = (int64_t)nchunks * a->B * rtiles;
   const char* e = getenv("PZ_DECODE_WG");  // target workgroups (A/B; read per call)
   const int64_t target = e && atoll(e) > 0 ? atoll(e) : 256;
-  int nch = (int)((wg1 + target - 1) / target);
+  int nch = one ? nchunks : (int)((wg1 + target - 1) / target);
   int ngroups = (nchunks + nch - 1) / nch;
-  if (ngroups == 1 && !(PZ_ALIGNED(a->o, 16) && a->ldo % 8 == 0)) {  // the direct-O path stores 16 B per lane
-    PZ_CHECK_ARG(nchunks > 1, "decode_attn: a single key chunk needs a 16-byte aligned O with ldo %% 8 == 0");
+  // PZ_DECODE_PART=valu: the VALU P.V part kernel (A/B; read per call); default the MFMA kernel
+  const char* ep = getenv("PZ_DECODE_PART");
+  const bool mfma = !(ep && strcmp(ep, "valu") == 0);
+  const bool o_vec = mfma ? (PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0) : (PZ_ALIGNED(a->o, 16) && a->ldo % 8 == 0);
+  if (ngroups == 1 && !o_vec) {  // the direct-O paths store 8 B (MFMA) / 16 B (VALU) per lane
+    PZ_CHECK_ARG(nchunks > 1, "decode_attn: a single key chunk needs an aligned O (8 / 16 B, ldo %% 4 / 8 == 0)");
     nch = (nchunks + 1) / 2;
     ngroups = (nchunks + nch - 1) / nch;
   }
-  hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
+  if (mfma)
+    hipLaunchKernelGGL(decode_attn_mfma, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
+  else
+    hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
   PZ_CHECK_LAUNCH();
   if (ngroups == 1) return PZ_OK;  // the part kernel wrote O
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,

@@ -734,18 +734,23 @@ def test_time_embed_modes_match_reference():
         assert outs[1] < outs[0], outs
 
 
-@pytest.mark.parametrize("one", ["0", "1"])
+@pytest.mark.parametrize("mode", ["mfma", "one", "valu", "mfma_wg64"])
 @pytest.mark.parametrize("B,T,cnts,P", [(1, 4, [270], 276), (2, 4, [276, 259], 276), (1, 2, [100], 276),
                                           (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276)])
-def test_decode_attn_matches_reference(B, T, cnts, P, one, monkeypatch):
+def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
     with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
-    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  one = "0": the
-    key-split kernel + fixed-order merge (default); "1": the opt-in one-workgroup kernel (every key chunk
-    in one workgroup, MFMA P.V, no merge launch)"""
+    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  mode "mfma": the
+    key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default); "one": one workgroup walks
+    every key chunk (no merge launch); "valu": the VALU P.V part kernel; "mfma_wg64": several chunks per
+    workgroup (online softmax across chunks) + merge"""
     from pizero_native import ops
 
-    monkeypatch.setenv("PZ_DECODE_ONE", one)
+    monkeypatch.setenv("PZ_DECODE_ONE", "1" if mode == "one" else "0")
+    if mode == "valu":
+        monkeypatch.setenv("PZ_DECODE_PART", "valu")
+    if mode == "mfma_wg64":
+        monkeypatch.setenv("PZ_DECODE_WG", "4")
     C, nh, hd = 1, 8, 256
     nk = P + C + T
     Lp = (nk + 7) // 8 * 8

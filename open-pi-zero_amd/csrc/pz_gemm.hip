@@ -2357,11 +2357,11 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   if (r == 0 || (q > 0 && 2 * r >= G) || q > 8) return;
   int64_t s = G / r;
   s = s < 16 ? s : 16;
-  // every K-piece at least 4 K-tiles: a piece writes (and the merge re-reads) a 256 KiB fp32 partial, which a
-  // short piece cannot amortise -- the K = 320 action-expert wgrad (8192 x 1024, 5 K-tiles) took 42.0 us with
+  // no split below 8 K-tiles: a piece writes (and the merge re-reads) a 256 KiB fp32 partial, which a short
+  // reduction cannot amortise -- the K = 320 action-expert wgrad (8192 x 1024, 5 K-tiles) took 42.0 us with
   // 2 pieces per leftover tile vs 20.0 us whole (tools/shape_ab.py, profiles/r03/shape_ab.log)
-  s = s < nk / 4 ? s : nk / 4;
-  if (s < 2) return;
+  s = s < nk / 2 ? s : nk / 2;
+  if (s < 2 || nk < 8) return;
   const int64_t kt = (nk + s - 1) / s;
   s = (nk + kt - 1) / kt;
   if (s < 2 || r * s * (int64_t)(32 * NT2 * 16) > a->ws_bytes) return;

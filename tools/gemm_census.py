@@ -1,5 +1,7 @@
 """Every pz_gemm launch of one bench micro-batch (fwd + bwd, micro-batch 64) with its shape, layout,
-epilogue, kernel and HIP-event duration, aggregated per (layout, M, N, K, epilogue).
+epilogue, kernel and HIP-event duration, aggregated per (layout, M, N, K, epilogue).  Single stream
+(PZ_EXPERT_STREAM=0 unless set): events on the launching stream would otherwise time the action-expert
+GEMMs while they share the chip with the vlm group's on the second stream.
 
     python tools/gemm_census.py [--micro-batch 64]
 """
@@ -14,6 +16,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "open-pi-zero_amd"))
 
 import torch  # noqa: E402
+
+os.environ.setdefault("PZ_EXPERT_STREAM", "0")
 
 
 def main():

@@ -161,14 +161,18 @@ typedef struct pz_qkv_rope_args {
   const int64_t* pos; const float* cs;
   void* q_out; void* k_out; void* v_out;
   int64_t T, nh, hd, Lq, qoff, Lk, koff;
+  /* (ABI 15) w_fp8 = 1: W holds OCP e4m3 codes [N][K] (ldw in codes) with the per-tensor scale w_scale (the fp8
+   * inference weights of C5); pz_gemm_qkv_rope's few-row path only (W8A16), 0 everywhere else */
+  int32_t w_fp8; float w_scale;
 } pz_qkv_rope_args;
 int pz_gemv_qkv_rope(const pz_qkv_rope_args* a, void* stream);
 /* The same fused projection + RoPE + scatter for MANY rows (training / prefill, mixture.py:162-215,
  * utils.py:4-16, joint_model.py:170-257): one 8-phase 256-tile MFMA GEMM whose epilogue rounds each head's
  * projection to bf16, rotates Q / K and writes Q / K / V straight into the joint buffers (no [M, N] qkv
- * tensor, no pz_qkv_rope_split launch; bit-identical to that pair).  hd = 256, q_out required, norm_w NULL.
- * Returns PZ_ERR_UNSUPPORTED when the shape does not take the 8-phase kernel (too few rows): the caller
- * runs pz_gemm + pz_qkv_rope_split instead.  (ABI 14) */
+ * tensor, no pz_qkv_rope_split launch; bit-identical to that pair).  hd = 256, q_out required.  16 < M <= 64
+ * rows (C5's 50-row denoise chunk) take the skinny-64 MFMA kernel with the same epilogue and an optional fused
+ * Gemma RMSNorm (norm_w); the 8-phase path takes norm_w NULL.  Returns PZ_ERR_UNSUPPORTED when the shape takes
+ * neither kernel: the caller runs pz_gemm + pz_qkv_rope_split instead.  (ABI 14; few-row path ABI 15) */
 int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream);
 /* backward of the above: writes d(qkv) (un-rotates dQ/dK, copies dV).  dq NULL -> zero dQ part */
 int pz_qkv_rope_split_bwd(const void* dq, const void* dk, const void* dv, const int64_t* pos,

@@ -1981,215 +1981,6 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny_kernel(GemmP p) {
 }
 
 // -------------------------------------------------------------------------
-// Skinny GEMM for 16 < M <= 64 rows, and for fp8 (OCP e4m3) weights at M <= 64 (W8A16): the C5
-// denoise steps (an action chunk of 50 rows per sample).  The scheme of gemm_skinny_kernel -- W waves
-// per NC output columns, K split into W contiguous ranges, weights streamed once into VGPRs, LDS
-// reduction -- with MB 16-row blocks sharing every weight fragment (MB MFMAs per fragment; the
-// activation rows are re-read from L2 by every block).  K is walked in 64-k chunks: lane group g
-// takes k = 64c + 16g + [0, 16) of A (two bf16x8) and of B (two bf16x8, or ONE 16-byte load of fp8
-// codes expanded in registers by v_cvt_scalef32_pk_bf16_fp8 -- exact, every e4m3 value is a bf16);
-// the chunk's two MFMAs sum over k = 64c + 16g + [0, 8) and [8, 16), g = 0..3: the same k set on
-// both operands, so the sum is the plain dot product.  The weight scale of fp8 codes is alpha.
-// Requires K % 64 == 0, k-contiguous A and B, batch 1.
-// -------------------------------------------------------------------------
-__device__ __forceinline__ void fp8x16_to_bf16(const u32x4 q, bf16x8& lo, bf16x8& hi) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  bf16x2 h[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    h[2 * e] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, false);
-    h[2 * e + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, true);
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    lo[2 * e] = h[e][0];
-    lo[2 * e + 1] = h[e][1];
-    hi[2 * e] = h[4 + e][0];
-    hi[2 * e + 1] = h[4 + e][1];
-  }
-}
-
-template <int W, int NC, int MB, bool F8W>
-__global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
-  static_assert(W >= MB, "one wave per row block in the epilogue");
-  constexpr int U = MB >= 3 ? 2 : 4;  // 64-k chunks per load batch (register budget: A is MB x 8 VGPRs)
-  __shared__ f32x4 red[W][MB][64];
-  __shared__ float redn[W][MB][16];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const bool geglu = p.epi == PZ_EPI_GEGLU;
-  const bool nrm = p.nw != nullptr;
-  const int64_t ncols = geglu ? p.geglu_I : p.N;
-  const int64_t n0 = (int64_t)blockIdx.x * NC;
-  const int64_t nr = n0 + (lane & 15) % NC;
-  const bool nok = nr < ncols;
-  // row chunks of 64 (blockIdx.y): M > 64 runs as independent 64-row problems sharing the weights in L2
-  const int64_t row0 = (int64_t)blockIdx.y * 64;
-  const int64_t Mc = min((int64_t)64, p.M - row0);
-  constexpr int ES = F8W ? 1 : 2;  // weight element bytes
-  const char* Bc = reinterpret_cast<const char*>(p.B);
-  const char* Brow = Bc + (nr * p.ldb + 16 * g) * ES;
-  const char* Brow2 = Bc + ((p.geglu_I + nr) * p.ldb + 16 * g) * ES;
-  const bf16_t* Arow[MB];
-  bool mok[MB];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    const int64_t m = mb * 16 + (lane & 15);
-    mok[mb] = m < Mc;
-    Arow[mb] = p.A + (row0 + m) * p.lda + 16 * g;
-  }
-  const bf16_t* Wn = p.nw + 16 * g;
-  f32x4 acc[MB], acc2[MB];
-  float ss[MB];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    acc[mb] = acc2[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    ss[mb] = 0.f;
-  }
-  // split-K over blockIdx.z (p.ksplit > 0: raw fp32 partials -> ws, summed by splitk_epilogue_kernel)
-  const bool split = p.ksplit > 0;
-  const int64_t kchunks_all = p.K / 64;
-  const int64_t kz0 = split ? (int64_t)blockIdx.z * (p.ksplit / 64) : 0;
-  const int64_t kchunks = split ? min(kchunks_all - kz0, p.ksplit / 64) : kchunks_all;
-  const int64_t per = (kchunks + W - 1) / W;
-  const int64_t kb = kz0 + wave * per, ke = kz0 + min(kchunks, (int64_t)(wave + 1) * per);
-  auto load_b = [&](const char* row, int64_t c, bf16x8& lo, bf16x8& hi) {
-    if (!nok) {
-      lo = hi = bf16x8{};
-    } else if (F8W) {
-      fp8x16_to_bf16(*reinterpret_cast<const u32x4*>(row + c * 64), lo, hi);
-    } else {
-      lo = *reinterpret_cast<const bf16x8*>(row + c * 128);
-      hi = *reinterpret_cast<const bf16x8*>(row + c * 128 + 16);
-    }
-  };
-  int64_t kc = kb;
-  auto run = [&](auto U_) {
-    constexpr int UU = decltype(U_)::value;
-    for (; kc + UU <= ke; kc += UU) {
-      bf16x8 a[UU][MB][2], b[UU][2], b2[UU][2], wv[UU][2];
-      u32x4 braw[UU], braw2[UU];
-#pragma unroll
-      for (int u = 0; u < UU; ++u) {
-        if (F8W) {  // raw codes first (all loads in flight), expanded after the A loads are issued
-          braw[u] = nok ? *reinterpret_cast<const u32x4*>(Brow + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
-          if (geglu) braw2[u] = nok ? *reinterpret_cast<const u32x4*>(Brow2 + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
-        } else {
-          load_b(Brow, kc + u, b[u][0], b[u][1]);
-          if (geglu) load_b(Brow2, kc + u, b2[u][0], b2[u][1]);
-        }
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-          for (int h = 0; h < 2; ++h)
-            a[u][mb][h] = mok[mb] ? *reinterpret_cast<const bf16x8*>(Arow[mb] + (kc + u) * 64 + 8 * h) : bf16x8{};
-        if (nrm)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) wv[u][h] = *reinterpret_cast<const bf16x8*>(Wn + (kc + u) * 64 + 8 * h);
-      }
-#pragma unroll
-      for (int u = 0; u < UU; ++u) {
-        if (F8W) {
-          fp8x16_to_bf16(braw[u], b[u][0], b[u][1]);
-          if (geglu) fp8x16_to_bf16(braw2[u], b2[u][0], b2[u][1]);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb) {
-            if (nrm) {  // sum of squares of the raw row; the product takes x * (1 + w), rsqrt applied after
-              const u32x4 xa = __builtin_bit_cast(u32x4, a[u][mb][h]), xw = __builtin_bit_cast(u32x4, wv[u][h]);
-              u32x4 o;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float x0 = __uint_as_float(xa[e] << 16), x1 = __uint_as_float(xa[e] & 0xffff0000u);
-                const float w0 = __uint_as_float(xw[e] << 16), w1 = __uint_as_float(xw[e] & 0xffff0000u);
-                ss[mb] += x0 * x0 + x1 * x1;
-                o[e] = pack2bf(x0 * (1.f + w0), x1 * (1.f + w1));
-              }
-              a[u][mb][h] = __builtin_bit_cast(bf16x8, o);
-            }
-            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][h], a[u][mb][h], acc[mb], 0, 0, 0);
-            if (geglu) acc2[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[u][h], a[u][mb][h], acc2[mb], 0, 0, 0);
-          }
-        }
-      }
-    }
-  };
-  run(std::integral_constant<int, U>{});
-  run(std::integral_constant<int, 1>{});
-  // D[n_local = 4g + r][m = mb*16 + (lane & 15)]; wave w < MB finishes row block w
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    red[wave][mb][lane] = acc[mb];
-    if (nrm) {
-      float t = ss[mb];
-      t += __shfl_xor(t, 16, 64);
-      t += __shfl_xor(t, 32, 64);
-      if (lane < 16) redn[wave][mb][lane] = t;
-    }
-  }
-  __syncthreads();
-  const int mb = wave;
-  f32x4 o = {0.f, 0.f, 0.f, 0.f}, o2 = {0.f, 0.f, 0.f, 0.f};
-  if (mb < MB)
-    for (int w = 0; w < W; ++w) o += red[w][mb][lane];
-  if (geglu) {
-    __syncthreads();
-#pragma unroll
-    for (int b = 0; b < MB; ++b) red[wave][b][lane] = acc2[b];
-    __syncthreads();
-    if (mb < MB)
-      for (int w = 0; w < W; ++w) o2 += red[w][mb][lane];
-  }
-  if (mb >= MB) return;
-  const int64_t ml = mb * 16 + (lane & 15);
-  if (ml >= Mc) return;
-  const int64_t mm = row0 + ml;
-  if (split) {  // (host: no fused norm, no GeGLU with split)
-    float* wz = p.ws + (int64_t)blockIdx.z * p.M * p.ldw + mm * p.ldw;
-    for (int r = 0; r < 4; ++r) {
-      const int64_t nn = n0 + 4 * g + r;
-      if (4 * g + r < NC && nn < ncols) wz[nn] = o[r];
-    }
-    return;
-  }
-  float scale = p.alpha;
-  if (nrm) {
-    float t = 0.f;
-    for (int w = 0; w < W; ++w) t += redn[w][mb][lane & 15];
-    scale *= rsqrtf(t / (float)p.K + p.neps);
-  }
-  const int64_t n = n0 + 4 * g;
-  for (int r = 0; r < 4; ++r) {
-    const int64_t nn = n + r;
-    if (4 * g + r >= NC || nn >= ncols) continue;
-    float x = o[r] * scale;
-    if (geglu) {
-      const float gg = x, u = o2[r] * scale;
-      if (p.aux) {
-        p.aux[mm * p.ld_aux + nn] = f2bf(gg);
-        p.aux[mm * p.ld_aux + p.geglu_I + nn] = f2bf(u);
-      }
-      x = gelu_tanh(gg) * u;
-    } else {
-      if (p.bias) x += bf2f(p.bias[nn]);
-      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
-        if (p.aux) p.aux[mm * p.ld_aux + nn] = f2bf(x);
-        x = p.epi == PZ_EPI_GELU ? gelu_tanh(x) : silu(x);
-      }
-      if (p.resid) x += bf2f(p.resid[mm * p.ld_resid + nn]);
-    }
-    if (p.c_fp32) {
-      float* Cp = reinterpret_cast<float*>(p.C) + mm * p.ldc + nn;
-      *Cp = p.beta ? *Cp + x : x;
-    } else {
-      bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + mm * p.ldc + nn;
-      *Cp = f2bf(p.beta ? bf2f(*Cp) + x : x);
-    }
-  }
-}
-
-// -------------------------------------------------------------------------
 // Small strided fp32-accumulate GEMM for the K=7 / N=7 action/proprio linears
 // (SURVEY 2.2 "proprio enc / action dec": 0.03 GF).  One thread per output.
 // -------------------------------------------------------------------------
@@ -2583,39 +2374,11 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   return buf;
 }
 
-template <int W, int NC, int MB, bool F8W>
-static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
-  const int S = p.ksplit > 0 ? (int)((p.K / 64 + p.ksplit / 64 - 1) / (p.ksplit / 64)) : 1;
-  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64), S),
-                     dim3(W * 64), 0, st, p);
+int pz_splitk_epi_launch(const GemmP& p, int S, hipStream_t st) {
+  const int64_t work = p.M * ((p.N + 3) / 4);
+  hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, p, S);
   PZ_CHECK_LAUNCH();
-  if (S > 1) {
-    const int64_t work = p.M * ((p.N + 3) / 4);
-    hipLaunchKernelGGL(splitk_epilogue_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, p, S);
-    PZ_CHECK_LAUNCH();
-  }
   return PZ_OK;
-}
-
-template <int W, int MB, bool F8W>
-static int launch_sk64_nc(const GemmP& p, int nc, int64_t tiles_n, hipStream_t st) {
-  if (nc == 4) return launch_sk64<W, 4, MB, F8W>(p, tiles_n, st);
-  if (nc == 8) return launch_sk64<W, 8, MB, F8W>(p, tiles_n, st);
-  return launch_sk64<W, 16, MB, F8W>(p, tiles_n, st);
-}
-
-template <bool F8W>
-static int launch_sk64_any(const GemmP& p, const Plan& pl, hipStream_t st) {
-  const int nc = pl.skinny_nc;
-  const int64_t tn = pl.tiles_n;
-  if (pl.skinny_w == 8) {
-    if (pl.skinny_mb == 1) return launch_sk64_nc<8, 1, F8W>(p, nc, tn, st);
-    if (pl.skinny_mb == 2) return launch_sk64_nc<8, 2, F8W>(p, nc, tn, st);
-    return launch_sk64_nc<8, 4, F8W>(p, nc, tn, st);
-  }
-  if (pl.skinny_mb == 1) return launch_sk64_nc<4, 1, F8W>(p, nc, tn, st);
-  if (pl.skinny_mb == 2) return launch_sk64_nc<4, 2, F8W>(p, nc, tn, st);
-  return launch_sk64_nc<4, 4, F8W>(p, nc, tn, st);
 }
 
 template <bool GEGLU>
@@ -2866,7 +2629,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
       p.ksplit = pl.ksplit;
       p.ldw = pl.ldw;
     }
-    return a->fp8_mode == 2 ? launch_sk64_any<true>(p, pl, st) : launch_sk64_any<false>(p, pl, st);
+    return pz_sk64_launch(p, pl.skinny_w, pl.skinny_nc, pl.skinny_mb, a->fp8_mode == 2, pl.tiles_n, st);
   }
   if (a->fp8_mode == 1) {
     p.tiles_m = (int)pl.tiles_m;
@@ -2940,8 +2703,9 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
                "gemm_qkv_rope: bad args");
   PZ_CHECK_ARG(a->nh >= 1 && a->N == (a->nh + 2) * a->hd && a->T > 0 && a->M % a->T == 0,
                "gemm_qkv_rope: N = (nh + 2) * hd, M %% T == 0");
-  // one 256-column tile per head, Q written, no fused norm: otherwise not this kernel (no error text)
-  if (a->hd != BT || !a->q_out || a->norm_w) return PZ_ERR_UNSUPPORTED;
+  // head_dim 256 (one 256-column 8-phase tile / 16 skinny blocks per head) and Q written: otherwise not this
+  // kernel (no error text)
+  if (a->hd != BT || !a->q_out) return PZ_ERR_UNSUPPORTED;
   PZ_CHECK_ARG(PZ_ALIGNED(a->x, 16) && PZ_ALIGNED(a->W, 16) && a->ldx % 8 == 0 && a->ldw % 8 == 0 && a->K % 8 == 0 &&
                    PZ_ALIGNED(a->q_out, 16) && PZ_ALIGNED(a->k_out, 16) && PZ_ALIGNED(a->v_out, 16),
                "gemm_qkv_rope: 16-byte alignment");
@@ -2953,8 +2717,38 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
   g.C = a->q_out; g.ldc = a->N;
   g.batch = 1; g.batch_inner = 1;
   g.alpha = 1.f;
+  g.norm_w = a->norm_w;
+  g.norm_eps = a->norm_eps;
+  if (a->w_fp8) {
+    PZ_CHECK_ARG(a->ldw % 16 == 0, "gemm_qkv_rope: fp8 weights need ldw %% 16 == 0");
+    g.fp8_mode = 2;
+    g.alpha = a->w_scale;
+  }
   const Plan pl = make_plan(&g);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
-  if (!use_8phase() || pl.kind != PATH_256) return PZ_ERR_UNSUPPORTED;
+  // few rows (16 < M <= 64: C5's 50-row denoise chunk): the skinny-64 kernel with the RoPE epilogue, the
+  // Gemma RMSNorm optionally fused (mixture.py:162-215 + utils.py:4-16 in one launch)
+  if (pl.kind == PATH_SKINNY64 && pl.ksplit == 0 && a->K % 64 == 0 && a->N % 256 == 0 && a->M <= 64 &&
+      (!a->norm_w || PZ_ALIGNED(a->norm_w, 16))) {
+    GemmP p;
+    memset(&p, 0, sizeof(p));
+    p.A = (const bf16_t*)a->x;
+    p.B = (const bf16_t*)a->W;
+    p.C = a->q_out;
+    p.M = a->M; p.N = a->N; p.K = a->K;
+    p.lda = a->ldx; p.ldb = a->ldw; p.ldc = a->N;
+    p.batch_inner = 1;
+    p.alpha = a->w_fp8 ? a->w_scale : 1.f;
+    p.nw = (const bf16_t*)a->norm_w;
+    p.neps = a->norm_eps;
+    p.rpos = a->pos;
+    p.rcs = a->cs;
+    p.rq = (bf16_t*)a->q_out;
+    p.rk = (bf16_t*)a->k_out;
+    p.rv = (bf16_t*)a->v_out;
+    p.rT = a->T; p.rnh = a->nh; p.rLq = a->Lq; p.rqoff = a->qoff; p.rLk = a->Lk; p.rkoff = a->koff;
+    return pz_sk64_launch(p, pl.skinny_w, 16, pl.skinny_mb, a->w_fp8 != 0, a->N / 16, (hipStream_t)stream);
+  }
+  if (a->norm_w || a->w_fp8 || !use_8phase() || pl.kind != PATH_256) return PZ_ERR_UNSUPPORTED;
   GemmP p;
   memset(&p, 0, sizeof(p));
   p.A = (const bf16_t*)a->x;

@@ -1,4 +1,4 @@
-// Row-slab GEMM kernel (own translation unit: pz_gemm.hip takes minutes to compile).
+// Few-row (skinny-64) and row-slab GEMM kernels (own translation unit: pz_gemm.hip takes minutes to compile).
 #include "pz_gemm_epi.h"
 
 namespace {
@@ -121,6 +121,260 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP
   }
 }
 
+// -------------------------------------------------------------------------
+// Skinny GEMM for 16 < M <= 64 rows, and for fp8 (OCP e4m3) weights at M <= 64 (W8A16): the C5
+// denoise steps (an action chunk of 50 rows per sample).  The scheme of gemm_skinny_kernel -- W waves
+// per NC output columns, K split into W contiguous ranges, weights streamed once into VGPRs, LDS
+// reduction -- with MB 16-row blocks sharing every weight fragment (MB MFMAs per fragment; the
+// activation rows are re-read from L2 by every block).  K is walked in 64-k chunks: lane group g
+// takes k = 64c + 16g + [0, 16) of A (two bf16x8) and of B (two bf16x8, or ONE 16-byte load of fp8
+// codes expanded in registers by v_cvt_scalef32_pk_bf16_fp8 -- exact, every e4m3 value is a bf16);
+// the chunk's two MFMAs sum over k = 64c + 16g + [0, 8) and [8, 16), g = 0..3: the same k set on
+// both operands, so the sum is the plain dot product.  The weight scale of fp8 codes is alpha.
+// Requires K % 64 == 0, k-contiguous A and B, batch 1.
+// -------------------------------------------------------------------------
+__device__ __forceinline__ void fp8x16_to_bf16(const u32x4 q, bf16x8& lo, bf16x8& hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 h[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[2 * e] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, false);
+    h[2 * e + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, true);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    lo[2 * e] = h[e][0];
+    lo[2 * e + 1] = h[e][1];
+    hi[2 * e] = h[4 + e][0];
+    hi[2 * e + 1] = h[4 + e][1];
+  }
+}
+
+template <int W, int NC, int MB, bool F8W>
+__global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
+  static_assert(W >= MB, "one wave per row block in the epilogue");
+  constexpr int U = MB >= 3 ? 2 : 4;  // 64-k chunks per load batch (register budget: A is MB x 8 VGPRs)
+  __shared__ f32x4 red[W][MB][64];
+  __shared__ float redn[W][MB][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const bool geglu = p.epi == PZ_EPI_GEGLU;
+  const bool nrm = p.nw != nullptr;
+  const int64_t ncols = geglu ? p.geglu_I : p.N;
+  const int64_t n0 = (int64_t)blockIdx.x * NC;
+  // fused RoPE + Q / K / V scatter (pz_gemm_qkv_rope few-row path, NC == 16, head_dim 256): block = 8 rotation
+  // pairs of one head -- columns i..i+7 and their partners i+128..i+135 -- so the epilogue holds both halves
+  const bool rope = p.rcs != nullptr;
+  const int64_t nr = rope ? (int64_t)(blockIdx.x >> 4) * 256 + (blockIdx.x & 15) * 8 + (lane & 7) + ((lane & 8) << 4)
+                          : n0 + (lane & 15) % NC;
+  const bool nok = nr < ncols;
+  // row chunks of 64 (blockIdx.y): M > 64 runs as independent 64-row problems sharing the weights in L2
+  const int64_t row0 = (int64_t)blockIdx.y * 64;
+  const int64_t Mc = min((int64_t)64, p.M - row0);
+  constexpr int ES = F8W ? 1 : 2;  // weight element bytes
+  const char* Bc = reinterpret_cast<const char*>(p.B);
+  const char* Brow = Bc + (nr * p.ldb + 16 * g) * ES;
+  const char* Brow2 = Bc + ((p.geglu_I + nr) * p.ldb + 16 * g) * ES;
+  const bf16_t* Arow[MB];
+  bool mok[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int64_t m = mb * 16 + (lane & 15);
+    mok[mb] = m < Mc;
+    Arow[mb] = p.A + (row0 + m) * p.lda + 16 * g;
+  }
+  const bf16_t* Wn = p.nw + 16 * g;
+  f32x4 acc[MB], acc2[MB];
+  float ss[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    acc[mb] = acc2[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    ss[mb] = 0.f;
+  }
+  // split-K over blockIdx.z (p.ksplit > 0: raw fp32 partials -> ws, summed by splitk_epilogue_kernel)
+  const bool split = p.ksplit > 0;
+  const int64_t kchunks_all = p.K / 64;
+  const int64_t kz0 = split ? (int64_t)blockIdx.z * (p.ksplit / 64) : 0;
+  const int64_t kchunks = split ? min(kchunks_all - kz0, p.ksplit / 64) : kchunks_all;
+  const int64_t per = (kchunks + W - 1) / W;
+  const int64_t kb = kz0 + wave * per, ke = kz0 + min(kchunks, (int64_t)(wave + 1) * per);
+  auto load_b = [&](const char* row, int64_t c, bf16x8& lo, bf16x8& hi) {
+    if (!nok) {
+      lo = hi = bf16x8{};
+    } else if (F8W) {
+      fp8x16_to_bf16(*reinterpret_cast<const u32x4*>(row + c * 64), lo, hi);
+    } else {
+      lo = *reinterpret_cast<const bf16x8*>(row + c * 128);
+      hi = *reinterpret_cast<const bf16x8*>(row + c * 128 + 16);
+    }
+  };
+  int64_t kc = kb;
+  auto run = [&](auto U_) {
+    constexpr int UU = decltype(U_)::value;
+    for (; kc + UU <= ke; kc += UU) {
+      bf16x8 a[UU][MB][2], b[UU][2], b2[UU][2], wv[UU][2];
+      u32x4 braw[UU], braw2[UU];
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
+        if (F8W) {  // raw codes first (all loads in flight), expanded after the A loads are issued
+          braw[u] = nok ? *reinterpret_cast<const u32x4*>(Brow + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+          if (geglu) braw2[u] = nok ? *reinterpret_cast<const u32x4*>(Brow2 + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+        } else {
+          load_b(Brow, kc + u, b[u][0], b[u][1]);
+          if (geglu) load_b(Brow2, kc + u, b2[u][0], b2[u][1]);
+        }
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            a[u][mb][h] = mok[mb] ? *reinterpret_cast<const bf16x8*>(Arow[mb] + (kc + u) * 64 + 8 * h) : bf16x8{};
+        if (nrm)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) wv[u][h] = *reinterpret_cast<const bf16x8*>(Wn + (kc + u) * 64 + 8 * h);
+      }
+#pragma unroll
+      for (int u = 0; u < UU; ++u) {
+        if (F8W) {
+          fp8x16_to_bf16(braw[u], b[u][0], b[u][1]);
+          if (geglu) fp8x16_to_bf16(braw2[u], b2[u][0], b2[u][1]);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb) {
+            if (nrm) {  // sum of squares of the raw row; the product takes x * (1 + w), rsqrt applied after
+              const u32x4 xa = __builtin_bit_cast(u32x4, a[u][mb][h]), xw = __builtin_bit_cast(u32x4, wv[u][h]);
+              u32x4 o;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float x0 = __uint_as_float(xa[e] << 16), x1 = __uint_as_float(xa[e] & 0xffff0000u);
+                const float w0 = __uint_as_float(xw[e] << 16), w1 = __uint_as_float(xw[e] & 0xffff0000u);
+                ss[mb] += x0 * x0 + x1 * x1;
+                o[e] = pack2bf(x0 * (1.f + w0), x1 * (1.f + w1));
+              }
+              a[u][mb][h] = __builtin_bit_cast(bf16x8, o);
+            }
+            acc[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[u][h], a[u][mb][h], acc[mb], 0, 0, 0);
+            if (geglu) acc2[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b2[u][h], a[u][mb][h], acc2[mb], 0, 0, 0);
+          }
+        }
+      }
+    }
+  };
+  run(std::integral_constant<int, U>{});
+  run(std::integral_constant<int, 1>{});
+  // D[n_local = 4g + r][m = mb*16 + (lane & 15)]; wave w < MB finishes row block w
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    red[wave][mb][lane] = acc[mb];
+    if (nrm) {
+      float t = ss[mb];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if (lane < 16) redn[wave][mb][lane] = t;
+    }
+  }
+  __syncthreads();
+  const int mb = wave;
+  f32x4 o = {0.f, 0.f, 0.f, 0.f}, o2 = {0.f, 0.f, 0.f, 0.f};
+  if (mb < MB)
+    for (int w = 0; w < W; ++w) o += red[w][mb][lane];
+  if (geglu) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < MB; ++b) red[wave][b][lane] = acc2[b];
+    __syncthreads();
+    if (mb < MB)
+      for (int w = 0; w < W; ++w) o2 += red[w][mb][lane];
+  }
+  if (mb >= MB) return;
+  const int64_t ml = mb * 16 + (lane & 15);
+  if (rope) {  // (host: no split, no GeGLU / bias / residual)
+    float scale = p.alpha;
+    if (nrm) {
+      float t = 0.f;
+      for (int w = 0; w < W; ++w) t += redn[w][mb][lane & 15];
+      scale *= rsqrtf(t / (float)p.K + p.neps);
+    }
+    // the bf16 projection (what pz_qkv_rope_split reads), then the partner half of each rotation pair from lane
+    // ^ 32 (lane group g ^ 2: local columns 4g.. are pairs 4(g & 1).. of the low half for g < 2, the high half
+    // for g >= 2); both lanes of a pair hold the same row, so they are active together
+    float x[4], y[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = bf2f(f2bf(o[r] * scale));
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = __shfl_xor(x[r], 32, 64);
+    if (ml >= Mc) return;
+    const int64_t mm = row0 + ml;
+    const int64_t head = blockIdx.x >> 4, b = mm / p.rT, t = mm - b * p.rT;
+    const int i = (blockIdx.x & 15) * 8 + 4 * (g & 1);  // pair index of x[0]
+    const bool hi = g >= 2;
+    float v[4];
+    bf16_t* dst;
+    if (head == p.rnh + 1) {  // value head: copied
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = x[r];
+      dst = p.rv + (b * p.rLk + p.rkoff + t) * 256;
+    } else {
+      const float* cs = p.rcs + p.rpos[mm] * 256 + 2 * i;  // (cos, sin) of pairs i..i+3
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float o1, o2;
+        if (hi) rope_pair(y[r], x[r], cs[2 * r], cs[2 * r + 1], o1, o2);
+        else rope_pair(x[r], y[r], cs[2 * r], cs[2 * r + 1], o1, o2);
+        v[r] = hi ? o2 : o1;
+      }
+      dst = head < p.rnh ? p.rq + (b * p.rLq + p.rqoff + t) * (p.rnh * 256) + head * 256
+                         : p.rk + (b * p.rLk + p.rkoff + t) * 256;
+    }
+    *reinterpret_cast<u32x2*>(dst + i + (hi ? 128 : 0)) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+    return;
+  }
+  if (ml >= Mc) return;
+  const int64_t mm = row0 + ml;
+  if (split) {  // (host: no fused norm, no GeGLU with split)
+    float* wz = p.ws + (int64_t)blockIdx.z * p.M * p.ldw + mm * p.ldw;
+    for (int r = 0; r < 4; ++r) {
+      const int64_t nn = n0 + 4 * g + r;
+      if (4 * g + r < NC && nn < ncols) wz[nn] = o[r];
+    }
+    return;
+  }
+  float scale = p.alpha;
+  if (nrm) {
+    float t = 0.f;
+    for (int w = 0; w < W; ++w) t += redn[w][mb][lane & 15];
+    scale *= rsqrtf(t / (float)p.K + p.neps);
+  }
+  const int64_t n = n0 + 4 * g;
+  for (int r = 0; r < 4; ++r) {
+    const int64_t nn = n + r;
+    if (4 * g + r >= NC || nn >= ncols) continue;
+    float x = o[r] * scale;
+    if (geglu) {
+      const float gg = x, u = o2[r] * scale;
+      if (p.aux) {
+        p.aux[mm * p.ld_aux + nn] = f2bf(gg);
+        p.aux[mm * p.ld_aux + p.geglu_I + nn] = f2bf(u);
+      }
+      x = gelu_tanh(gg) * u;
+    } else {
+      if (p.bias) x += bf2f(p.bias[nn]);
+      if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
+        if (p.aux) p.aux[mm * p.ld_aux + nn] = f2bf(x);
+        x = p.epi == PZ_EPI_GELU ? gelu_tanh(x) : silu(x);
+      }
+      if (p.resid) x += bf2f(p.resid[mm * p.ld_resid + nn]);
+    }
+    if (p.c_fp32) {
+      float* Cp = reinterpret_cast<float*>(p.C) + mm * p.ldc + nn;
+      *Cp = p.beta ? *Cp + x : x;
+    } else {
+      bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + mm * p.ldc + nn;
+      *Cp = f2bf(p.beta ? bf2f(*Cp) + x : x);
+    }
+  }
+}
+
 }  // namespace
 
 template <int W, int TNB, bool GEGLU>
@@ -147,4 +401,37 @@ static int launch_rows_w(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
 
 int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, hipStream_t st) {
   return w == 8 ? launch_rows_w<8>(p, tnb, geglu, st) : launch_rows_w<4>(p, tnb, geglu, st);
+}
+
+template <int W, int NC, int MB, bool F8W>
+static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
+  const int S = p.ksplit > 0 ? (int)((p.K / 64 + p.ksplit / 64 - 1) / (p.ksplit / 64)) : 1;
+  hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64), S),
+                     dim3(W * 64), 0, st, p);
+  PZ_CHECK_LAUNCH();
+  if (S > 1) return pz_splitk_epi_launch(p, S, st);
+  return PZ_OK;
+}
+
+template <int W, int MB, bool F8W>
+static int launch_sk64_nc(const GemmP& p, int nc, int64_t tiles_n, hipStream_t st) {
+  if (nc == 4) return launch_sk64<W, 4, MB, F8W>(p, tiles_n, st);
+  if (nc == 8) return launch_sk64<W, 8, MB, F8W>(p, tiles_n, st);
+  return launch_sk64<W, 16, MB, F8W>(p, tiles_n, st);
+}
+
+template <bool F8W>
+static int launch_sk64_any(const GemmP& p, int w, int nc, int mb, int64_t tn, hipStream_t st) {
+  if (w == 8) {
+    if (mb == 1) return launch_sk64_nc<8, 1, F8W>(p, nc, tn, st);
+    if (mb == 2) return launch_sk64_nc<8, 2, F8W>(p, nc, tn, st);
+    return launch_sk64_nc<8, 4, F8W>(p, nc, tn, st);
+  }
+  if (mb == 1) return launch_sk64_nc<4, 1, F8W>(p, nc, tn, st);
+  if (mb == 2) return launch_sk64_nc<4, 2, F8W>(p, nc, tn, st);
+  return launch_sk64_nc<4, 4, F8W>(p, nc, tn, st);
+}
+
+int pz_sk64_launch(const GemmP& p, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st) {
+  return f8w ? launch_sk64_any<true>(p, w, nc, mb, tiles_n, st) : launch_sk64_any<false>(p, w, nc, mb, tiles_n, st);
 }

@@ -308,6 +308,7 @@ int pz_gemv_launch(const pz_gemm_args* a, hipStream_t st) {
 extern "C" int pz_gemv_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
   PZ_CHECK_ARG(a && a->x && a->W && a->pos && a->cs && a->k_out && a->v_out && a->M >= 1 && a->M <= 8,
                "gemv_qkv_rope: bad args (M <= 8)");
+  PZ_CHECK_ARG(!a->w_fp8, "gemv_qkv_rope: bf16 weights only");
   PZ_CHECK_ARG(a->K % 512 == 0 && a->hd % 2 == 0 && a->N == (a->nh + 2) * a->hd && a->T > 0 && a->M % a->T == 0,
                "gemv_qkv_rope: bad shape");
   PZ_CHECK_ARG(PZ_ALIGNED(a->x, 16) && PZ_ALIGNED(a->W, 16) && a->ldx % 8 == 0 && a->ldw % 8 == 0 &&

@@ -94,6 +94,7 @@ class QkvRopeArgs(C.Structure):
         ("x", vp), ("ldx", i64), ("W", vp), ("ldw", i64), ("M", i64), ("N", i64), ("K", i64),
         ("norm_w", vp), ("norm_eps", f32), ("pos", vp), ("cs", vp), ("q_out", vp), ("k_out", vp), ("v_out", vp),
         ("T", i64), ("nh", i64), ("hd", i64), ("Lq", i64), ("qoff", i64), ("Lk", i64), ("koff", i64),
+        ("w_fp8", i32), ("w_scale", f32),
     ]
 
 

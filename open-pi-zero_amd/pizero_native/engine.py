@@ -1097,6 +1097,12 @@ class Engine:
         d = self.d
         return d.hd == 256 and os.environ.get("PZ_DECODE_ATTN", "1") != "0" and d.H * d.nh <= 1024
 
+    def _qkv_w_f8(self, p):
+        """(q|k|v weights, fp8 scale): the e4m3 codes and their scale when prepare_fp8() holds them for layer p,
+        else (bf16 weights, None)"""
+        f = self.f8.get(p + "self_attn.q_proj.weight") if self.f8 else None
+        return (self.qkv_w(p), None) if f is None else (f[0], f[1])
+
     def prefetch_weights(self):
         """workgroups of the denoise weight prefetch (pz_prefetch of layer l+1 on a side stream while layer l
         runs; PZ_PREFETCH=<workgroups>, 0 = off)"""
@@ -1326,9 +1332,14 @@ class Engine:
                 side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):
                     ops.prefetch(self.ar.prefix_span(f"{g.prefix}{(l + 1) % d.nL}."), pf)
+            nrm = (self.w(p + "input_layernorm.weight"), d.rms_eps)
             if self.gemv_ok(M, d.aH):  # one launch: RMSNorm + q|k|v GEMV + RoPE + Q / K-cache / V-cache scatter
                 ops.gemv_qkv_rope(x, self.qkv_w(p), apos, self.rope(g.theta), Q, Kj, Vj, d.H, nh, hd, d.H, 0, Lp,
-                                  g.off, norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                                  g.off, norm=nrm)
+            elif self.fuse_qkv_rope and self.few_rows(M, d.aH) and \
+                    ops.gemm_qkv_rope(x, self._qkv_w_f8(p)[0], apos, self.rope(g.theta), Q, Kj, Vj, d.H, nh, hd, d.H,
+                                      0, Lp, g.off, norm=nrm, w_scale=self._qkv_w_f8(p)[1]):
+                pass  # C5's 50-row chunk: RMSNorm + skinny-64 q|k|v (bf16 or W8A16) + RoPE + scatter in one launch
             else:
                 qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
                 if self.few_rows(M, d.aH):  # RMSNorm fused into the q|k|v GEMM

@@ -361,14 +361,19 @@ def gemv_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, k
 PZ_ERR_UNSUPPORTED = 3  # include/pz_abi.h
 
 
-def gemm_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, koff):
-    """Many-row q|k|v projection with RoPE and the joint Q / K / V scatter fused into the 8-phase GEMM's
-    epilogue (pz_gemm_qkv_rope).  Returns False (nothing launched) when the shape does not take the
-    8-phase kernel -- the caller then runs linear + qkv_rope_split (same bits)."""
+def gemm_qkv_rope(x, W, pos, cs, q_out, k_out, v_out, T, nh, hd, Lq, qoff, Lk, koff, norm=None, w_scale=None):
+    """q|k|v projection with RoPE and the joint Q / K / V scatter fused into the GEMM's epilogue
+    (pz_gemm_qkv_rope): the 8-phase kernel for many rows, the skinny-64 kernel for 16 < M <= 64 (norm = (w, eps):
+    fused Gemma RMSNorm; w_scale: W is e4m3 codes, W8A16 -- few-row path only).  Returns False (nothing launched) when the shape takes neither --
+    the caller then runs linear + qkv_rope_split (same bits)."""
     a = QkvRopeArgs()
     a.x, a.ldx = _p(x), x.stride(0)
     a.W, a.ldw = _p(W), W.stride(0)
     a.M, a.N, a.K = x.shape[0], W.shape[0], x.shape[1]
+    if norm is not None:
+        a.norm_w, a.norm_eps = _p(norm[0]), float(norm[1])
+    if w_scale is not None:  # W = e4m3 codes (uint8 [N, K]) with a per-tensor scale: few-row W8A16 path
+        a.w_fp8, a.w_scale = 1, float(w_scale)
     a.pos, a.cs = _p(pos), _p(cs)
     a.q_out, a.k_out, a.v_out = _p(q_out), _p(k_out), _p(v_out)
     a.T, a.nh, a.hd, a.Lq, a.qoff, a.Lk, a.koff = T, nh, hd, Lq, qoff, Lk, koff

@@ -769,6 +769,67 @@ def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     close(o, ref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("B,T,off,K", [(1, 50, 789, 1024), (10, 5, 277, 1024), (6, 5, 277, 2048), (4, 16, 20, 1024)])
+@pytest.mark.parametrize("norm", [False, True])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_gemm_qkv_rope_few_rows_bit_identical(B, T, off, K, norm, fp8):
+    """pz_gemm_qkv_rope's few-row path (16 < M <= 64: C5's 50-row denoise chunk): the skinny-64 kernel with the
+    rotation pairs of a head in one block, RoPE + Q / K / V scatter in the epilogue, RMSNorm optionally fused,
+    bf16 or e4m3 (W8A16) weights -- bit-identical to pz_gemm (skinny-64, same fused norm / same fp8 codes) +
+    pz_qkv_rope_split."""
+    from pizero_native import ops
+
+    nh, hd = 8, 256
+    L = off + T + 3
+    Lp = (L + 7) // 8 * 8
+    M = B * T
+    x, W = bf(M, K), bf((nh + 2) * hd, K, scale=K ** -0.5)
+    nw = bf(K, scale=0.1) if norm else None
+    nrm = (nw, 1e-6) if norm else None
+    if fp8:  # the e4m3 codes + per-tensor scale of prepare_fp8, and the bf16 weights they decode to
+        sc = ops.fp8_weight_scale(W)
+        Wq = torch.empty(W.shape, device=dev, dtype=torch.uint8)
+        ops.fp8_quant_tensor(W, Wq, sc)
+        W = (Wq.view(torch.float8_e4m3fn).float() * float(sc)).to(torch.bfloat16)
+    pos = (torch.arange(T, device=dev) + off).repeat(B).contiguous()
+    cs = torch.empty((L + 9) * hd, device=dev, dtype=torch.float32)
+    ops.rope_table(cs, L + 8, hd, 10000.0)
+    outs = []
+    for fused in (True, False):
+        Q = torch.full((B, T, nh * hd), 7.0, device=dev, dtype=torch.bfloat16)
+        Kj = torch.full((B, Lp, hd), 7.0, device=dev, dtype=torch.bfloat16)
+        Vj = torch.full((B, Lp, hd), 7.0, device=dev, dtype=torch.bfloat16)
+        if fused:
+            assert ops.gemm_qkv_rope(x, Wq if fp8 else W, pos, cs, Q, Kj, Vj, T, nh, hd, T, 0, Lp, off, norm=nrm,
+                                     w_scale=sc if fp8 else None)
+        else:
+            qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=torch.bfloat16)
+            if fp8:
+                ops.linear_fp8(x, Wq, sc, qkv, norm=nrm)
+            else:
+                ops.linear(x, W, qkv, norm=nrm)
+            ops.qkv_rope_split(qkv, pos, cs, Q, Kj, Vj, B, T, nh, 1, hd, T, 0, Lp, off)
+        outs.append((Q, Kj, Vj))
+    torch.cuda.synchronize()
+    for nm, a, b in zip("QKV", *outs):
+        assert torch.equal(a, b), (nm, int((a != b).sum()), float((a.float() - b.float()).abs().max()))
+    assert (outs[0][1][:, :off] == 7.0).all() and (outs[0][1][:, off + T:] == 7.0).all()  # only rows off..off+T-1
+    # and against torch fp32 (the reference's rotate_half form, utils.py:4-16)
+    xf = x.float()
+    if norm:
+        xf = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-6) * (1.0 + nw.float())
+    qkv = (xf @ W.float().t()).view(B, T, nh + 2, hd)
+    c = cs.view(-1, hd)[pos.view(B, T)]
+    co, si = c[..., 0::2], c[..., 1::2]
+    cos, sin = torch.cat([co, co], -1)[:, :, None], torch.cat([si, si], -1)[:, :, None]
+    rot = lambda t: torch.cat([-t[..., hd // 2:], t[..., : hd // 2]], -1)  # noqa: E731
+    qk = qkv[:, :, : nh + 1] * cos + rot(qkv[:, :, : nh + 1]) * sin
+    tol = 5e-2 if fp8 else 3e-2  # fp8: the reference uses the decoded weights (rounded to bf16 here)
+    close(outs[0][0].view(B, T, nh, hd), qk[:, :, :nh], atol=tol)
+    close(outs[0][1][:, off:off + T], qk[:, :, nh], atol=tol)
+    close(outs[0][2][:, off:off + T], qkv[:, :, nh + 1], atol=tol)
+
+
 @pytest.mark.parametrize("B,T,off", [(16, 276, 0), (64, 276, 0), (16, 5, 276)])
 def test_gemm_qkv_rope_bit_identical_to_gemm_plus_split(B, T, off):
     """pz_gemm_qkv_rope (q|k|v GEMM with RoPE + joint Q/K/V scatter in the 8-phase epilogue, N1) against
@@ -791,7 +852,7 @@ def test_gemm_qkv_rope_bit_identical_to_gemm_plus_split(B, T, off):
         Vj = torch.full((B, Lp, hd), 7.0, device=dev, dtype=torch.bfloat16)
         done = fused and ops.gemm_qkv_rope(x, W, pos, cs, Q, Kj, Vj, T, nh, hd, L, off, Lp, off)
         if fused and T < 256:
-            assert not done  # 80 rows: not an 8-phase shape
+            assert not done  # 80 rows: neither an 8-phase nor a few-row (<= 64) shape
         if not done:
             qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=torch.bfloat16)
             ops.linear(x, W, qkv)

@@ -128,11 +128,18 @@ int pz_layernorm_fwd(const void* x, int64_t ldx, const void* w, const void* b, v
                      float* mean, float* rstd, int64_t R, int64_t D, float eps, void* stream);
 int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
                      const float* mean, const float* rstd, const void* dres, void* dx, int64_t lddx,
-                     float* dw_part, float* db_part, int64_t R, int64_t D, void* stream);
+                     float* dw_part, float* db_part, int64_t R, int64_t D, float* dx_part, void* stream);
 /* rows_per_part used by the *_bwd partial sums */
 int64_t pz_norm_rows_per_part(void);
 /* out[n] (+)= sum_p part[p*D + n]  -> bf16 (parameter gradient of a norm weight/bias) */
 int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream);
+/* (ABI 15) pz_layernorm_bwd's dx_part (NULL ok): per-part column sums of the bf16 dx, [ceil(R / rows_per_part)][D]
+ * fp32 -- reduce_parts of them is the bias gradient of the Linear whose output gradient dx is (SigLIP fc2 /
+ * out_proj, siglip.py:183-192 / 103-106 autograd), without re-reading dx.
+ * pz_act_bwd_colsum: dpre = dh * act'(pre) (pz_act_bwd, dpre may alias dh) and dbias (+)= the column sums of the
+ * bf16 dpre (the fc1 bias gradient) through ws [ws_rows][N] fp32 partials, in one pass over dh / pre. */
+int pz_act_bwd_colsum(const void* dh, int64_t lddh, const void* pre, int64_t ldpre, void* dpre, int64_t M, int64_t N,
+                      int32_t act, float* ws, int64_t ws_rows, void* dbias, int32_t beta, void* stream);
 /* bias gradient: out[n] (+)= sum_m X[m*ld + n] (bf16 X, fp32 workspace ws of >= 64*N floats) */
 int pz_colsum(const void* X, int64_t ld, int64_t M, int64_t N, void* out, int32_t beta, float* ws,
               void* stream);

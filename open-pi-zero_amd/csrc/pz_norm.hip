@@ -294,6 +294,18 @@ __global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restr
   if (c < D) {
     const float* src = part + c;
     int64_t p = pl;
+    // 16 loads in flight per thread (the norm-backward partials: P = rows / 16, e.g. 1104 x 2048 -> 17 per
+    // part-lane, one round instead of five), summed in a fixed tree
+    for (; p + 15 * PL < P; p += 16 * PL) {
+      f32x4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const f32x4*>(src + (p + u * PL) * D);
+#pragma unroll
+      for (int w = 8; w > 0; w >>= 1)
+#pragma unroll
+        for (int u = 0; u < w; ++u) v[u] += v[u + w];
+      s += v[0];
+    }
     for (; p + 3 * PL < P; p += 4 * PL) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(src + p * D);
       const f32x4 b = *reinterpret_cast<const f32x4*>(src + (p + PL) * D);
@@ -305,9 +317,14 @@ __global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restr
   }
   red[pl][ct] = s;
   __syncthreads();
+  // fold the part-lanes as a fixed tree (log2(PL) barrier steps instead of PL - 1 dependent LDS reads)
+#pragma unroll
+  for (int w = PL / 2; w > 0; w >>= 1) {
+    if (pl < w) red[pl][ct] += red[pl + w][ct];
+    __syncthreads();
+  }
   if (pl == 0 && c < D) {
-#pragma unroll 8
-    for (int i = 1; i < PL; ++i) s += red[i][ct];
+    s = red[0][ct];
     u32x2 o;
     if (beta) {
       const u32x2 prev = *reinterpret_cast<const u32x2*>(out + c);
@@ -350,7 +367,20 @@ __global__ void __launch_bounds__(256) colsum8_pass1(const bf16_t* __restrict__ 
   const int64_t r1 = min(M, r0 + rpc);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < N) {
-    for (int64_t r = r0 + rl; r < r1; r += 8) {
+    int64_t r = r0 + rl;
+    for (; r + 56 < r1; r += 64) {  // 8 rows' 16-B loads in flight per thread
+      u32x4 w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = *reinterpret_cast<const u32x4*>(X + (r + 8 * u) * ld + c);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[2 * e] += __uint_as_float(w[u][e] << 16);
+          s[2 * e + 1] += __uint_as_float(w[u][e] & 0xffff0000u);
+        }
+    }
+    for (; r < r1; r += 8) {
       float v[8];
       load8(X + r * ld + c, v);
 #pragma unroll
@@ -368,6 +398,45 @@ __global__ void __launch_bounds__(256) colsum8_pass1(const bf16_t* __restrict__ 
     for (int i = 0; i < 8; ++i) t += red[i][j];
     ws[blockIdx.y * N + c0 + j] = t;
   }
+}
+
+// GELU / SiLU backward fused with the bias gradient (SigLIP fc1: siglip.py:183-192 autograd): dpre = dh * act'(pre)
+// (act_bwd8's arithmetic; dpre may alias dh), and the column sums of the bf16 dpre over this workgroup's rpc rows
+// -> ws[chunk][N] (fp32, fixed order), folded by reduce_parts.  Thread = 8 columns, 8 rows' loads in flight.
+__global__ void __launch_bounds__(256) act_bwd_colsum8_kernel(const bf16_t* dh, int64_t lddh, const bf16_t* pre,
+                                                              int64_t ldpre, bf16_t* dpre, int64_t M, int64_t N,
+                                                              int64_t rpc, int act, float* ws) {
+  const int64_t c = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto row = [&](const u32x4& xp, const u32x4& xd, int64_t r) {
+    float x[8], d[8];
+    unpack8(xp, x);
+    unpack8(xd, d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[e] = bf2f(f2bf(d[e] * (act == PZ_EPI_GELU ? gelu_tanh_grad(x[e]) : silu_grad(x[e]))));
+      s[e] += x[e];
+    }
+    store8(dpre + r * ldpre + c, x);
+  };
+  int64_t r = r0;
+  for (; r + 7 < r1; r += 8) {  // 8 rows' loads in flight
+    u32x4 xp[8], xd[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xp[u] = *reinterpret_cast<const u32x4*>(pre + (r + u) * ldpre + c);
+      xd[u] = *reinterpret_cast<const u32x4*>(dh + (r + u) * lddh + c);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) row(xp[u], xd[u], r + u);
+  }
+  for (; r < r1; ++r)
+    row(*reinterpret_cast<const u32x4*>(pre + r * ldpre + c), *reinterpret_cast<const u32x4*>(dh + r * lddh + c), r);
+  float* w = ws + (int64_t)blockIdx.y * N + c;
+  *reinterpret_cast<f32x4*>(w) = f32x4{s[0], s[1], s[2], s[3]};
+  *reinterpret_cast<f32x4*>(w + 4) = f32x4{s[4], s[5], s[6], s[7]};
 }
 
 __global__ void batch_sum_kernel(const bf16_t* __restrict__ X, int64_t B, int64_t stride, int64_t n,
@@ -394,7 +463,8 @@ template <bool LN>
 __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
     const bf16_t* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
-    const bf16_t* dres, bf16_t* dx, int64_t lddx, float* dw_part, float* db_part, int64_t R, int D) {
+    const bf16_t* dres, bf16_t* dx, int64_t lddx, float* dw_part, float* db_part, int64_t R, int D,
+    float* dx_part) {
   __shared__ float red[2][2][4];  // [row parity][sum][wave]
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const bool act = t < D / 8;
@@ -404,9 +474,10 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
 #pragma unroll
     for (int i = 0; i < 8; ++i) wv[i] = 0.f;
   }
-  float dwa[8], dba[8];
+  float dwa[8], dba[8], dxa[8];  // dxa: column sums of the bf16 dx (dx_part: the bias gradient of the Linear
+                                 // whose output gradient dx is -- SigLIP fc2 / out_proj, colsum fused)
 #pragma unroll
-  for (int i = 0; i < 8; ++i) dwa[i] = dba[i] = 0.f;
+  for (int i = 0; i < 8; ++i) dwa[i] = dba[i] = dxa[i] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
   const int nrows = (int)(R - r0 < ROWS_PER_PART ? R - r0 : ROWS_PER_PART);
   const u32x4 z4 = {0u, 0u, 0u, 0u};
@@ -466,12 +537,21 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
         for (int e = 0; e < 8; ++e) o[e] += r * g[e] - k * xv[e];
       }
       store8(dx + row * lddx + t * 8, o);
+      if (dx_part) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dxa[e] += bf2f(f2bf(o[e]));
+      }
     }
     xr = xn;
     dyr = dyn;
     drr = drn;
   }
   if (!act) return;
+  if (dx_part) {
+    float* d = dx_part + (int64_t)blockIdx.x * D + t * 8;
+    *reinterpret_cast<f32x4*>(d) = f32x4{dxa[0], dxa[1], dxa[2], dxa[3]};
+    *reinterpret_cast<f32x4*>(d + 4) = f32x4{dxa[4], dxa[5], dxa[6], dxa[7]};
+  }
   if (dw_part) {
     float* d = dw_part + (int64_t)blockIdx.x * D + t * 8;
     *reinterpret_cast<f32x4*>(d) = f32x4{dwa[0], dwa[1], dwa[2], dwa[3]};
@@ -530,7 +610,7 @@ extern "C" int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16))
     hipLaunchKernelGGL(norm_bwd_row_kernel<false>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
                        ldx, (const bf16_t*)w, nullptr, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, nullptr,
-                       R, (int)D);
+                       R, (int)D, nullptr);
   else
     NORM_DISPATCH(rmsnorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
                   rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, R, (int)D);
@@ -553,7 +633,7 @@ extern "C" int pz_layernorm_fwd(const void* x, int64_t ldx, const void* w, const
 
 extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, const void* w,
                                 const float* mean, const float* rstd, const void* dres, void* dx, int64_t lddx,
-                                float* dw_part, float* db_part, int64_t R, int64_t D, void* stream) {
+                                float* dw_part, float* db_part, int64_t R, int64_t D, float* dx_part, void* stream) {
   int e = check_norm(x, ldx, dx, lddx, D);
   if (e) return e;
   PZ_CHECK_ARG(lddy % 8 == 0, "layernorm_bwd: lddy");
@@ -564,7 +644,10 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
       PZ_ALIGNED(db_part, 16))
     hipLaunchKernelGGL(norm_bwd_row_kernel<true>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
                        ldx, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R,
-                       (int)D);
+                       (int)D, dx_part);
+  else if (dx_part)
+    PZ_CHECK_ARG(false, "layernorm_bwd: dx_part (fused column sums of dx) needs the row kernel (16-byte aligned "
+                        "dy / dres / partials, PZ_NORM_BWD != wave)");
   else
     NORM_DISPATCH(layernorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
                   mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D);
@@ -614,6 +697,28 @@ extern "C" int pz_colsum(const void* X, int64_t ld, int64_t M, int64_t N, void* 
   }
   PZ_CHECK_LAUNCH();
   launch_reduce_parts(ws, chunks, N, (bf16_t*)out, (int)beta, st);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_act_bwd_colsum(const void* dh, int64_t lddh, const void* pre, int64_t ldpre, void* dpre, int64_t M,
+                                 int64_t N, int32_t act, float* ws, int64_t ws_rows, void* dbias, int32_t beta,
+                                 void* stream) {
+  PZ_CHECK_ARG(dh && pre && dpre && ws && dbias && M > 0 && N > 0 && ws_rows > 0 &&
+                   (act == PZ_EPI_GELU || act == PZ_EPI_SILU),
+               "act_bwd_colsum: bad args");
+  PZ_CHECK_ARG(N % 8 == 0 && lddh % 8 == 0 && ldpre % 8 == 0 && PZ_ALIGNED(dh, 16) && PZ_ALIGNED(pre, 16) &&
+                   PZ_ALIGNED(dpre, 16) && PZ_ALIGNED(ws, 16),
+               "act_bwd_colsum: N, strides %% 8 and 16-byte alignment");
+  hipStream_t st = (hipStream_t)stream;
+  // row chunks: up to ws_rows partial rows, >= 16 rows each (3072 workgroups for the SigLIP fc1 gradient at 1024)
+  int64_t chunks = ws_rows < (M + 15) / 16 ? ws_rows : (M + 15) / 16;
+  const int64_t rpc = (M + chunks - 1) / chunks;
+  chunks = (M + rpc - 1) / rpc;
+  hipLaunchKernelGGL(act_bwd_colsum8_kernel, dim3((unsigned)((N / 8 + 255) / 256), (unsigned)chunks), dim3(256), 0, st,
+                     (const bf16_t*)dh, lddh, (const bf16_t*)pre, ldpre, (bf16_t*)dpre, M, N, rpc, (int)act, ws);
+  PZ_CHECK_LAUNCH();
+  launch_reduce_parts(ws, chunks, N, (bf16_t*)dbias, (int)beta, st);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -118,7 +118,8 @@ SIGNATURES = {
     "pz_rmsnorm_fwd": [vp, i64, vp, vp, i64, vp, i64, i64, f32, vp],
     "pz_rmsnorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, i64, vp],
     "pz_layernorm_fwd": [vp, i64, vp, vp, vp, i64, vp, vp, i64, i64, f32, vp],
-    "pz_layernorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, vp, vp, i64, i64, vp],
+    "pz_layernorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, vp, vp, i64, i64, vp, vp],
+    "pz_act_bwd_colsum": [vp, i64, vp, i64, vp, i64, i64, i32, vp, i64, vp, i32, vp],
     "pz_norm_rows_per_part": [],
     "pz_reduce_parts": [vp, i64, i64, vp, i32, vp],
     "pz_colsum": [vp, i64, i64, i64, vp, i32, vp, vp],

@@ -314,6 +314,15 @@ class Engine:
             self._tables[key] = cs
         return self._tables[key]
 
+    def colsum_ws_rows(self, rows, n):
+        """fp32 [rows, n] partial-sum scratch (pz_act_bwd_colsum), one per device, grown on demand"""
+        dev = self.ar.data.device
+        t = self._ws.get(("colsum_rows", dev))
+        if t is None or t.numel() < rows * n:
+            t = torch.empty(rows * n, device=dev, dtype=F32)
+            self._ws[("colsum_rows", dev)] = t
+        return t[: rows * n].view(rows, n)
+
     def colsum_ws(self, n):
         dev = self.ar.data.device
         t = self._ws.get(("colsum", dev))
@@ -449,6 +458,12 @@ class Engine:
         ws = self.colsum_ws(max(d.vI, 3 * d.vH))
         pw = torch.empty(P, d.vH, device=dev, dtype=F32)
         pb = torch.empty(P, d.vH, device=dev, dtype=F32)
+        # bias gradients fused into the passes that produce their output gradients (LayerNorm backward -> the
+        # column sums of dx: fc2 / out_proj; GELU backward -> fc1); PZ_FUSED_BIAS_GRAD=0: separate colsum passes
+        fb = os.environ.get("PZ_FUSED_BIAS_GRAD", "1") != "0" and os.environ.get("PZ_NORM_BWD", "row")[:1] != "w"
+        pd = torch.empty(P, d.vH, device=dev, dtype=F32) if fb else None  # column partials of the current dx
+        pd2 = torch.empty(P, d.vH, device=dev, dtype=F32) if fb else None  # ... of dxm
+        ws_act = self.colsum_ws_rows(1024, d.vI) if fb else None
         # projector
         nm = "multi_modal_projector.linear."
         if self.rg(nm + "weight"):
@@ -459,7 +474,7 @@ class Engine:
         ops.linear_dgrad(dimg, self.w(nm + "weight"), dy)
         dx = torch.empty_like(dy)
         ops.layernorm_bwd(dy, sv["x_last"], self.w(vt + "post_layernorm.weight"), sv["mu"], sv["r"], dx,
-                          dw_part=pw, db_part=pb)
+                          dw_part=pw, db_part=pb, dx_part=pd)
         self._norm_grads(vt + "post_layernorm.", pw, pb, beta)
         nh, hd = d.vheads, d.vH // d.vheads
         Np = d.img_tok
@@ -475,29 +490,39 @@ class Engine:
             st = sv["layers"][i]
             # MLP: x' = xm + fc2(gelu(fc1(ln2(xm))))
             # dgrad through fc2, then the GELU derivative at the saved pre-activation a1
+            fc1b = self.rg(p + "mlp.fc1.bias")
             if self.split_dact:  # plain dgrad GEMM, then the GELU backward (HBM-bound) in place
                 ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg)
-                ops.act_bwd(dg, st["a1"], dg, None, PZ_EPI_GELU)
+                if fb and fc1b:  # + the fc1 bias gradient from the same pass
+                    ops.act_bwd_colsum(dg, st["a1"], dg, PZ_EPI_GELU, ws_act, self.gw(p + "mlp.fc1.bias"), beta=beta)
+                else:
+                    ops.act_bwd(dg, st["a1"], dg, None, PZ_EPI_GELU)
             else:
                 ops.linear_dgrad(dx, self.w(p + "mlp.fc2.weight"), dg, epi=PZ_EPI_DGELU, aux=st["a1"])
             if self.rg(p + "mlp.fc2.weight"):
                 ops.linear_wgrad(dx, st["g1"], self.gw(p + "mlp.fc2.weight"), beta=beta)
             st["g1"] = None
             if self.rg(p + "mlp.fc2.bias"):
-                ops.colsum(dx, self.gw(p + "mlp.fc2.bias"), ws, beta=beta)
+                if fb:  # column sums of dx from the LayerNorm backward that produced it
+                    ops.reduce_parts(pd, self.gw(p + "mlp.fc2.bias"), beta=beta)
+                else:
+                    ops.colsum(dx, self.gw(p + "mlp.fc2.bias"), ws, beta=beta)
             if self.rg(p + "mlp.fc1.weight"):
                 ops.linear_wgrad(dg, st["h2"], self.gw(p + "mlp.fc1.weight"), beta=beta)
-            if self.rg(p + "mlp.fc1.bias"):
+            if fc1b and not (fb and self.split_dact):
                 ops.colsum(dg, self.gw(p + "mlp.fc1.bias"), ws, beta=beta)
             ops.linear_dgrad(dg, self.w(p + "mlp.fc1.weight"), dh)
             ops.layernorm_bwd(dh, st["xm"], self.w(p + "layer_norm2.weight"), st["mu2"], st["r2"], dxm, dres=dx,
-                              dw_part=pw, db_part=pb)
+                              dw_part=pw, db_part=pb, dx_part=pd2)
             self._norm_grads(p + "layer_norm2.", pw, pb, beta)
             # attention out-proj
             if self.rg(p + "self_attn.out_proj.weight"):
                 ops.linear_wgrad(dxm, st["O"], self.gw(p + "self_attn.out_proj.weight"), beta=beta)
             if self.rg(p + "self_attn.out_proj.bias"):
-                ops.colsum(dxm, self.gw(p + "self_attn.out_proj.bias"), ws, beta=beta)
+                if fb:
+                    ops.reduce_parts(pd2, self.gw(p + "self_attn.out_proj.bias"), beta=beta)
+                else:
+                    ops.colsum(dxm, self.gw(p + "self_attn.out_proj.bias"), ws, beta=beta)
             ops.linear_dgrad(dxm, self.w(p + "self_attn.out_proj.weight"), dO)
             # fused attention backward: dQ | dK | dV straight into the q|k|v gradient rows
             ops.flash_bwd(ops.siglip_flash_args(st["qkv"], st["O"], st["lse"], B, nh, hd, Np, dO=dO, delta=delta,
@@ -515,7 +540,7 @@ class Engine:
             ops.linear_dgrad(dqkv, self.qkv_siglip(p), dh)
             dxn = torch.empty_like(dx)
             ops.layernorm_bwd(dh, st["x"], self.w(p + "layer_norm1.weight"), st["mu1"], st["r1"], dxn, dres=dxm,
-                              dw_part=pw, db_part=pb)
+                              dw_part=pw, db_part=pb, dx_part=pd)
             self._norm_grads(p + "layer_norm1.", pw, pb, beta)
             dx = dxn
             self._notify("vision", i)

@@ -293,11 +293,21 @@ def layernorm(x, w, b, y, mean, rstd, eps):
     return y
 
 
-def layernorm_bwd(dy, x, w, mean, rstd, dx, dres=None, dw_part=None, db_part=None):
+def layernorm_bwd(dy, x, w, mean, rstd, dx, dres=None, dw_part=None, db_part=None, dx_part=None):
+    """dx_part: per-part column sums of the bf16 dx (reduce_parts -> the bias gradient of the Linear whose output
+    gradient dx is)"""
     R, D = x.shape
     call("pz_layernorm_bwd", _p(dy), dy.stride(0), _p(x), x.stride(0), _p(w), _p(mean), _p(rstd), _p(dres),
-         _p(dx), dx.stride(0), _p(dw_part), _p(db_part), R, D, _st())
+         _p(dx), dx.stride(0), _p(dw_part), _p(db_part), R, D, _p(dx_part), _st())
     return dx
+
+
+def act_bwd_colsum(dh, pre, dpre, act, ws, dbias, beta=False):
+    """dpre = dh * act'(pre) (dpre may alias dh) and dbias (+)= colsum(dpre) in one pass; ws fp32 [rows >= 16, N]"""
+    M, N = pre.shape
+    call("pz_act_bwd_colsum", _p(dh), dh.stride(0), _p(pre), pre.stride(0), _p(dpre), M, N, int(act), _p(ws),
+         ws.numel() // N, _p(dbias), int(beta), _st())
+    return dpre
 
 
 _RPP = None

@@ -560,6 +560,34 @@ def test_layernorm_fwd_bwd(kern, monkeypatch):
     ws = torch.empty(64 * D, device=dev)
     ops.colsum(dy, db2, ws)
     close(db2, dy.float().sum(0), atol=0.1)
+    if kern == "row":  # fused column sums of the bf16 dx (+ residual gradient): the next Linear's bias gradient
+        dres = bf(R, D)
+        dx2, pd = torch.empty_like(x), torch.empty(P, D, device=dev)
+        ops.layernorm_bwd(dy, x, w, mean, rstd, dx2, dres=dres, dw_part=pw, db_part=pb, dx_part=pd)
+        close(dx2, xr.grad + dres.float(), atol=3e-2)
+        s1, s2 = torch.empty(D, device=dev, dtype=torch.bfloat16), torch.empty(D, device=dev, dtype=torch.bfloat16)
+        ops.reduce_parts(pd, s1)
+        ops.colsum(dx2, s2, ws)
+        close(s1, dx2.float().sum(0), atol=0.1)
+        assert (s1.float() - s2.float()).abs().max().item() <= 2 * 2 ** -7 * s2.float().abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("M,N,act", [(16384, 4304, "gelu"), (300, 1152, "gelu"), (320, 4096, "silu"), (17, 64, "gelu")])
+def test_act_bwd_colsum_matches_unfused(M, N, act):
+    """pz_act_bwd_colsum (GELU / SiLU backward + the bias gradient in one pass, SigLIP fc1) vs pz_act_bwd + pz_colsum:
+    dpre bit-identical, the column sums within fp32 summation-order noise, beta accumulation."""
+    from pizero_native import ops
+
+    a = ops.PZ_EPI_GELU if act == "gelu" else ops.PZ_EPI_SILU
+    dh, pre = bf(M, N), bf(M, N) * 2
+    d1, d2 = dh.clone(), dh.clone()
+    ops.act_bwd(d1, pre, d1, None, a)
+    ws = torch.empty(256, N, device=dev)
+    b2 = torch.full((N,), 0.5, device=dev, dtype=torch.bfloat16)
+    ops.act_bwd_colsum(d2, pre, d2, a, ws, b2, beta=True)  # in place, as the engine calls it
+    assert torch.equal(d1, d2)
+    ref = 0.5 + d1.float().sum(0)
+    close(b2, ref, rtol=2e-2, atol=0.05 + 1e-4 * math.sqrt(M))
 
 
 @pytest.mark.parametrize("M,N", [(16384, 1152), (17664, 2048), (300, 4304), (5, 7), (1000, 40), (64, 3456), (257, 1024)])

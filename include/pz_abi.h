@@ -133,6 +133,13 @@ int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int64_t ldx, c
 int64_t pz_norm_rows_per_part(void);
 /* out[n] (+)= sum_p part[p*D + n]  -> bf16 (parameter gradient of a norm weight/bias) */
 int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream);
+/* (ABI 15) several pz_reduce_parts in one launch (a SigLIP layer's LayerNorm weight / bias and Linear bias
+ * gradients, reduced together once the layer's backward is done): segment i = (part [P][D] fp32, out [D] bf16,
+ * beta), D % 4 == 0, 16-byte aligned partials, 8-byte aligned out; any number of segments (8 per launch) */
+typedef struct pz_reduce_seg {
+  const float* part; int64_t P, D; void* out; int32_t beta;
+} pz_reduce_seg;
+int pz_reduce_parts_multi(const pz_reduce_seg* segs, int32_t nseg, void* stream);
 /* (ABI 15) pz_layernorm_bwd's dx_part (NULL ok): per-part column sums of the bf16 dx, [ceil(R / rows_per_part)][D]
  * fp32 -- reduce_parts of them is the bias gradient of the Linear whose output gradient dx is (SigLIP fc2 /
  * out_proj, siglip.py:183-192 / 103-106 autograd), without re-reading dx.

@@ -2114,7 +2114,7 @@ struct Plan {
   int wm, tag, skinny_w, skinny_nc, skinny_mb, splits;
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
-  int rows_w, rows_tnb;           // row-slab kernel: waves, 16-column blocks per tile
+  int rows_w, rows_tnb, rows_tmb;  // row-slab kernel: waves, 16-column / 16-row blocks per tile
 };
 
 // compute units of the current device (the "wave" of resident 8-phase workgroups: 1 per CU)
@@ -2178,7 +2178,10 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
       a->epilogue >= PZ_EPI_DGELU || a->norm_w)
     return false;
   if (!(er && er[0] == '1') && (a->K > 2048 || ncols > 4096)) return false;
-  const int64_t tm = (a->M + 63) / 64;
+  // 16-row blocks per tile: 4 (64 rows); PZ_ROWS_TMB=2 (32-row tiles, twice the workgroups) for A/B runs
+  const char* eb = getenv("PZ_ROWS_TMB");
+  const int tmb = (eb && atoi(eb) == 2 && !pl.geglu) ? 2 : 4;
+  const int64_t tm = (a->M + 16 * tmb - 1) / (16 * tmb);
   int tnb = pl.geglu ? 2 : 4;
   while (tnb > 1 && tm * ((ncols + 16 * tnb - 1) / (16 * tnb)) < 128) tnb /= 2;
   pl.kind = PATH_ROWS;
@@ -2188,6 +2191,7 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   const char* et = getenv("PZ_ROWS_TNB");
   if (et && (atoi(et) == 1 || atoi(et) == 2 || (atoi(et) == 4 && !pl.geglu))) tnb = atoi(et);
   pl.rows_tnb = tnb;
+  pl.rows_tmb = tmb;
   pl.tiles_m = tm;
   pl.tiles_n = (ncols + 16 * tnb - 1) / (16 * tnb);
   return true;
@@ -2364,7 +2368,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
       break;
     case PATH_ROWS:
-      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, 4, %d, %s>", pl.rows_w, pl.rows_tnb, bstr(pl.geglu));
+      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
+               bstr(pl.geglu));
       break;
     case PATH_SPLIT:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
@@ -2652,7 +2657,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
-  if (pl.kind == PATH_ROWS) return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, pl.geglu, st);
+  if (pl.kind == PATH_ROWS) return pz_rows_launch(p, pl.rows_w, pl.rows_tmb, pl.rows_tnb, pl.geglu, st);
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {
       p.ws = (float*)a->workspace;

@@ -377,10 +377,10 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
 
 }  // namespace
 
-template <int W, int TNB, bool GEGLU>
+template <int W, int TMB, int TNB, bool GEGLU>
 static int launch_rows_k(const GemmP& p, hipStream_t st) {
-  constexpr int smem = W * (GEGLU ? 2 : 1) * 4 * TNB * 1024;
-  auto kern = gemm_rows_kernel<W, 4, TNB, GEGLU>;
+  constexpr int smem = W * (GEGLU ? 2 : 1) * TMB * TNB * 1024;
+  auto kern = gemm_rows_kernel<W, TMB, TNB, GEGLU>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -392,15 +392,20 @@ static int launch_rows_k(const GemmP& p, hipStream_t st) {
 }
 
 template <int W>
-static int launch_rows_w(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
-  if (geglu) return tnb == 2 ? launch_rows_k<W, 2, true>(p, st) : launch_rows_k<W, 1, true>(p, st);
-  if (tnb == 4) return launch_rows_k<W, 4, false>(p, st);
-  if (tnb == 2) return launch_rows_k<W, 2, false>(p, st);
-  return launch_rows_k<W, 1, false>(p, st);
+static int launch_rows_w(const GemmP& p, int tmb, int tnb, bool geglu, hipStream_t st) {
+  if (geglu) return tnb == 2 ? launch_rows_k<W, 4, 2, true>(p, st) : launch_rows_k<W, 4, 1, true>(p, st);
+  if (tmb == 2) {
+    if (tnb == 4) return launch_rows_k<W, 2, 4, false>(p, st);
+    if (tnb == 2) return launch_rows_k<W, 2, 2, false>(p, st);
+    return launch_rows_k<W, 2, 1, false>(p, st);
+  }
+  if (tnb == 4) return launch_rows_k<W, 4, 4, false>(p, st);
+  if (tnb == 2) return launch_rows_k<W, 4, 2, false>(p, st);
+  return launch_rows_k<W, 4, 1, false>(p, st);
 }
 
-int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, hipStream_t st) {
-  return w == 8 ? launch_rows_w<8>(p, tnb, geglu, st) : launch_rows_w<4>(p, tnb, geglu, st);
+int pz_rows_launch(const GemmP& p, int w, int tmb, int tnb, bool geglu, hipStream_t st) {
+  return w == 8 ? launch_rows_w<8>(p, tmb, tnb, geglu, st) : launch_rows_w<4>(p, tmb, tnb, geglu, st);
 }
 
 template <int W, int NC, int MB, bool F8W>

@@ -3,6 +3,8 @@
 //   Gemma RMSNorm (paligemma/modules.py:7-21) and SigLIP LayerNorm
 //   (siglip.py:211,217,290), forward + backward, plus the column reductions
 //   used for norm-weight / bias / position-embedding gradients.
+#include <string.h>
+
 #include "pz_common.h"
 
 namespace {
@@ -284,12 +286,12 @@ __global__ void reduce_parts_kernel(const float* __restrict__ part, int64_t P, i
 // 4*CT columns; CT column-threads read float4s, 256/CT part-lanes stride over P (4 loads in flight),
 // then the part-lanes are folded through LDS in a fixed order (deterministic, run to run).
 template <int CT>
-__global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restrict__ part, int64_t P,
-                                                            int64_t D, bf16_t* out, int beta) {
+__device__ __forceinline__ void reduce_parts4_body(const float* __restrict__ part, int64_t P, int64_t D, bf16_t* out,
+                                                   int beta, int64_t bid) {
   constexpr int PL = 256 / CT;
   __shared__ f32x4 red[PL][CT];
   const int ct = threadIdx.x % CT, pl = threadIdx.x / CT;
-  const int64_t c = ((int64_t)blockIdx.x * CT + ct) * 4;
+  const int64_t c = (bid * CT + ct) * 4;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (c < D) {
     const float* src = part + c;
@@ -337,6 +339,29 @@ __global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restr
     o[1] = pack2bf(s[2], s[3]);
     *reinterpret_cast<u32x2*>(out + c) = o;
   }
+}
+
+template <int CT>
+__global__ void __launch_bounds__(256) reduce_parts4_kernel(const float* __restrict__ part, int64_t P,
+                                                            int64_t D, bf16_t* out, int beta) {
+  reduce_parts4_body<CT>(part, P, D, out, beta, blockIdx.x);
+}
+
+// several independent reductions in one launch (a layer's norm weight / bias and Linear bias gradients):
+// workgroup ranges [blk0[i], blk0[i + 1]) belong to segment i
+constexpr int RED_MAXSEG = 8;
+struct RedSegs {
+  const float* part[RED_MAXSEG];
+  bf16_t* out[RED_MAXSEG];
+  int64_t P[RED_MAXSEG], D[RED_MAXSEG];
+  int beta[RED_MAXSEG], blk0[RED_MAXSEG + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) reduce_parts4_multi_kernel(RedSegs a) {
+  int i = 0;
+  while (i + 1 < a.n && (int)blockIdx.x >= a.blk0[i + 1]) ++i;  // workgroup-uniform
+  reduce_parts4_body<4>(a.part[i], a.P[i], a.D[i], a.out[i], a.beta[i], (int64_t)blockIdx.x - a.blk0[i]);
 }
 
 // column sums of a bf16 matrix: pass 1 -> ws[chunk][n], pass 2 -> out
@@ -676,6 +701,38 @@ static void launch_reduce_parts(const float* part, int64_t P, int64_t D, bf16_t*
 extern "C" int pz_reduce_parts(const float* part, int64_t P, int64_t D, void* out, int32_t beta, void* stream) {
   PZ_CHECK_ARG(part && out && P > 0 && D > 0, "reduce_parts: bad args");
   launch_reduce_parts(part, P, D, (bf16_t*)out, (int)beta, (hipStream_t)stream);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_reduce_parts_multi(const pz_reduce_seg* segs, int32_t nseg, void* stream) {
+  PZ_CHECK_ARG(segs && nseg > 0, "reduce_parts_multi: bad args");
+  RedSegs a;
+  memset(&a, 0, sizeof(a));
+  hipStream_t st = (hipStream_t)stream;
+  int blocks = 0;
+  for (int32_t i = 0; i < nseg; ++i) {
+    const pz_reduce_seg& g = segs[i];
+    PZ_CHECK_ARG(g.part && g.out && g.P > 0 && g.D > 0 && g.D % 4 == 0 && PZ_ALIGNED(g.part, 16) && PZ_ALIGNED(g.out, 8),
+                 "reduce_parts_multi: segment %d needs D %% 4 == 0, 16-byte aligned partials, 8-byte aligned out", i);
+    if (a.n == RED_MAXSEG) {  // flush a full table
+      a.blk0[a.n] = blocks;
+      hipLaunchKernelGGL(reduce_parts4_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
+      PZ_CHECK_LAUNCH();
+      memset(&a, 0, sizeof(a));
+      blocks = 0;
+    }
+    const int k = a.n++;
+    a.part[k] = g.part;
+    a.out[k] = (bf16_t*)g.out;
+    a.P[k] = g.P;
+    a.D[k] = g.D;
+    a.beta[k] = g.beta;
+    a.blk0[k] = blocks;
+    blocks += (int)((g.D + 15) / 16);
+  }
+  a.blk0[a.n] = blocks;
+  hipLaunchKernelGGL(reduce_parts4_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

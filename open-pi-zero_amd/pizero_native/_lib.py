@@ -98,6 +98,10 @@ class QkvRopeArgs(C.Structure):
     ]
 
 
+class ReduceSeg(C.Structure):
+    _fields_ = [("part", vp), ("P", i64), ("D", i64), ("out", vp), ("beta", i32)]
+
+
 class DecodeAttnArgs(C.Structure):
     _fields_ = [
         ("q", vp), ("ldq", i64), ("Lq", i64), ("qoff", i64), ("k", vp), ("v", vp), ("k_bstride", i64),
@@ -120,6 +124,7 @@ SIGNATURES = {
     "pz_layernorm_fwd": [vp, i64, vp, vp, vp, i64, vp, vp, i64, i64, f32, vp],
     "pz_layernorm_bwd": [vp, i64, vp, i64, vp, vp, vp, vp, vp, i64, vp, vp, i64, i64, vp, vp],
     "pz_act_bwd_colsum": [vp, i64, vp, i64, vp, i64, i64, i32, vp, i64, vp, i32, vp],
+    "pz_reduce_parts_multi": [vp, i32, vp],
     "pz_norm_rows_per_part": [],
     "pz_reduce_parts": [vp, i64, i64, vp, i32, vp],
     "pz_colsum": [vp, i64, i64, i64, vp, i32, vp, vp],

@@ -462,7 +462,13 @@ class Engine:
         # column sums of dx: fc2 / out_proj; GELU backward -> fc1); PZ_FUSED_BIAS_GRAD=0: separate colsum passes
         fb = os.environ.get("PZ_FUSED_BIAS_GRAD", "1") != "0" and os.environ.get("PZ_NORM_BWD", "row")[:1] != "w"
         pd = torch.empty(P, d.vH, device=dev, dtype=F32) if fb else None  # column partials of the current dx
+        pdn = torch.empty(P, d.vH, device=dev, dtype=F32) if fb else None  # ... of the next layer's dx
         pd2 = torch.empty(P, d.vH, device=dev, dtype=F32) if fb else None  # ... of dxm
+        # a layer's LayerNorm weight / bias and Linear bias reductions go out as one launch at its end
+        # (pz_reduce_parts_multi; PZ_REDUCE_MULTI=0: one launch each)
+        multi = os.environ.get("PZ_REDUCE_MULTI", "1") != "0"
+        pw2 = torch.empty(P, d.vH, device=dev, dtype=F32) if multi else pw
+        pb2 = torch.empty(P, d.vH, device=dev, dtype=F32) if multi else pb
         ws_act = self.colsum_ws_rows(1024, d.vI) if fb else None
         # projector
         nm = "multi_modal_projector.linear."
@@ -488,6 +494,7 @@ class Engine:
         for i in reversed(range(d.vL)):
             p = f"{vt}encoder.layers.{i}."
             st = sv["layers"][i]
+            red = [] if multi else None  # deferred (partials, gradient) reductions of this layer
             # MLP: x' = xm + fc2(gelu(fc1(ln2(xm))))
             # dgrad through fc2, then the GELU derivative at the saved pre-activation a1
             fc1b = self.rg(p + "mlp.fc1.bias")
@@ -504,7 +511,7 @@ class Engine:
             st["g1"] = None
             if self.rg(p + "mlp.fc2.bias"):
                 if fb:  # column sums of dx from the LayerNorm backward that produced it
-                    ops.reduce_parts(pd, self.gw(p + "mlp.fc2.bias"), beta=beta)
+                    self._reduce(red, pd, self.gw(p + "mlp.fc2.bias"), beta)
                 else:
                     ops.colsum(dx, self.gw(p + "mlp.fc2.bias"), ws, beta=beta)
             if self.rg(p + "mlp.fc1.weight"):
@@ -513,14 +520,14 @@ class Engine:
                 ops.colsum(dg, self.gw(p + "mlp.fc1.bias"), ws, beta=beta)
             ops.linear_dgrad(dg, self.w(p + "mlp.fc1.weight"), dh)
             ops.layernorm_bwd(dh, st["xm"], self.w(p + "layer_norm2.weight"), st["mu2"], st["r2"], dxm, dres=dx,
-                              dw_part=pw, db_part=pb, dx_part=pd2)
-            self._norm_grads(p + "layer_norm2.", pw, pb, beta)
+                              dw_part=pw2, db_part=pb2, dx_part=pd2)
+            self._norm_grads(p + "layer_norm2.", pw2, pb2, beta, red)
             # attention out-proj
             if self.rg(p + "self_attn.out_proj.weight"):
                 ops.linear_wgrad(dxm, st["O"], self.gw(p + "self_attn.out_proj.weight"), beta=beta)
             if self.rg(p + "self_attn.out_proj.bias"):
                 if fb:
-                    ops.reduce_parts(pd2, self.gw(p + "self_attn.out_proj.bias"), beta=beta)
+                    self._reduce(red, pd2, self.gw(p + "self_attn.out_proj.bias"), beta)
                 else:
                     ops.colsum(dxm, self.gw(p + "self_attn.out_proj.bias"), ws, beta=beta)
             ops.linear_dgrad(dxm, self.w(p + "self_attn.out_proj.weight"), dO)
@@ -540,8 +547,11 @@ class Engine:
             ops.linear_dgrad(dqkv, self.qkv_siglip(p), dh)
             dxn = torch.empty_like(dx)
             ops.layernorm_bwd(dh, st["x"], self.w(p + "layer_norm1.weight"), st["mu1"], st["r1"], dxn, dres=dxm,
-                              dw_part=pw, db_part=pb, dx_part=pd)
-            self._norm_grads(p + "layer_norm1.", pw, pb, beta)
+                              dw_part=pw, db_part=pb, dx_part=pdn)
+            self._norm_grads(p + "layer_norm1.", pw, pb, beta, red)
+            if red:
+                ops.reduce_parts_multi(red, beta=beta)
+            pd, pdn = pdn, pd  # this layer's dxn partials: the next (lower) layer's fc2 bias gradient
             dx = dxn
             self._notify("vision", i)
         # patch embedding + position embedding
@@ -562,11 +572,19 @@ class Engine:
     def qkv_siglip(self, p):
         return self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight")
 
-    def _norm_grads(self, prefix, pw, pb, beta):
+    def _norm_grads(self, prefix, pw, pb, beta, red=None):
         if pw is not None and self.rg(prefix + "weight"):
-            ops.reduce_parts(pw, self.gw(prefix + "weight"), beta=beta)
+            self._reduce(red, pw, self.gw(prefix + "weight"), beta)
         if pb is not None and self.rg(prefix + "bias"):
-            ops.reduce_parts(pb, self.gw(prefix + "bias"), beta=beta)
+            self._reduce(red, pb, self.gw(prefix + "bias"), beta)
+
+    @staticmethod
+    def _reduce(red, part, out, beta):
+        """reduce_parts now (red None) or deferred into the layer's list for one pz_reduce_parts_multi launch"""
+        if red is None:
+            ops.reduce_parts(part, out, beta=beta)
+        else:
+            red.append((part, out))
 
     # ============================================================ embeddings ==
     def embed_prefix(self, ids, img):

@@ -328,6 +328,18 @@ def reduce_parts(part, out, beta=False):
     return out
 
 
+def reduce_parts_multi(items, beta=False):
+    """[(part [P, D] fp32, out [D] bf16)]: every out (+)= the column sums of its part, one launch"""
+    from ._lib import ReduceSeg
+
+    if not items:
+        return
+    segs = (ReduceSeg * len(items))()
+    for s, (part, out) in zip(segs, items):
+        s.part, s.P, s.D, s.out, s.beta = _p(part), part.shape[0], part.shape[1], _p(out), int(beta)
+    call("pz_reduce_parts_multi", C.cast(segs, C.c_void_p), len(items), _st())
+
+
 def colsum(X, out, ws, beta=False):
     M, N = X.shape
     call("pz_colsum", _p(X), X.stride(0), M, N, _p(out), int(beta), _p(ws), _st())

@@ -572,6 +572,25 @@ def test_layernorm_fwd_bwd(kern, monkeypatch):
         assert (s1.float() - s2.float()).abs().max().item() <= 2 * 2 ** -7 * s2.float().abs().max().item() + 1e-3
 
 
+def test_reduce_parts_multi_matches_single():
+    """pz_reduce_parts_multi (a layer's partial-sum reductions in one launch, > 8 segments = two launches) is
+    bit-identical to one pz_reduce_parts per segment, beta included."""
+    from pizero_native import ops
+
+    shapes = [(1024, 1152), (1104, 2048), (3, 4), (64, 4304), (1024, 1152), (17, 256), (1, 8), (300, 1152), (5, 12)]
+    items, refs = [], []
+    for P, D in shapes:
+        part = torch.randn(P, D, device=dev)
+        out1 = bf(D)
+        out2 = out1.clone()
+        ops.reduce_parts(part, out1, beta=True)
+        items.append((part, out2))
+        refs.append(out1)
+    ops.reduce_parts_multi(items, beta=True)
+    for (part, o), r in zip(items, refs):
+        assert torch.equal(o, r), part.shape
+
+
 @pytest.mark.parametrize("M,N,act", [(16384, 4304, "gelu"), (300, 1152, "gelu"), (320, 4096, "silu"), (17, 64, "gelu")])
 def test_act_bwd_colsum_matches_unfused(M, N, act):
     """pz_act_bwd_colsum (GELU / SiLU backward + the bias gradient in one pass, SigLIP fc1) vs pz_act_bwd + pz_colsum:

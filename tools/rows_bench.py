@@ -60,7 +60,10 @@ def main():
                            ("rows w8", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_W": "8"}),
                            ("rows tnb1", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TNB": "1"}),
                            ("rows tnb2", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TNB": "2"}),
-                           ("rows tnb4", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TNB": "4"})]:
+                           ("rows tnb4", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TNB": "4"}),
+                           ("rows tmb2", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TMB": "2"}),
+                           ("rows tmb2 tnb2", {"PZ_ROWS_FIRST": "1", "PZ_GEMM_ROWS": "1", "PZ_ROWS_TMB": "2",
+                                               "PZ_ROWS_TNB": "2"})]:
             os.environ.update(env)
             kn = ops.gemm_kernel_name(M, N, K, epi=epi, **gi)
             ref = None

@@ -572,6 +572,50 @@ def test_layernorm_fwd_bwd(kern, monkeypatch):
         assert (s1.float() - s2.float()).abs().max().item() <= 2 * 2 ** -7 * s2.float().abs().max().item() + 1e-3
 
 
+@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True)])
+def test_gemm_column_split(akc, bkc, monkeypatch):
+    """N % 256 == 128 with >= one full round of 256-wide tiles (SigLIP's 1152-wide outputs at micro-batch 64):
+    the first N - 128 columns on the 8-phase kernel, the last 128 on the narrow path (pz_gemm column split,
+    opt-in PZ_GEMM_COLSPLIT=1: measured slower); every column-local epilogue against torch fp32 and against the
+    one-launch plan (PZ_GEMM_COLSPLIT=0)."""
+    from pizero_native import ops
+
+    M, N, K = 16384, 1152, 1152
+    monkeypatch.setenv("PZ_GEMM_COLSPLIT", "1")
+    name = ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc)
+    assert " | " in name, name
+    A = bf(M, K) if akc else bf(K, M)
+    Bm = bf(N, K, scale=K ** -0.5) if bkc else bf(K, N, scale=K ** -0.5)
+    lda, ldb = (K if akc else M), (K if bkc else N)
+    Af = A.float() if akc else A.float().t()
+    Bf = Bm.float() if bkc else Bm.float().t()
+    ref = Af @ Bf.t()
+    b, r = bf(N), bf(M, N)
+    outs = {}
+    for cs in ("1", "0"):
+        monkeypatch.setenv("PZ_GEMM_COLSPLIT", cs)
+        o1 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o1, N, bias=b, resid=r, ld_resid=N)
+        pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        o2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o2, N, bias=b, epi=ops.PZ_EPI_GELU, aux=pre, ld_aux=N)
+        o3 = torch.ones(M, N, device=dev, dtype=torch.float32)
+        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o3, N, beta=True)
+        o4 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o4, N, epi=ops.PZ_EPI_DGELU, aux=r, ld_aux=N)
+        outs[cs] = (o1, pre, o2, o3, o4)
+    o1, pre, o2, o3, o4 = outs["1"]
+    close(o1, ref + b.float() + r.float(), atol=2e-2)
+    close(pre, ref + b.float())
+    close(o2, torch.nn.functional.gelu(ref + b.float(), approximate="tanh"))
+    close(o3, 1.0 + ref, rtol=1e-3, atol=1e-3)
+    xr = r.float().requires_grad_()
+    torch.nn.functional.gelu(xr, approximate="tanh").backward(torch.ones_like(xr))
+    close(o4, ref * xr.grad, atol=2e-2)
+    for a_, b_ in zip(outs["1"], outs["0"]):  # the one-launch plan (its leftover tiles sum K-pieces: not bitwise)
+        close(a_, b_, rtol=2e-2, atol=2e-2)
+
+
 def test_reduce_parts_multi_matches_single():
     """pz_reduce_parts_multi (a layer's partial-sum reductions in one launch, > 8 segments = two launches) is
     bit-identical to one pz_reduce_parts per segment, beta included."""

@@ -198,8 +198,9 @@ def c5_inference(cfg, dev, iters):
     return {"metric": "action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
                       "1 proprio, chunk 50, B=1, prefill + 10 Euler steps)",
             "graph_ms": ms, "dtype": "bf16", "fp8_graph_ms": ms8,
-            "fp8": "e4m3 weights (per-tensor scales) for every SigLIP / vlm / action-expert Linear: prefill W8A8 "
-                   "on the fp8 MFMA (per-row activation scales), denoise W8A16",
+            "fp8": "e4m3 weights (per-tensor scales) for every SigLIP / vlm / action-expert Linear: prefill MLP "
+                   "GEMMs W8A8 on the fp8 MFMA (per-row activation scales), prefill q|k|v / o and denoise W8A16 "
+                   "(codes expanded to bf16); attention QK^T / PV bf16",
             "fp8_vs_bf16_chunk_rel_l2": rel, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
             "baseline_source": "Pi0 paper figure quoted in the reference README.md:80,84 (other hardware)",
             "vs_baseline": 73.0 / ms, "fp8_vs_baseline": 73.0 / ms8}

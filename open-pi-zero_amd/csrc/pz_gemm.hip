@@ -2115,6 +2115,7 @@ struct Plan {
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
   int rows_w, rows_tnb, rows_tmb;  // row-slab kernel: waves, 16-column / 16-row blocks per tile
+  bool rows_f8;                    // ... with e4m3 weight codes (W8A16)
 };
 
 // compute units of the current device (the "wave" of resident 8-phase workgroups: 1 per CU)
@@ -2173,11 +2174,14 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
 bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   const char* er = getenv("PZ_GEMM_ROWS");
   const char* em = getenv("PZ_ROWS_MAXM");
-  const int64_t maxm = em ? atoll(em) : 512;
+  const int64_t maxm = em ? atoll(em) : 1024;  // (C5's 768 / 789 prefill rows: 21.32 vs 21.52 ms at 512)
   if ((er && er[0] == '0') || a->M <= 64 || a->M > maxm || !pl.akc || !pl.bkc || a->batch != 1 ||
       a->epilogue >= PZ_EPI_DGELU || a->norm_w)
     return false;
   if (!(er && er[0] == '1') && (a->K > 2048 || ncols > 4096)) return false;
+  // e4m3 weights with bf16 rows (W8A16): 64-chunks of whole 16-code loads
+  if (a->fp8_mode == 2 && (a->K % 64 != 0 || a->ldb % 16 != 0)) return false;
+  pl.rows_f8 = a->fp8_mode == 2;
   // 16-row blocks per tile: 4 (64 rows); PZ_ROWS_TMB=2 (32-row tiles, twice the workgroups) for A/B runs
   const char* eb = getenv("PZ_ROWS_TMB");
   const int tmb = (eb && atoi(eb) == 2 && !pl.geglu) ? 2 : 4;
@@ -2233,6 +2237,11 @@ Plan make_plan(const pz_gemm_args* a) {
   const bool sk64_ok = (a->M <= 64 || a->M <= sk_maxm) && pl.akc && pl.bkc && a->K % 64 == 0 && a->batch == 1 &&
                        !a->c_fp32 && a->epilogue < PZ_EPI_DGELU;
   const char* e64 = getenv("PZ_SK64");  // "0": rows 17..64 take the tile kernels (A/B; read per call)
+  if (a->fp8_mode == 2 && a->M > 64) {  // W8A16 above 64 rows: the row-slab kernel or nothing (pz_gemm rejects)
+    pl.kind = PATH_SKINNY64;
+    plan_rows(pl, a, ncols);
+    return pl;
+  }
   if (a->fp8_mode == 2 || (sk64_ok && a->M > 16 && !(e64 && e64[0] == '0'))) {
     pl.kind = PATH_SKINNY64;
     pl.skinny_mb = a->M > 64 ? 4 : (int)((a->M + 15) / 16);
@@ -2394,8 +2403,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
       break;
     case PATH_ROWS:
-      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
-               bstr(pl.geglu));
+      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
+               bstr(pl.geglu), bstr(pl.rows_f8));
       break;
     case PATH_SPLIT:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
@@ -2608,11 +2617,14 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
     a8.ldb = a->ldb / 2;
     a = &a8;
   }
-  if (a->fp8_mode == 2)
-    PZ_CHECK_ARG(a->M <= 64 && a->a_kcontig && a->b_kcontig && a->batch == 1 && a->K % 64 == 0 && !a->c_fp32 &&
+  if (a->fp8_mode == 2) {
+    PZ_CHECK_ARG(a->a_kcontig && a->b_kcontig && a->batch == 1 && a->K % 64 == 0 && !a->c_fp32 &&
                      a->epilogue < PZ_EPI_DGELU && a->ldb % 16 == 0,
-                 "pz_gemm: fp8 weights with bf16 rows (W8A16) need M <= 64, k-contiguous A and B, batch 1, "
+                 "pz_gemm: fp8 weights with bf16 rows (W8A16) need k-contiguous A and B, batch 1, "
                  "K %% 64 == 0, ldb %% 16 == 0, bf16 C and a forward epilogue");
+    PZ_CHECK_ARG(a->M <= 64 || make_plan(a).kind == PATH_ROWS,
+                 "pz_gemm: W8A16 above 64 rows needs a row-slab shape (M <= 1024, K <= 2048, <= 4096 columns)");
+  }
 
   GemmP p;
   memset(&p, 0, sizeof(p));
@@ -2703,7 +2715,8 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
-  if (pl.kind == PATH_ROWS) return pz_rows_launch(p, pl.rows_w, pl.rows_tmb, pl.rows_tnb, pl.geglu, st);
+  if (pl.kind == PATH_ROWS)
+    return pz_rows_launch(p, pl.rows_w, pl.rows_tmb, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {
       p.ws = (float*)a->workspace;

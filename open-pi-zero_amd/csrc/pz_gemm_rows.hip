@@ -3,6 +3,23 @@
 
 namespace {
 
+__device__ __forceinline__ void fp8x16_to_bf16(const u32x4 q, bf16x8& lo, bf16x8& hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  bf16x2 h[8];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[2 * e] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, false);
+    h[2 * e + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, true);
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    lo[2 * e] = h[e][0];
+    lo[2 * e + 1] = h[e][1];
+    hi[2 * e] = h[4 + e][0];
+    hi[2 * e + 1] = h[4 + e][1];
+  }
+}
+
 // -------------------------------------------------------------------------
 // Row-slab GEMM for 64 < M <= 512 rows with k-contiguous A [M][K] and B [N][K]: the forward (NT) GEMMs
 // of the B = 1 SigLIP / Gemma prefill (256 / 276 rows) and of the action expert's training rows
@@ -18,7 +35,10 @@ namespace {
 // partial 64-chunk zeroes its 8-element pieces past K.  Tiles of one column slab are consecutive in
 // tile_coords' order, i.e. on one XCD (their weight slice is read from HBM once per L2).
 // -------------------------------------------------------------------------
-template <int W, int TMB, int TNB, bool GEGLU>
+// F8W: B holds OCP e4m3 codes [N][K] (ldb in codes; W8A16, the C5 prefill's fp8 weights at 768-789 rows): lane
+// group g takes k = 64c + 16g + [0, 16) -- the A row's two bf16x8 and ONE 16-B load of 16 codes expanded exactly
+// to bf16 (skinny-64's mapping); the weight scale is alpha.  K % 64 == 0.
+template <int W, int TMB, int TNB, bool GEGLU, bool F8W = false>
 __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP p) {
   constexpr int NB = TMB * TNB, NS = GEGLU ? 2 : 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -29,15 +49,21 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP
   tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
   const int64_t m0 = (int64_t)tm * (16 * TMB), n0 = (int64_t)tn * (16 * TNB);
   // rows / columns past the edge are clamped onto the last one (finite data, never stored)
+  constexpr int AG = F8W ? 16 : 8;  // k offset of lane group g within a 64-chunk half
   const bf16_t* Ar[TMB];
   const bf16_t* Br[NS][TNB];
+  const unsigned char* Bq[NS][TNB];  // F8W: code rows
 #pragma unroll
-  for (int mb = 0; mb < TMB; ++mb) Ar[mb] = p.A + min(m0 + 16 * mb + rl, p.M - 1) * p.lda + 8 * g;
+  for (int mb = 0; mb < TMB; ++mb) Ar[mb] = p.A + min(m0 + 16 * mb + rl, p.M - 1) * p.lda + AG * g;
 #pragma unroll
   for (int nb = 0; nb < TNB; ++nb) {
     const int64_t col = min(n0 + 16 * nb + rl, ncols - 1);
     Br[0][nb] = p.B + col * p.ldb + 8 * g;
-    if (GEGLU) Br[NS - 1][nb] = p.B + (p.geglu_I + col) * p.ldb + 8 * g;
+    Bq[0][nb] = reinterpret_cast<const unsigned char*>(p.B) + col * p.ldb + 16 * g;
+    if (GEGLU) {
+      Br[NS - 1][nb] = p.B + (p.geglu_I + col) * p.ldb + 8 * g;
+      Bq[NS - 1][nb] = reinterpret_cast<const unsigned char*>(p.B) + (p.geglu_I + col) * p.ldb + 16 * g;
+    }
   }
   const int nfull = (int)(p.K / 64), nch = (int)((p.K + 63) / 64);  // nch > nfull: a last partial chunk
   const int per = (nch + W - 1) / W;
@@ -53,6 +79,20 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP
   bf16x8 fa[2][TMB][2], fb[2][NS][TNB][2];
   auto load = [&](auto B_, int c, bool partial) {
     constexpr int bi = decltype(B_)::value;
+    if constexpr (F8W) {  // (host: K % 64 == 0, no partial chunk)
+#pragma unroll
+      for (int mb = 0; mb < TMB; ++mb) {
+        fa[bi][mb][0] = *reinterpret_cast<const bf16x8*>(Ar[mb] + (int64_t)c * 64);
+        fa[bi][mb][1] = *reinterpret_cast<const bf16x8*>(Ar[mb] + (int64_t)c * 64 + 8);
+      }
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int nb = 0; nb < TNB; ++nb)
+          fp8x16_to_bf16(*reinterpret_cast<const u32x4*>(Bq[s][nb] + (int64_t)c * 64), fb[bi][s][nb][0],
+                         fb[bi][s][nb][1]);
+      return;
+    }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int64_t ko = (int64_t)c * 64 + 32 * h;
@@ -133,22 +173,6 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP
 // both operands, so the sum is the plain dot product.  The weight scale of fp8 codes is alpha.
 // Requires K % 64 == 0, k-contiguous A and B, batch 1.
 // -------------------------------------------------------------------------
-__device__ __forceinline__ void fp8x16_to_bf16(const u32x4 q, bf16x8& lo, bf16x8& hi) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  bf16x2 h[8];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    h[2 * e] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, false);
-    h[2 * e + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8((int)q[e], 1.f, true);
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    lo[2 * e] = h[e][0];
-    lo[2 * e + 1] = h[e][1];
-    hi[2 * e] = h[4 + e][0];
-    hi[2 * e + 1] = h[4 + e][1];
-  }
-}
 
 template <int W, int NC, int MB, bool F8W>
 __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
@@ -377,10 +401,10 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
 
 }  // namespace
 
-template <int W, int TMB, int TNB, bool GEGLU>
+template <int W, int TMB, int TNB, bool GEGLU, bool F8W = false>
 static int launch_rows_k(const GemmP& p, hipStream_t st) {
   constexpr int smem = W * (GEGLU ? 2 : 1) * TMB * TNB * 1024;
-  auto kern = gemm_rows_kernel<W, TMB, TNB, GEGLU>;
+  auto kern = gemm_rows_kernel<W, TMB, TNB, GEGLU, F8W>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
@@ -404,7 +428,16 @@ static int launch_rows_w(const GemmP& p, int tmb, int tnb, bool geglu, hipStream
   return launch_rows_k<W, 4, 1, false>(p, st);
 }
 
-int pz_rows_launch(const GemmP& p, int w, int tmb, int tnb, bool geglu, hipStream_t st) {
+template <int W>
+static int launch_rows_f8(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
+  if (geglu) return tnb == 2 ? launch_rows_k<W, 4, 2, true, true>(p, st) : launch_rows_k<W, 4, 1, true, true>(p, st);
+  if (tnb == 4) return launch_rows_k<W, 4, 4, false, true>(p, st);
+  if (tnb == 2) return launch_rows_k<W, 4, 2, false, true>(p, st);
+  return launch_rows_k<W, 4, 1, false, true>(p, st);
+}
+
+int pz_rows_launch(const GemmP& p, int w, int tmb, int tnb, bool geglu, bool f8w, hipStream_t st) {
+  if (f8w) return w == 8 ? launch_rows_f8<8>(p, tnb, geglu, st) : launch_rows_f8<4>(p, tnb, geglu, st);
   return w == 8 ? launch_rows_w<8>(p, tmb, tnb, geglu, st) : launch_rows_w<4>(p, tmb, tnb, geglu, st);
 }
 

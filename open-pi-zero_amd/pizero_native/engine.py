@@ -234,8 +234,9 @@ class Engine:
     def prepare_fp8(self):
         """fp8 e4m3 copies (per-tensor scale max|W|/448) of every inference Linear of SigLIP, the vlm
         mixture and the action expert (BASELINE.json configs[4]: fp8 attention / MLP GEMMs).  Prefill
-        GEMMs (>= 65 rows) run W8A8 on the fp8 MFMA with per-row activation scales; denoise rows
-        (<= 64) run W8A16 (codes expanded to bf16 in registers, RMSNorm still fused).  Taken from the
+        GEMMs (>= 65 rows) run W8A8 on the fp8 MFMA with per-row activation scales, except the row-slab
+        shapes (<= 1024 rows, K <= 2048, <= 4096 columns: q|k|v / o), which run W8A16 like the denoise rows
+        (<= 64: codes expanded to bf16 in registers, RMSNorm still fused).  Taken from the
         current weights; the codes carry the arena's weight version (``weights_version``) and every
         inference entry point re-quantises them when the weights changed since (fp8_refresh)."""
         d = self.d
@@ -289,6 +290,9 @@ class Engine:
             if K % 64:  # (SigLIP fc2, K = 4304, never has so few rows in practice)
                 return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
             return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
+        ncols = W.shape[0] // 2 if epi == PZ_EPI_GEGLU else W.shape[0]
+        if norm is None and ops.rows_w8a16_ok(M, K, ncols):  # C5 prefill rows: W8A16 on the row-slab kernel
+            return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux)
         if norm is not None:
             raise ValueError("lin: a fused norm needs <= 64 rows")
         if K % 16 or x.stride(0) % 16:  # W8A8 stages K in 16-code steps (tiny test widths: bf16)

@@ -206,6 +206,17 @@ def linear_fp8(x, Wq, w_scale, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, a
     return out
 
 
+def rows_w8a16_ok(M, K, ncols):
+    """e4m3 weights with bf16 rows above 64 rows: the row-slab kernel's shapes (pz_gemm.hip plan_rows: 64 < M <=
+    PZ_ROWS_MAXM (1024), K % 64 == 0, K <= 2048, <= 4096 output columns; PZ_GEMM_ROWS=0 disables)"""
+    import os
+
+    if os.environ.get("PZ_GEMM_ROWS") == "0" or os.environ.get("PZ_ROWS_W8A16") == "0":
+        return False
+    maxm = int(os.environ.get("PZ_ROWS_MAXM", "1024"))
+    return 64 < M <= maxm and K % 64 == 0 and (os.environ.get("PZ_GEMM_ROWS") == "1" or (K <= 2048 and ncols <= 4096))
+
+
 def linear_dgrad(dy, W, dx, *, beta=False, resid=None, epi=PZ_EPI_NONE, aux=None):
     """dx[M,K] (+)= dy[M,N] @ W[N,K] (+ resid).
 

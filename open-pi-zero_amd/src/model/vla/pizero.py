@@ -258,8 +258,8 @@ class PiZero(nn.Module, NoSyncBase):
     def use_fp8_inference(self, enabled: bool = True):
         """Config C5 (BASELINE.json configs[4], "fp8 MFMA attention/MLP"): run inference (infer_action,
         infer_text) with OCP e4m3 weights -- per-tensor scales -- for every Linear of SigLIP, the vlm
-        mixture and the action expert: prefill GEMMs W8A8 on the fp8 MFMA (per-row activation scales),
-        denoise rows W8A16.  Training never uses them.  The codes are a snapshot of the current weights:
+        mixture and the action expert: prefill MLP GEMMs W8A8 on the fp8 MFMA (per-row activation scales),
+        prefill q|k|v / o projections and denoise rows W8A16.  Training never uses them.  The codes are a snapshot of the current weights:
         call again after the weights change.  An extension: the reference has no fp8 path."""
         self._fp8_infer = bool(enabled)
         eng = self._engine()

@@ -157,6 +157,31 @@ def test_w8a16_skinny(M, epi, N, K):
         assert _rel(out.float(), ref) < 1e-2, (M, epi, norm is not None, _rel(out.float(), ref))
 
 
+@pytest.mark.parametrize("M", [65, 256, 768, 789, 1024])
+@pytest.mark.parametrize("epi,N,K", [(PZ_EPI_NONE, 3456, 1152), (PZ_EPI_NONE, 1152, 1152), (PZ_EPI_NONE, 2048, 2048),
+                                     (PZ_EPI_GEGLU, 2 * 2048, 1024), (PZ_EPI_GELU, 2560, 2048)])
+def test_w8a16_rows(M, epi, N, K):
+    """W8A16 above 64 rows (C5's 768 / 789 prefill rows): the row-slab kernel with e4m3 weight codes expanded to
+    bf16 in registers (pz_gemm fp8_mode 2 -> gemm_rows_kernel<..., F8W>) vs torch fp32 of the dequantised weights;
+    bias, residual, GELU + aux, GeGLU + g|u."""
+    assert ops.rows_w8a16_ok(M, K, N // 2 if epi == PZ_EPI_GEGLU else N)
+    x = _rand(M, K, seed=M)
+    W = _rand(N, K, scale=0.03, seed=5)
+    Wq, ws = _quant_w(W)
+    I = N // 2
+    out = torch.empty(M, I if epi == PZ_EPI_GEGLU else N, device=DEV, dtype=torch.bfloat16)
+    resid = _rand(M, N, seed=13) if epi == PZ_EPI_NONE else None
+    bias = _rand(N, scale=0.1, seed=17) if epi != PZ_EPI_GEGLU else None
+    aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16) if epi != PZ_EPI_NONE else None
+    ops.linear_fp8(x, Wq, ws, out, bias=bias, resid=resid, epi=epi, aux=aux)
+    acc = x.float() @ _deq(Wq, ws).t()
+    ref = _epi_ref(acc, epi, bias, resid, I)
+    assert _rel(out.float(), ref) < 1e-2, (M, epi, _rel(out.float(), ref))
+    if aux is not None:
+        pre = acc if bias is None else acc + bias.float()
+        assert _rel(aux.float(), pre) < 1e-2
+
+
 @pytest.mark.parametrize("M", [17, 33, 50, 64])
 @pytest.mark.parametrize("N,K,epi", [(2560, 1024, PZ_EPI_NONE), (1024, 4096, PZ_EPI_NONE),
                                      (2 * 4096, 1024, PZ_EPI_GEGLU), (1024, 2048, PZ_EPI_SILU)])

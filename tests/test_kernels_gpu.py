@@ -342,7 +342,7 @@ def test_rows_kernel_forward_epilogues(M, N, K, variant, monkeypatch):
     if I * 2 == N:
         monkeypatch.setenv("PZ_ROWS_FIRST", "1")  # GeGLU shapes that the 256-tile path would otherwise take
         name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I)
-        assert name.startswith("gemm_rows_kernel") and name.endswith("true>"), name
+        assert name.startswith("gemm_rows_kernel") and name.endswith("true, false>"), name
         h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
         gu = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)

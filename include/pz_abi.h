@@ -309,6 +309,11 @@ int pz_embed_merge_bwd(const int64_t* ids, const void* dout, void* dimg, int64_t
 int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, float max_period, int32_t mode,
                   void* stream);
 /* out[b*H+h] = [temb[b], e1[b*H+h]] (vla/modules.py:46-51), bf16 */
+/* (ABI 15) inference form of pz_time_embed + pz_concat_time: the embedding of sample r / H written into columns
+ * [0, D) of row r of out (row stride ldo) for B * H rows -- the action encoder's concat input without the
+ * separate time-embedding buffer and concat launch (the encoder's first Linear writes columns [D, 2D)) */
+int pz_time_embed_rows(const float* t, void* out, int64_t ldo, int64_t B, int64_t H, int64_t D, float max_period,
+                       int32_t mode, void* stream);
 int pz_concat_time(const void* temb, const void* e1, void* out, int64_t B, int64_t H, int64_t D,
                    void* stream);
 /* dtemb not needed (t is data); de1 = dcat[:, D:] */

@@ -98,6 +98,28 @@ __global__ void time_embed_kernel(const float* __restrict__ t, bf16_t* out, int6
   out[idx] = f2bf(j < half ? sinf(a) : cosf(a));
 }
 
+// time embedding written straight into the first D columns of the action encoder's concat input (inference:
+// every one of a sample's H rows gets its sample's embedding; time_embed_kernel's arithmetic)
+__global__ void time_embed_rows_kernel(const float* __restrict__ t, bf16_t* out, int64_t ldo, int64_t rows,
+                                       int64_t H, int D, float max_period, int mode) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * D) return;
+  const int64_t r = idx / D;
+  const int j = (int)(idx % D), half = D / 2;
+  const int i = j < half ? j : j - half;
+  const float e = (float)(log((double)max_period) / (double)(half - 1));
+  const float tb = t[r / H];
+  float a;
+  if (mode == 0) {
+    a = tb * expf((float)i * -e);
+  } else {
+    const float ib = bf2f(f2bf((float)i));
+    const float f = bf2f(f2bf(expf(bf2f(f2bf(ib * -e)))));
+    a = bf2f(f2bf(bf2f(f2bf(tb)) * f));
+  }
+  out[r * ldo + j] = f2bf(j < half ? sinf(a) : cosf(a));
+}
+
 __global__ void concat_time_kernel(const bf16_t* __restrict__ temb, const bf16_t* __restrict__ e1, bf16_t* out,
                                    int64_t rows, int64_t H, int64_t D) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -368,6 +390,16 @@ extern "C" int pz_time_embed(const float* t, void* out, int64_t B, int64_t D, fl
   PZ_CHECK_ARG(t && out && B > 0 && D % 2 == 0 && D >= 4 && (mode == 0 || mode == 1), "time_embed: bad args");
   hipLaunchKernelGGL(time_embed_kernel, dim3(nblk(B * D)), dim3(256), 0, ST, t, (bf16_t*)out, B, (int)D,
                      max_period, (int)mode);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_time_embed_rows(const float* t, void* out, int64_t ldo, int64_t B, int64_t H, int64_t D,
+                                  float max_period, int32_t mode, void* stream) {
+  PZ_CHECK_ARG(t && out && B > 0 && H > 0 && D >= 4 && D % 2 == 0 && ldo >= D && (mode == 0 || mode == 1),
+               "time_embed_rows: bad args");
+  hipLaunchKernelGGL(time_embed_rows_kernel, dim3(nblk(B * H * D)), dim3(256), 0, ST, t, (bf16_t*)out, ldo, B * H, H,
+                     (int)D, max_period, (int)mode);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

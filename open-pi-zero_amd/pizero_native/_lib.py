@@ -154,6 +154,7 @@ SIGNATURES = {
     "pz_euler_step": [vp, vp, i64, i64, vp, i64, i64, i64, f32, vp],
     "pz_copy_rows": [vp, i64, i64, vp, i64, i64, i64, i64, i64, f32, i32, vp],
     "pz_prefetch": [vp, i64, i32, vp],
+    "pz_time_embed_rows": [vp, vp, i64, i64, i64, i64, f32, i32, vp],
     "pz_clamp": [vp, i64, f32, f32, vp],
     "pz_geglu_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, vp],
     "pz_act_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, i32, vp],

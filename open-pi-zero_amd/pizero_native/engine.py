@@ -601,11 +601,24 @@ class Engine:
         return X
 
     def action_embed(self, psi_bf, t, save):
-        """ActionEncoder (vla/modules.py:39-53) with time embedding (vla/modules.py:15-22)."""
+        """ActionEncoder (vla/modules.py:39-53) with time embedding (vla/modules.py:15-22).  Inference (save None):
+        the first Linear and the time embedding write straight into the concat input (pz_time_embed_rows: no
+        separate embedding buffer or concat launch) and no pre-activation is kept."""
         d = self.d
         rows = psi_bf.shape[0]
         B = t.shape[0]
         dev = psi_bf.device
+        if save is None:
+            cat = torch.empty(rows, 2 * d.aH, device=dev, dtype=BF16)
+            ops.small_linear(psi_bf, self.w("action_encoder.linear_1.weight"), cat[:, d.aH:],
+                             bias=self.w("action_encoder.linear_1.bias"))
+            ops.time_embed_rows(t, cat[:, : d.aH], rows // B, d.tmax, ref_bf16=d.time_bf16)
+            e2 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+            ops.linear(cat, self.w("action_encoder.linear_2.weight"), e2, bias=self.w("action_encoder.linear_2.bias"),
+                       epi=PZ_EPI_SILU)
+            e3 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
+            ops.linear(e2, self.w("action_encoder.linear_3.weight"), e3, bias=self.w("action_encoder.linear_3.bias"))
+            return e3
         e1 = torch.empty(rows, d.aH, device=dev, dtype=BF16)
         ops.small_linear(psi_bf, self.w("action_encoder.linear_1.weight"), e1, bias=self.w("action_encoder.linear_1.bias"))
         temb = torch.empty(B, d.aH, device=dev, dtype=BF16)

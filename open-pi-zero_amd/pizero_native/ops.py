@@ -552,6 +552,13 @@ def time_embed(t, out, max_period, ref_bf16=False):
     call("pz_time_embed", _p(t), _p(out), B, D, float(max_period), int(bool(ref_bf16)), _st())
 
 
+def time_embed_rows(t, out, H, max_period, ref_bf16=False):
+    """time embedding of sample r // H into out[r, :] (a column slice of the concat input), B * H rows"""
+    rows, D = out.shape
+    call("pz_time_embed_rows", _p(t), _p(out), out.stride(0), rows // H, H, D, float(max_period), int(bool(ref_bf16)),
+         _st())
+
+
 def concat_time(temb, e1, out, B, H, D):
     call("pz_concat_time", _p(temb), _p(e1), _p(out), B, H, D, _st())
 

@@ -800,6 +800,25 @@ def test_wgrad_split_k_matches_single_pass():
     close(dW, 2 * ref, atol=0.1 * math.sqrt(M) / 16)
 
 
+@pytest.mark.parametrize("mode", [False, True])
+def test_time_embed_rows_matches_embed_plus_concat(mode):
+    """pz_time_embed_rows (inference: the embedding written into the concat input's first D columns, H rows per
+    sample) is bit-identical to pz_time_embed + pz_concat_time."""
+    from pizero_native import ops
+
+    B, H, D = 3, 50, 1024
+    t = torch.rand(B, device=dev)
+    e1 = bf(B * H, D)
+    temb = torch.empty(B, D, device=dev, dtype=torch.bfloat16)
+    ops.time_embed(t, temb, 4.0, ref_bf16=mode)
+    cat1 = torch.empty(B * H, 2 * D, device=dev, dtype=torch.bfloat16)
+    ops.concat_time(temb, e1, cat1, B, H, D)
+    cat2 = torch.empty(B * H, 2 * D, device=dev, dtype=torch.bfloat16)
+    cat2[:, D:].copy_(e1)
+    ops.time_embed_rows(t, cat2[:, :D], H, 4.0, ref_bf16=mode)
+    assert torch.equal(cat1, cat2)
+
+
 def test_time_embed_modes_match_reference():
     """pz_time_embed mode 0 = the reference SinusoidalPosEmb in fp32; mode 1 = the reference's bf16
     arithmetic (bf16 arange rounds odd indices above 256, every op rounded; vla/modules.py:15-22)

@@ -328,6 +328,12 @@ int pz_flow_loss(const void* v, int64_t ldv, int64_t v_bstride, const float* x0,
 /* Euler step (pizero.py:479-481): a += dt*v ; t += dt.  v row (b,h) at v + b*v_bstride + h*ldv */
 int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t v_bstride, float* t, int64_t B, int64_t H,
                   int64_t A, float dt, void* stream);
+/* (ABI 15) the denoise step's tail in one launch: final action-expert RMSNorm of the rows of x (pz_rmsnorm_fwd's
+ * arithmetic), the action decoder W [A][D] (+ bias; bf16-rounded like pz_gemm_small) and pz_euler_step's update
+ * (action fp32 [B*H][A] += dt * v; t [B] += dt, NULL ok) -- pizero.py:478-481 + vla/modules.py action decoder */
+int pz_action_head_euler(const void* x, int64_t ldx, const void* norm_w, float eps, const void* W, int64_t ldw,
+                         const void* bias, float* action, float* t, int64_t B, int64_t H, int64_t D, int64_t A,
+                         float dt, void* stream);
 int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream);
 
 /* elementwise backward of fused MLP epilogues (recompute activations, no extra saves) */

@@ -173,6 +173,52 @@ __global__ void euler_kernel(float* action, const bf16_t* __restrict__ v, int64_
   if (t && idx < B) t[idx] += dt;
 }
 
+// denoise-step tail in one launch (pizero.py:461-481 + vla/modules.py action decoder): the final action-expert
+// RMSNorm of one row (fp32 statistics, the (1 + w) scale, rounded to bf16 like pz_rmsnorm_fwd), the A-wide
+// decoder Linear (+ bias, rounded to bf16 like pz_gemm_small) and the Euler update action += dt * v; t += dt
+// once per sample.  One workgroup of 256 threads per row.
+constexpr int AHE_AMAX = 32;
+__global__ void __launch_bounds__(256) action_head_euler_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                                const bf16_t* __restrict__ nw, float eps,
+                                                                const bf16_t* __restrict__ W, int64_t ldw,
+                                                                const bf16_t* __restrict__ bias, float* action,
+                                                                float* t, int64_t H, int D, int A, float dt) {
+  __shared__ float red[AHE_AMAX + 1][4];
+  const int64_t r = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bf16_t* xr = x + r * ldx;
+  float ss = 0.f;
+  for (int e = tid; e < D; e += 256) {
+    const float v = bf2f(xr[e]);
+    ss += v * v;
+  }
+  ss = warp_sum(ss);
+  if (lane == 0) red[AHE_AMAX][wave] = ss;
+  __syncthreads();
+  const float rs = rsqrtf((red[AHE_AMAX][0] + red[AHE_AMAX][1] + red[AHE_AMAX][2] + red[AHE_AMAX][3]) / (float)D + eps);
+  float dot[AHE_AMAX];
+#pragma unroll
+  for (int a = 0; a < AHE_AMAX; ++a) dot[a] = 0.f;
+  for (int e = tid; e < D; e += 256) {
+    const float y = bf2f(f2bf(bf2f(xr[e]) * rs * (1.f + bf2f(nw[e]))));
+#pragma unroll
+    for (int a = 0; a < AHE_AMAX; ++a)
+      if (a < A) dot[a] += y * bf2f(W[a * ldw + e]);
+  }
+#pragma unroll
+  for (int a = 0; a < AHE_AMAX; ++a) {
+    if (a >= A) break;
+    const float s = warp_sum(dot[a]);
+    if (lane == 0) red[a][wave] = s;
+  }
+  __syncthreads();
+  if (tid < A) {
+    const float s = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3] + (bias ? bf2f(bias[tid]) : 0.f);
+    action[r * A + tid] += dt * bf2f(f2bf(s));
+  }
+  if (t && tid == 0 && r % H == 0) t[r / H] += dt;
+}
+
 __global__ void copy_rows_kernel(const bf16_t* __restrict__ src, int64_t sld, int64_t sbs, bf16_t* dst, int64_t dld,
                                  int64_t dbs, int64_t rows, int64_t D, float scale, int beta) {
   const int64_t b = blockIdx.y;
@@ -446,6 +492,18 @@ extern "C" int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t 
   const int64_t n = B * H * A > B ? B * H * A : B;
   hipLaunchKernelGGL(euler_kernel, dim3(nblk(n)), dim3(256), 0, ST, action, (const bf16_t*)v, ldv, v_bstride, t, B,
                      H, A, dt);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_action_head_euler(const void* x, int64_t ldx, const void* norm_w, float eps, const void* W,
+                                    int64_t ldw, const void* bias, float* action, float* t, int64_t B, int64_t H,
+                                    int64_t D, int64_t A, float dt, void* stream) {
+  PZ_CHECK_ARG(x && norm_w && W && action && B > 0 && H > 0 && D > 0 && A >= 1 && A <= AHE_AMAX,
+               "action_head_euler: bad args (A <= %d)", AHE_AMAX);
+  hipLaunchKernelGGL(action_head_euler_kernel, dim3((unsigned)(B * H)), dim3(256), 0, ST, (const bf16_t*)x, ldx,
+                     (const bf16_t*)norm_w, eps, (const bf16_t*)W, ldw, (const bf16_t*)bias, action, t, H, (int)D,
+                     (int)A, dt);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

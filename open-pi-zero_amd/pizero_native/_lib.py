@@ -152,6 +152,7 @@ SIGNATURES = {
     "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
     "pz_flow_loss": [vp, i64, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
     "pz_euler_step": [vp, vp, i64, i64, vp, i64, i64, i64, f32, vp],
+    "pz_action_head_euler": [vp, i64, vp, f32, vp, i64, vp, vp, vp, i64, i64, i64, i64, f32, vp],
     "pz_copy_rows": [vp, i64, i64, vp, i64, i64, i64, i64, i64, f32, i32, vp],
     "pz_prefetch": [vp, i64, i32, vp],
     "pz_time_embed_rows": [vp, vp, i64, i64, i64, i64, f32, i32, vp],

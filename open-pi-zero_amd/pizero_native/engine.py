@@ -1430,6 +1430,13 @@ class Engine:
             x = self._post_attn(g, p, x, Pm, Vj, B, d.H, Lp, qrow0=0)
         if pf:
             torch.cuda.current_stream(dev).wait_stream(side)  # join the side stream (graph capture needs it)
+        # norm + decoder + Euler update in one launch: opt-in (PZ_FUSED_HEAD=1) -- measured neutral (C4 12.89 vs
+        # 12.87 ms, C5 21.32 vs 21.32 ms, profiles/r03/fused_head_ab.txt), so the three-launch path stays the default
+        if os.environ.get("PZ_FUSED_HEAD", "0") == "1":
+            ops.action_head_euler(x, self.w("joint_model.mixtures.action.norm.weight"), d.rms_eps,
+                                  self.w("action_decoder.weight"), self.w("action_decoder.bias"), action, t, B, d.H,
+                                  1.0 / d.steps)
+            return
         y = torch.empty_like(x)
         ops.rmsnorm(x, self.w("joint_model.mixtures.action.norm.weight"), y, None, d.rms_eps)
         v = torch.empty(B * d.H, 8, device=dev, dtype=BF16)

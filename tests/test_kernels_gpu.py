@@ -800,6 +800,33 @@ def test_wgrad_split_k_matches_single_pass():
     close(dW, 2 * ref, atol=0.1 * math.sqrt(M) / 16)
 
 
+@pytest.mark.parametrize("B,H,D,A", [(1, 4, 1024, 7), (1, 50, 1024, 7), (3, 5, 96, 7), (2, 4, 1024, 32)])
+def test_action_head_euler_matches_unfused(B, H, D, A):
+    """pz_action_head_euler (final action RMSNorm + decoder + Euler update in one launch) vs pz_rmsnorm_fwd +
+    pz_gemm_small + pz_euler_step: the normed row identical, v within one bf16 rounding of the reordered fp32 dot,
+    t advanced once per sample."""
+    from pizero_native import ops
+
+    x, nw = bf(B * H, D), bf(D, scale=0.1)
+    W, bias = bf(A, D, scale=D ** -0.5), bf(A, scale=0.1)
+    a0 = torch.randn(B, H, A, device=dev)
+    t0 = torch.rand(B, device=dev)
+    a1, t1 = a0.clone(), t0.clone()
+    y = torch.empty_like(x)
+    ops.rmsnorm(x, nw, y, None, 1e-6)
+    lv = max(8, A)
+    v = torch.empty(B * H, lv, device=dev, dtype=torch.bfloat16)
+    ops.small_linear(y, W, v[:, :A], bias=bias)
+    ops.euler_step(a1, v, lv, H * lv, t1, B, H, A, 0.1)
+    a2, t2 = a0.clone(), t0.clone()
+    ops.action_head_euler(x, nw, 1e-6, W, bias, a2, t2, B, H, 0.1)  # (opt-in in the engine: PZ_FUSED_HEAD=1)
+    assert torch.equal(t1, t2)
+    vmax = v[:, :A].float().abs().max().item()
+    assert (a1 - a2).abs().max().item() <= 0.1 * vmax * 2 ** -7 + 1e-6
+    ref = (y.float() @ W.float().t() + bias.float()).view(B, H, A)
+    close(a2, a0 + 0.1 * ref, rtol=1e-2, atol=1e-3)
+
+
 @pytest.mark.parametrize("mode", [False, True])
 def test_time_embed_rows_matches_embed_plus_concat(mode):
     """pz_time_embed_rows (inference: the embedding written into the concat input's first D columns, H rows per

@@ -50,18 +50,23 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return t;
 }
 
-// tanh through one v_exp_f32 + one reciprocal (|err| ~1e-7 absolute; saturates cleanly to +-1):
-// libm tanhf expands to ~40 instructions, which bloats every fused epilogue that applies it per element
-__device__ __forceinline__ float tanh_fast(float u) {
-  const float e = __expf(2.f * u);
-  return 1.f - __fdividef(2.f, e + 1.f);
-}
+// Activations with hardware v_exp_f32 / v_rcp_f32 (each ~1 ulp): a plain '/' or __fdividef compiles to the
+// IEEE division sequence (v_div_scale / v_div_fmas / v_div_fixup, ~11 instructions) in this build, which made
+// the per-element VALU work of every fused activation epilogue (GELU + aux, GeGLU, their backward) 23
+// instructions instead of 8 for gelu_tanh.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+// e^u as 2^(u log2 e) on v_exp_f32
+__device__ __forceinline__ float fast_exp(float u) { return __builtin_amdgcn_exp2f(u * 1.4426950408889634f); }
 
-// gelu(x, approximate="tanh") and its derivative (fp32)
+// tanh(u) = 1 - 2 / (e^{2u} + 1): saturates cleanly to +-1
+__device__ __forceinline__ float tanh_fast(float u) { return 1.f - 2.f * fast_rcp(fast_exp(2.f * u) + 1.f); }
+
+// gelu(x, approximate="tanh") = 0.5 x (1 + tanh(u)) = x * sigmoid(2u), u = k0 (x + k1 x^3):
+// one v_exp_f32, one v_rcp_f32 and 5 FMA / mul (fp32)
 __device__ __forceinline__ float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.f + tanh_fast(u));
+  constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, c1 = c0 * 0.044715f;
+  const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));  // e^{-2u}
+  return x * fast_rcp(1.f + e);
 }
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -71,9 +76,9 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
 }
 
-__device__ __forceinline__ float silu(float x) { return x / (1.f + __expf(-x)); }
+__device__ __forceinline__ float silu(float x) { return x * fast_rcp(1.f + fast_exp(-x)); }
 __device__ __forceinline__ float silu_grad(float x) {
-  const float s = 1.f / (1.f + __expf(-x));
+  const float s = fast_rcp(1.f + fast_exp(-x));
   return s * (1.f + x * (1.f - s));
 }
 

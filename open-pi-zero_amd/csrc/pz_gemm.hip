@@ -2107,7 +2107,7 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS, PATH_2W };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
@@ -2202,7 +2202,18 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 }
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
-Plan make_plan(const pz_gemm_args* a);
+// allow_2w = false: never the two-workgroup kernel (pz_gemm_qkv_rope's RoPE epilogue lives in the 8-phase one)
+Plan make_plan(const pz_gemm_args* a, bool allow_2w = true);
+
+// two-resident-workgroup 256 x 128 kernel (pz_gemm_2w.hip) instead of the 8-phase 256 x 256 one for a
+// forward (NT) GEMM: its epilogue runs under the co-resident tile's main loop.  PZ_GEMM_2W=1: every
+// eligible shape, 0: never (A/B runs; read per call)
+bool use_2w(const pz_gemm_args* a, const Plan& pl) {
+  const char* e = getenv("PZ_GEMM_2W");
+  if (!(e && e[0] == '1')) return false;
+  return pl.akc && pl.bkc && a->batch == 1 && a->K % 32 == 0 && a->fp8_mode == 0 && !a->c_fp32 && !a->norm_w &&
+         a->epilogue <= PZ_EPI_SILU;
+}
 
 // pz_gemm's column split (see there): 256-tile bf16 plan, N % 256 == 128, >= one full round of whole tiles
 bool colsplit(const pz_gemm_args* a, const Plan& pl) {
@@ -2216,7 +2227,7 @@ bool colsplit(const pz_gemm_args* a, const Plan& pl) {
          pl.tiles_m * (a->N / 256) >= device_cus();
 }
 
-Plan make_plan(const pz_gemm_args* a) {
+Plan make_plan(const pz_gemm_args* a, bool allow_2w) {
   Plan pl{};
   pl.akc = a->a_kcontig != 0;
   pl.bkc = a->b_kcontig != 0;
@@ -2318,6 +2329,12 @@ Plan make_plan(const pz_gemm_args* a) {
   const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192) ? 256 : 512);
   if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= (pl.geglu ? 256 : 512)) {
     const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;
+    if (allow_2w && use_2w(a, pl)) {
+      pl.kind = PATH_2W;
+      pl.tiles_m = tm;
+      pl.tiles_n = (ncols + cw / 2 - 1) / (cw / 2);
+      return pl;
+    }
     Plan cand = pl;
     cand.kind = PATH_256;
     cand.tiles_m = tm;
@@ -2401,6 +2418,9 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
     case PATH_TILE:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
+      break;
+    case PATH_2W:
+      snprintf(buf, sizeof(buf), "gemm2w_kernel<%s>", bstr(pl.geglu));
       break;
     case PATH_ROWS:
       snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
@@ -2715,6 +2735,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
+  if (pl.kind == PATH_2W) return pz_2w_launch(p, geglu, st);
   if (pl.kind == PATH_ROWS)
     return pz_rows_launch(p, pl.rows_w, pl.rows_tmb, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
   if (pl.kind == PATH_256 && use_8phase()) {
@@ -2788,7 +2809,7 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
     g.fp8_mode = 2;
     g.alpha = a->w_scale;
   }
-  const Plan pl = make_plan(&g);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
+  const Plan pl = make_plan(&g, false);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
   // few rows (16 < M <= 64: C5's 50-row denoise chunk): the skinny-64 kernel with the RoPE epilogue, the
   // Gemma RMSNorm optionally fused (mixture.py:162-215 + utils.py:4-16 in one launch)
   if (pl.kind == PATH_SKINNY64 && pl.ksplit == 0 && a->K % 64 == 0 && a->N % 256 == 0 && a->M <= 64 &&

@@ -1064,3 +1064,67 @@ def test_persistent_8phase_bit_identical_to_one_shot(case, monkeypatch):
         if r is not None:
             ref = ref + r[rows].float()
         close(o2[rows], ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 1152, 1152), (512, 3456, 1152), (768, 2048, 2048), (512, 1024, 32),
+                                   (512, 768, 64), (600, 1000, 416), (1300, 520, 96)])
+def test_gemm2w_forward_epilogues(M, N, K, monkeypatch):
+    """Two-resident-workgroup 256 x 128 NT GEMM (pz_gemm_2w.hip, PZ_GEMM_2W=1): every forward epilogue (bias,
+    residual, GELU / SiLU + saved pre-activation, bf16 beta accumulation, GeGLU + saved g|u), 1- and 2-K-tile
+    pipelines, row / column edge tiles; against torch fp32 and -- interior-only shapes -- bit-identical to the
+    8-phase kernel without its split tail (same k order, same epilogue rounding)."""
+    from pizero_native import ops
+
+    x, W, b, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(N), bf(M, N)
+    c0 = bf(M, N)
+    I = N // 2 // 4 * 4
+
+    def run():
+        outs = []
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, o, bias=b, resid=r)
+        outs.append(o)
+        o, pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, o, bias=b, epi=ops.PZ_EPI_GELU, aux=pre)
+        outs += [o, pre]
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, o, epi=ops.PZ_EPI_SILU)
+        outs.append(o)
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.linear(x, W, o)
+        outs.append(o)
+        o = c0.clone()
+        ops.gemm(M, N, K, x, K, True, W, K, True, o, N, beta=True)
+        outs.append(o)
+        if I * 2 == N:
+            h, gu = torch.empty(M, I, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+            outs += [h, gu]
+        return outs
+
+    monkeypatch.setenv("PZ_GEMM_2W", "1")
+    monkeypatch.setenv("PZ_GEMM_256_MINM", "256")
+    monkeypatch.setenv("PZ_GEMM_256_MINUNITS", "1")
+    monkeypatch.setenv("PZ_GEMM_ROWS", "0")
+    assert ops.gemm_kernel_name(M, N, K) == "gemm2w_kernel<false>", ops.gemm_kernel_name(M, N, K)
+    if I * 2 == N:
+        assert ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I) == "gemm2w_kernel<true>"
+    got = run()
+    ref = x.float() @ W.float().t()
+    close(got[0], ref + b.float() + r.float(), atol=2e-2)
+    close(got[1], torch.nn.functional.gelu(ref + b.float(), approximate="tanh"))
+    close(got[2], ref + b.float())
+    close(got[3], torch.nn.functional.silu(ref))
+    close(got[4], ref)
+    close(got[5], c0.float() + ref, atol=2e-2)
+    if I * 2 == N:
+        close(got[7], ref)
+        close(got[6], torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:], rtol=3e-2, atol=3e-2)
+    if M % 256 == 0 and N % 256 == 0:
+        monkeypatch.setenv("PZ_GEMM_2W", "0")
+        monkeypatch.setenv("PZ_GEMM_TAIL", "0")
+        assert ops.gemm_kernel_name(M, N, K).startswith("gemm8p_kernel"), ops.gemm_kernel_name(M, N, K)
+        want = run()
+        torch.cuda.synchronize()
+        for i, (a, c) in enumerate(zip(got, want)):
+            assert torch.equal(a, c), (i, float((a.float() - c.float()).abs().max()))

@@ -193,6 +193,11 @@ class Engine:
         # vectorised elementwise pass; "0" = fused into the dgrad GEMM's epilogue, which the 8-phase kernel
         # cannot overlap with its main loop (measured: "1" +0.7 % samples/s)
         self.split_dact = os.environ.get("PZ_SPLIT_DACT", "1") == "1"
+        # ... and of the Gemma GeGLU MLPs (PZ_SPLIT_DGEGLU, A/B): "0" (default) = d(gate|up) in the down-proj dgrad
+        # epilogue, which became the faster form once the activations ran on the hardware exp / rcp (vlm layer
+        # 1.390 vs 1.553 ms, action 24.2 vs 26.0 us, tools/dact_ab.py, profiles/r03/dact_ab.log); "1" = plain dgrad
+        # + the separate geglu_bwd pass
+        self.split_dgeglu = os.environ.get("PZ_SPLIT_DGEGLU", "0") == "1"
         # q|k|v GEMM with the RoPE + Q/K/V scatter in its epilogue (pz_gemm_qkv_rope) where the 8-phase kernel
         # runs; PZ_FUSE_QKV_ROPE=0: GEMM + pz_qkv_rope_split (A/B, bit-identical)
         self.fuse_qkv_rope = os.environ.get("PZ_FUSE_QKV_ROPE", "1") == "1" and self.d.hd == 256
@@ -815,7 +820,7 @@ class Engine:
         # dgrad through down_proj with the GeGLU derivative fused into its epilogue:
         # gu (saved g|u) <- d(gate|up) in place; hm (saved GeGLU output) feeds the down_proj wgrad
         gu = gs["gu"]
-        if self.split_dact:  # plain dgrad GEMM, then the HBM-bound GeGLU backward in place on gu
+        if self.split_dgeglu:  # plain dgrad GEMM, then the HBM-bound GeGLU backward in place on gu
             dh = torch.empty(M, g.inter, device=dev, dtype=BF16)
             ops.linear_dgrad(dx, self.w(p + "mlp.down_proj.weight"), dh)
             ops.geglu_bwd(dh, gu, gu, None, M, g.inter)

@@ -295,6 +295,9 @@ def main():
     d = model._engine().d
     Mg, Ng, Kg = mb * d.P, 2 * d.gI, d.gH
     probe = ops.set_probe(lambda M, N, K, epi, batch: (M, N, K, epi) == (Mg, Ng, Kg, ops.PZ_EPI_GEGLU))
+    if ddp:
+        meta.reducer.timing = True  # RCCL time per bucket + the un-hidden wait
+        n_log0 = len(meta.reducer.log)
     torch.cuda.synchronize()
     if ddp:
         dist.barrier()
@@ -312,6 +315,19 @@ def main():
     if ddp:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
+    comm = None
+    if ddp:
+        meta.reducer.timing = False
+        comm = meta.reducer.timing_summary(args.steps)
+        if comm is not None:  # max over ranks (the slowest rank's communication sets the step)
+            ct = torch.tensor([comm["comm_ms_per_step"], comm["exposed_ms_per_step"]], device=dev)
+            dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+            comm["comm_ms_per_step"], comm["exposed_ms_per_step"] = float(ct[0]), float(ct[1])
+            c, x = comm["comm_ms_per_step"], comm["exposed_ms_per_step"]
+            comm["overlap_frac"] = 1.0 - x / c if c > 0 else None
+            nbytes = sum(e for _, e in meta.reducer.log[n_log0:]) * model._arena.grad.element_size() / args.steps
+            comm["bytes_per_step"] = nbytes
+            comm["algbw_GBps"] = nbytes / (c * 1e-3) / 1e9 if c > 0 else None  # busbw = 2 (N-1) / N x algbw
     durs = [a.elapsed_time(b) for a, b in probe]
     kern_ms = sum(durs) / max(1, len(durs))
     flops_launch = 2.0 * Mg * Ng * Kg
@@ -380,7 +396,7 @@ def main():
             "ddp": None if not ddp else {
                 "backend": dist.get_backend(), "buckets_reduced_per_step": sum(1 for _ in meta.reducer.log) / max(
                     1, args.steps + args.warmup), "async_rccl_buckets": sum(1 for a, _ in meta.reducer.log if a),
-                "forced_at_world_1": bool(args.force_ddp and world == 1)},
+                "forced_at_world_1": bool(args.force_ddp and world == 1), **(comm or {})},
             "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
             "roofline": {"bound": "mfma", "kernel": kname + " (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,

@@ -2182,9 +2182,8 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   // e4m3 weights with bf16 rows (W8A16): 64-chunks of whole 16-code loads
   if (a->fp8_mode == 2 && (a->K % 64 != 0 || a->ldb % 16 != 0)) return false;
   pl.rows_f8 = a->fp8_mode == 2;
-  // 16-row blocks per tile: 4 (64 rows); PZ_ROWS_TMB=2 (32-row tiles, twice the workgroups) for A/B runs
-  const char* eb = getenv("PZ_ROWS_TMB");
-  const int tmb = (eb && atoi(eb) == 2 && !pl.geglu) ? 2 : 4;
+  // 64-row tiles (32-row tiles, twice the workgroups, measured slower on every shape: rows_bench.log)
+  const int tmb = 4;
   const int64_t tm = (a->M + 16 * tmb - 1) / (16 * tmb);
   int tnb = pl.geglu ? 2 : 4;
   while (tnb > 1 && tm * ((ncols + 16 * tnb - 1) / (16 * tnb)) < 128) tnb /= 2;
@@ -2737,7 +2736,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
   if (pl.kind == PATH_2W) return pz_2w_launch(p, geglu, st);
   if (pl.kind == PATH_ROWS)
-    return pz_rows_launch(p, pl.rows_w, pl.rows_tmb, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
+    return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {
       p.ws = (float*)a->workspace;

@@ -416,13 +416,8 @@ static int launch_rows_k(const GemmP& p, hipStream_t st) {
 }
 
 template <int W>
-static int launch_rows_w(const GemmP& p, int tmb, int tnb, bool geglu, hipStream_t st) {
+static int launch_rows_w(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
   if (geglu) return tnb == 2 ? launch_rows_k<W, 4, 2, true>(p, st) : launch_rows_k<W, 4, 1, true>(p, st);
-  if (tmb == 2) {
-    if (tnb == 4) return launch_rows_k<W, 2, 4, false>(p, st);
-    if (tnb == 2) return launch_rows_k<W, 2, 2, false>(p, st);
-    return launch_rows_k<W, 2, 1, false>(p, st);
-  }
   if (tnb == 4) return launch_rows_k<W, 4, 4, false>(p, st);
   if (tnb == 2) return launch_rows_k<W, 4, 2, false>(p, st);
   return launch_rows_k<W, 4, 1, false>(p, st);
@@ -436,9 +431,9 @@ static int launch_rows_f8(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
   return launch_rows_k<W, 4, 1, false, true>(p, st);
 }
 
-int pz_rows_launch(const GemmP& p, int w, int tmb, int tnb, bool geglu, bool f8w, hipStream_t st) {
+int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, bool f8w, hipStream_t st) {
   if (f8w) return w == 8 ? launch_rows_f8<8>(p, tnb, geglu, st) : launch_rows_f8<4>(p, tnb, geglu, st);
-  return w == 8 ? launch_rows_w<8>(p, tmb, tnb, geglu, st) : launch_rows_w<4>(p, tmb, tnb, geglu, st);
+  return w == 8 ? launch_rows_w<8>(p, tnb, geglu, st) : launch_rows_w<4>(p, tnb, geglu, st);
 }
 
 template <int W, int NC, int MB, bool F8W>

@@ -666,13 +666,13 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16) &&
-      PZ_ALIGNED(db_part, 16))
+      PZ_ALIGNED(db_part, 16) && (!dx_part || PZ_ALIGNED(dx_part, 16)))
     hipLaunchKernelGGL(norm_bwd_row_kernel<true>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
                        ldx, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R,
                        (int)D, dx_part);
   else if (dx_part)
     PZ_CHECK_ARG(false, "layernorm_bwd: dx_part (fused column sums of dx) needs the row kernel (16-byte aligned "
-                        "dy / dres / partials, PZ_NORM_BWD != wave)");
+                        "dy / dres / partials / dx_part, PZ_NORM_BWD != wave)");
   else
     NORM_DISPATCH(layernorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
                   mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D);

@@ -32,6 +32,11 @@ class GradReducer:
         # (async, elements) per launched bucket since construction: "async" = the RCCL branch (event on the
         # compute stream, all_reduce(AVG) enqueued on the communication stream)
         self.log = []
+        # timing=True: HIP events around every bucket on the communication stream (RCCL time) and around the
+        # compute stream's wait for the last bucket in finish() (the exposed, un-overlapped part); read with
+        # timing_summary() after a synchronize
+        self.timing = False
+        self._comm_ev, self._wait_ev = [], []
         self._reset()
 
     def _reset(self):
@@ -51,7 +56,14 @@ class GradReducer:
         ev.record()
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev)
+            if self.timing:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record()
             dist.all_reduce(g, op=dist.ReduceOp.AVG, group=self.group)
+            if self.timing:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()  # the collective's completion (all_reduce made this stream wait on RCCL's)
+                self._comm_ev.append((e0, e1))
             # the arena slice is produced on the compute stream and consumed here: keep the caching
             # allocator from recycling it before the collective ran
             g.record_stream(self.stream)
@@ -81,8 +93,27 @@ class GradReducer:
             if hi8 > self.done[region]:
                 self._launch(region, self.done[region], hi8)
         if self.stream is not None:
-            torch.cuda.current_stream().wait_stream(self.stream)
+            if self.timing:
+                w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                w0.record()  # the compute stream finished its backward
+                torch.cuda.current_stream().wait_stream(self.stream)
+                w1.record()  # ... and the last bucket landed: w1 - w0 = communication NOT hidden by compute
+                self._wait_ev.append((w0, w1))
+            else:
+                torch.cuda.current_stream().wait_stream(self.stream)
         self._reset()
+
+    def timing_summary(self, steps):
+        """{comm_ms_per_step, exposed_ms_per_step, overlap_frac} over the events recorded since the last call
+        (the caller synchronizes first); None without timed buckets."""
+        if not self._comm_ev:
+            return None
+        comm = sum(a.elapsed_time(b) for a, b in self._comm_ev)
+        exposed = sum(max(0.0, a.elapsed_time(b)) for a, b in self._wait_ev)
+        self._comm_ev, self._wait_ev = [], []
+        steps = max(1, steps)
+        return {"comm_ms_per_step": comm / steps, "exposed_ms_per_step": exposed / steps,
+                "overlap_frac": 1.0 - exposed / comm if comm > 0 else None}
 
 
 def region_marks(model):

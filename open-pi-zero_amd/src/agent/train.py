@@ -200,18 +200,18 @@ class TrainAgent:
                 self.cnt_update += 1
                 if self.cnt_update % self.save_model_freq == 0 or self.cnt_update == self.n_updates:
                     self.save_training(self.cnt_update, self.cnt_batch)
+            # every micro-batch's loss enters the window (kept on the device: no sync), as the reference's
+            # deque of grad_accumulation_steps rank-mean losses (train.py:405-463); the window is all-reduced
+            # ONCE, on the logged batches only (every rank has the same cnt_batch, so all enter the collective)
+            loss_deque.append(loss.detach().reshape(1).float())
             if self.cnt_batch % self.log_freq == 0:
-                # the rank-mean of this micro-batch's loss, as the reference logs it (train.py:381-384) -- but
-                # all-reduced only on the batches that are logged (every rank has the same cnt_batch, so all
-                # of them enter the collective), not once per micro-batch
+                win = torch.cat(list(loss_deque))
                 if self.multi_gpu:
-                    loss = loss.detach().clone()
-                    torch.distributed.all_reduce(loss, op=torch.distributed.ReduceOp.SUM)
-                    loss = loss / self.world
-                loss_deque.append(loss.item())
+                    torch.distributed.all_reduce(win, op=torch.distributed.ReduceOp.SUM)
+                    win = win / self.world
                 if self.main_rank:
                     log.info("Batch %d Update %d: loss %.4f | action lr %.8f", self.cnt_batch, self.cnt_update,
-                             float(np.mean(loss_deque)), self.action_optimizer.param_groups[0]["lr"])
+                             float(win.mean()), self.action_optimizer.param_groups[0]["lr"])
             self.cnt_batch += 1
         return self
 

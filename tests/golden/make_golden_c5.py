@@ -100,6 +100,79 @@ def run(dtype):
     return res
 
 
+C5_INFER_DIMS = dict(FULL_DIMS, num_images=3, num_image_tokens=768, max_seq_len=788, horizon_steps=50)
+
+
+def run_infer(dtype, W, inp):
+    """The reference's own ``PiZero.infer_action`` (pizero.py:416-490) at the C5 shape, B=1: the full model
+    (SigLIP + projector + Gemma-2B + action expert, tied + frozen as train.py:99-102), prefill of vlm +
+    proprio into the reference KVCache, 10 Euler steps with ``cache_mode="append_non_active"``
+    (joint_model.py:143-240).  The reference takes one image per sample (pizero.py:389), so its
+    ``vision_tower`` is called once per image and the 3 x 256 token features are concatenated in image
+    order -- the composition the native multi-image embedding implements; everything after that
+    (projector, /sqrt(2048), the image-row scatter, the joint model, the loop) is the reference's code
+    unchanged.  ``torch.randn`` is patched to return a clone of the supplied noise (pizero.py:454), the
+    final clip is off (the chunk stays informative).  Returns the chunk and each step's velocity."""
+    from src.model.vla import pizero as pz
+
+    d = C5_INFER_DIMS
+    torch.manual_seed(0)
+    model = pz.PiZero(ref_cfg(d))
+    model.tie_action_proprio_weights()
+    model.freeze_unused_weights()
+    sd = model.state_dict()
+    model.load_state_dict({k: torch.as_tensor(W[k]) for k in sd}, strict=True)
+    model.to(dtype).eval()
+    vt = model.vision_tower
+    one_image = vt.forward
+    vt.forward = lambda pv: torch.cat([one_image(pv[:, i]) for i in range(pv.shape[1])], dim=1)
+    vel = []
+    model.action_decoder.register_forward_hook(lambda m, a, o: vel.append(o.detach().float().clone()))
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dtype)  # noqa: E731
+    am = torch.from_numpy(inp["attention_mask"])
+    mask, vpos, ppos, apos = model.build_causal_mask_and_position_ids(am, dtype)
+    itp, amask = model.split_full_mask_into_submasks(mask)
+    noise = T(inp["noise"])
+    orig = torch.randn
+    try:
+        torch.randn = lambda *a, **k: noise.clone()
+        model.final_action_clip_value = None
+        with torch.inference_mode():
+            a = model.infer_action(input_ids=torch.from_numpy(inp["input_ids"]), pixel_values=T(inp["pixel_values"]),
+                                   image_text_proprio_mask=itp, action_mask=amask, vlm_position_ids=vpos,
+                                   proprio_position_ids=ppos, action_position_ids=apos, proprios=T(inp["proprios"]))
+    finally:
+        torch.randn = orig
+    assert len(vel) == d["num_inference_steps"], len(vel)
+    return a.float().numpy(), torch.stack(vel, 0).numpy()
+
+
+def main_infer():
+    """tests/golden/c5_infer.npz: the benched C5 chunk (B=1, 3 images, full prefix, chunk 50) from the
+    reference, fp32 (canonical) and bf16 (the reference's own bf16 deviation sets the GPU tolerance)."""
+    from oracle.synth import synth_inputs
+
+    install_stubs()
+    sys.path.insert(0, REF)
+    torch.set_num_threads(os.cpu_count() or 8)
+    d = C5_INFER_DIMS
+    W = synth_weights(d)
+    inp = synth_inputs(d, 1, seed=0, ragged=False)
+    assert inp["pixel_values"].shape == (1, 3, 3, 224, 224) and inp["input_ids"].shape == (1, 788)
+    out = {"in/input_ids": inp["input_ids"], "in/noise": inp["noise"]}
+    for tag, dt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        t0 = time.time()
+        a, v = run_infer(dt, W, inp)
+        print(f"c5 infer {tag}: {time.time() - t0:.1f}s  chunk |a| mean {np.abs(a).mean():.4f}", flush=True)
+        out[f"{tag}/actions_unclipped"] = a
+        out[f"{tag}/velocities"] = v
+    dev = np.abs(out["bf16/actions_unclipped"] - out["fp32/actions_unclipped"])
+    print(f"reference bf16 vs fp32: mean |d| {dev.mean():.3e} max {dev.max():.3e}")
+    path = os.path.join(ROOT, "tests", "golden", "c5_infer.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 def main():
     install_stubs()
     sys.path.insert(0, REF)
@@ -128,4 +201,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "infer":
+        main_infer()
+    else:
+        main()

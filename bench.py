@@ -36,6 +36,8 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0  # dense MFMA bf16 (MI355X_MICROARCH.md)
 TRAIN_FLOP_PER_SAMPLE = 3.812e12  # SURVEY 8(d), FlopCounterMode on the reference
 PEAK_HBM_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
+PEAK_FP8_TFLOPS = 5000.0  # dense MFMA e4m3 (MI355X_MICROARCH.md)
+C5_PREFILL_FLOP = 3.711e12  # 3 images + 20 text + 1 proprio prefill (FlopCounterMode on the reference)
 INFER_BYTES = 11.5e9  # B=1 action chunk, weights streamed + KV reads
 
 
@@ -187,12 +189,40 @@ def c5_inference(cfg, dev, iters):
             a = g.replay()
         e1.record()
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1) / iters, a.float().clone()
+        out = a.float().clone()
+        # the two phases as separate graphs on the same static inputs (roofline of each): the prefill
+        # (3 x SigLIP + the 789-row prefix pass writing the K/V cache) and the 10 denoise steps
+        e, s = m._engine(), g.static
+        pre_ms = _graph_ms(lambda: e.prefill(s["ids"], s["pix"], s["cnt"], s["vpos"], s["ppos"], s["proprios"],
+                                              g.k, g.v), iters)
 
-    ms, a16 = timed()
+        def denoise():
+            act = s["noise"].clone()
+            t = torch.zeros(1, device=dev, dtype=torch.float32)
+            for _ in range(d.steps):
+                e.denoise_step(act, t, s["apos"], s["cnt"], g.k, g.v, 1)
+
+        den_ms = _graph_ms(denoise, iters)
+        return e0.elapsed_time(e1) / iters, out, pre_ms, den_ms
+
+    ms, a16, pre16, den16 = timed()
     m.use_fp8_inference(True)  # BASELINE configs[4]: fp8 MFMA attention / MLP GEMMs
-    ms8, a8 = timed()
+    ms8, a8, pre8, den8 = timed()
     rel = float((a8 - a16).norm() / a16.norm())
+    # algorithmic budgets: prefill 3.711 TFLOP; denoise = 10 x the action expert's Linear
+    # weights (bf16 2 B / e4m3 1 B per element) + the K/V cache rows each step reads (bf16)
+    n_aw = sum(w.numel() for k, w in m.state_dict().items() if ".mixtures.action." in k and k.endswith("proj.weight"))
+    kv = 10 * d.nL * (d.P + d.C + d.H) * d.hd * 2 * 2
+    den_b16, den_b8 = 10 * n_aw * 2 + kv, 10 * n_aw * 1 + kv
+
+    def roof(pre, den, peak_tf, wbytes):
+        return {"prefill": {"bound": "mfma", "ms": pre, "flop": C5_PREFILL_FLOP,
+                            "achieved": C5_PREFILL_FLOP / (pre * 1e-3) / 1e12, "peak": peak_tf, "unit": "TFLOP/s",
+                            "frac": C5_PREFILL_FLOP / (pre * 1e-3) / 1e12 / peak_tf},
+                "denoise": {"bound": "hbm", "ms": den, "bytes": wbytes,
+                            "achieved": wbytes / (den * 1e-3) / 1e9, "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                            "frac": wbytes / (den * 1e-3) / 1e9 / PEAK_HBM_GBPS}}
+
     del m
     torch.cuda.empty_cache()
     return {"metric": "action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
@@ -203,7 +233,36 @@ def c5_inference(cfg, dev, iters):
                    "(codes expanded to bf16); attention QK^T / PV bf16",
             "fp8_vs_bf16_chunk_rel_l2": rel, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
             "baseline_source": "Pi0 paper figure quoted in the reference README.md:80,84 (other hardware)",
-            "vs_baseline": 73.0 / ms, "fp8_vs_baseline": 73.0 / ms8}
+            "vs_baseline": 73.0 / ms, "fp8_vs_baseline": 73.0 / ms8,
+            "roofline": {"bf16": roof(pre16, den16, PEAK_BF16_TFLOPS, den_b16),
+                         "fp8": roof(pre8, den8, PEAK_FP8_TFLOPS, den_b8),
+                         "note": "phases timed as separate hipGraphs on the graph's static inputs; the fp8 prefill "
+                                 "is priced against the fp8 dense peak although its q|k|v / o and attention run on "
+                                 "the bf16 MFMA"}}
+
+
+def _graph_ms(fn, iters):
+    """ms per replay of fn captured into a hipGraph (two warm-up runs on a side stream first)"""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        fn()
+    for _ in range(3):
+        gr.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(iters):
+        gr.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
 
 
 def main():

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 15
+#define PZ_ABI_VERSION 16
 
 enum {
   PZ_OK = 0,
@@ -328,12 +328,6 @@ int pz_flow_loss(const void* v, int64_t ldv, int64_t v_bstride, const float* x0,
 /* Euler step (pizero.py:479-481): a += dt*v ; t += dt.  v row (b,h) at v + b*v_bstride + h*ldv */
 int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t v_bstride, float* t, int64_t B, int64_t H,
                   int64_t A, float dt, void* stream);
-/* (ABI 15) the denoise step's tail in one launch: final action-expert RMSNorm of the rows of x (pz_rmsnorm_fwd's
- * arithmetic), the action decoder W [A][D] (+ bias; bf16-rounded like pz_gemm_small) and pz_euler_step's update
- * (action fp32 [B*H][A] += dt * v; t [B] += dt, NULL ok) -- pizero.py:478-481 + vla/modules.py action decoder */
-int pz_action_head_euler(const void* x, int64_t ldx, const void* norm_w, float eps, const void* W, int64_t ldw,
-                         const void* bias, float* action, float* t, int64_t B, int64_t H, int64_t D, int64_t A,
-                         float dt, void* stream);
 int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream);
 
 /* elementwise backward of fused MLP epilogues (recompute activations, no extra saves) */
@@ -384,10 +378,6 @@ int pz_fill_uniform(void* x, int32_t out_fp32, int64_t n, uint64_t seed, float o
  * (the sqrt(hidden) embedding scaling of joint_model.py:348-355 for proprio/action rows) */
 int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t dld, int64_t dbs, int64_t B,
                  int64_t rows, int64_t D, float scale, int32_t beta, void* stream);
-/* read [p, p + bytes) once into the caches (MALL / L2) and discard it: the inference engine warms the next
- * action-expert layer's weights on a side stream while the current layer's latency-bound GEMV chain runs
- * (replaces nothing in the reference: the weight reads of pizero.py:461-481's denoise Linears) */
-int pz_prefetch(const void* p, int64_t bytes, int32_t workgroups, void* stream);
 /* bf16 <-> fp32 copies / scaled adds */
 int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);

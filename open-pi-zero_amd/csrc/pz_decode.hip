@@ -4,13 +4,11 @@
 // the action tokens themselves).
 //
 // Two launches, each short and wide:
-//   decode_attn_part: one workgroup per (32-key chunk, 32-row tile) of one sample (C4: one row tile
-//     holds all 4 tokens x 8 heads; C5's chunk of 50 tokens = 13 row tiles):
-//     S^T = K Q^T on the MFMA (16 keys x 16 rows tiles, one tile per wave, K and Q fragments loaded
-//     straight from global memory), soft-cap + Pi0 block mask, chunk-local softmax stats (m, l),
-//     partial O = P V on the VALU (each thread 8 head dims x 4 query rows, its 16-byte V loads issued
-//     before the S phase), written as fp32 partials to the caller's workspace;
-//   decode_attn_combine: one workgroup per query row merges the chunks' (m, l, O) in fixed order.
+//   decode_attn_mfma: one workgroup per (group of 32-key chunks, 32-row tile) of one sample (C4: one row
+//     tile holds all 4 tokens x 8 heads; C5's chunk of 50 tokens = 13 row tiles), S^T and P.V on the MFMA
+//     with an online softmax over the group's chunks, fp32 (O, m, l) partials to the caller's workspace
+//     (one group: O written directly, no second launch);
+//   decode_attn_combine: one workgroup per query row merges the groups' (m, l, O) in fixed order.
 // The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of once per head.
 // Deterministic (no atomics).
 #include <stdlib.h>
@@ -31,162 +29,6 @@ __device__ __forceinline__ bool da_allowed(int t, int j, int nk, int cnt, int P,
   if (t < P) return t < cnt && j < cnt;
   if (t < P + C) return j < cnt || (j >= P && j < P + C);
   return j < cnt || j >= P;
-}
-
-// grid (ngroups, B * rtiles), 256 threads = 4 waves: workgroup = (group of nch consecutive 32-key chunks,
-// 32-row tile rt, sample b); per chunk wave w computes key tile (w & 1) x row block (w >> 1) of S, then an
-// online-softmax update of the workgroup's running (m, l, O) (C5's 27 chunks x 13 row tiles in groups of
-// 2: half the partial rows to merge).  Workspace rows [b][group][Rpad][DA_RS], Rpad = 32 * rtiles.
-__global__ void __launch_bounds__(256) decode_attn_part(pz_decode_attn_args a, int nch) {
-  __shared__ float S[DA_R][DA_KC + 1];  // logits -> probabilities, [row][key]
-  __shared__ float alpha_s[DA_R];       // per-row rescale of the running O for this chunk
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int T = (int)a.T, nh = (int)a.nh, nk = (int)a.nk, R = T * nh;
-  const int rtiles = (R + DA_R - 1) / DA_R, Rpad = rtiles * DA_R;
-  const int grp = blockIdx.x, b = blockIdx.y / rtiles, rt = blockIdx.y % rtiles, r0 = rt * DA_R;
-  const bool masked = a.cnt != nullptr;  // NULL: no mask (text generation, pizero.py:336-365)
-  const int cnt = masked ? a.cnt[b] : nk;
-  const bf16_t* K = (const bf16_t*)a.k + (int64_t)b * a.k_bstride;
-  const bf16_t* V = (const bf16_t*)a.v + (int64_t)b * a.v_bstride;
-  const int nchunks = (nk + DA_KC - 1) / DA_KC;
-  const int c0 = grp * nch, c1 = min(nchunks, c0 + nch);
-  // P.V ownership: thread = 8 head dims (dg) x 4 query rows (rg); its V loads (16 keys x 16 B, 128 B
-  // contiguous per 8 lanes) are issued before the S phase so their latency overlaps it
-  const int dg = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  // this lane's query fragments (the same for every chunk): row block (wave >> 1), 8 x 16 B
-  const int g = lane >> 4;
-  const int row = r0 + (wave >> 1) * 16 + (lane & 15);  // query row = t * nh + h
-  const bool rok = row < R;
-  const int t = rok ? row / nh : 0, h = rok ? row % nh : 0;
-  const int qt = (int)a.qtok0 + t;
-  bf16x8 qf[8];
-  {
-    const bf16_t* qp = (const bf16_t*)a.q + ((int64_t)b * a.Lq + a.qoff + t) * a.ldq + (int64_t)h * DA_HD + 8 * g;
-#pragma unroll
-    for (int dc = 0; dc < 8; ++dc) qf[dc] = rok ? *reinterpret_cast<const bf16x8*>(qp + dc * 32) : bf16x8{};
-  }
-  const float inv_cap = a.cap > 0.f ? 1.f / a.cap : 0.f;
-  float o[4][8];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[r][e] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;  // threads < 32: row threadIdx.x's running stats
-  for (int c = c0; c < c1; ++c) {
-    const int j0 = c * DA_KC;
-    u32x4 vv[DA_KC / 2];
-#pragma unroll
-    for (int u = 0; u < DA_KC / 2; ++u)
-      vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + u, nk - 1) * DA_HD + 8 * dg);
-    {
-      const int kt = wave & 1;
-      const int key = min(j0 + kt * 16 + (lane & 15), nk - 1);
-      const bf16_t* kp = K + (int64_t)key * DA_HD + 8 * g;
-      bf16x8 kf[8];
-#pragma unroll
-      for (int dc = 0; dc < 8; ++dc) kf[dc] = *reinterpret_cast<const bf16x8*>(kp + dc * 32);
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int dc = 0; dc < 8; ++dc) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[dc], qf[dc], acc, 0, 0, 0);
-      // lane holds S^T[key = kt*16 + 4g + e][row]
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int kl = kt * 16 + 4 * g + e;
-        float x = acc[e] * a.scale;
-        if (a.cap > 0.f) x = a.cap * tanh_fast(x * inv_cap);
-        const bool ok = rok && (masked ? da_allowed(qt, j0 + kl, nk, cnt, (int)a.prefix, (int)a.cond) : j0 + kl < nk);
-        S[row - r0][kl] = ok ? x : -INFINITY;
-      }
-    }
-    __syncthreads();
-    // online softmax per row (thread r < 32): new max, rescale factor, S <- p
-    if (threadIdx.x < DA_R) {
-      const int r = threadIdx.x;
-      float m = m_run;
-#pragma unroll
-      for (int k = 0; k < DA_KC; ++k) m = fmaxf(m, S[r][k]);
-      const float al = m_run == -INFINITY ? 0.f : __expf(m_run - m);
-      float l = 0.f;
-#pragma unroll
-      for (int k = 0; k < DA_KC; ++k) {
-        const float p = m == -INFINITY ? 0.f : __expf(S[r][k] - m);
-        S[r][k] = p;
-        l += p;
-      }
-      l_run = l_run * al + l;
-      m_run = m;
-      alpha_s[r] = al;
-    }
-    __syncthreads();
-    // O[row][d] = alpha * O + sum_k p[row][k] V[k][d]: 4 rows x 8 dims per thread, two halves of 16 keys
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float al = alpha_s[4 * rg + r];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[r][e] *= al;
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      if (half == 1) {
-#pragma unroll
-        for (int u = 0; u < DA_KC / 2; ++u)
-          vv[u] = *reinterpret_cast<const u32x4*>(V + (int64_t)min(j0 + DA_KC / 2 + u, nk - 1) * DA_HD + 8 * dg);
-      }
-#pragma unroll
-      for (int u4 = 0; u4 < DA_KC / 8; ++u4) {
-        float pr[4][4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) pr[r][q] = S[4 * rg + r][half * (DA_KC / 2) + 4 * u4 + q];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float vf[8];
-          const u32x4 vr = vv[4 * u4 + q];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            vf[2 * e] = __uint_as_float(vr[e] << 16);
-            vf[2 * e + 1] = __uint_as_float(vr[e] & 0xffff0000u);
-          }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[r][e] += pr[r][q] * vf[e];
-        }
-      }
-    }
-    __syncthreads();  // S / alpha_s are rewritten by the next chunk
-  }
-  if (gridDim.x == 1) {  // one group holds every key: normalise and write O directly (no merge launch)
-    if (threadIdx.x < DA_R) alpha_s[threadIdx.x] = l_run > 0.f ? 1.f / l_run : 0.f;
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int rr = r0 + 4 * rg + r;
-      if (rr < R) {
-        const float il = alpha_s[4 * rg + r];
-        const int tt = rr / nh, hh = rr % nh;
-        bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD + 8 * dg;
-        *reinterpret_cast<u32x4*>(out) = u32x4{pack2bf(o[r][0] * il, o[r][1] * il), pack2bf(o[r][2] * il, o[r][3] * il),
-                                              pack2bf(o[r][4] * il, o[r][5] * il), pack2bf(o[r][6] * il, o[r][7] * il)};
-      }
-    }
-    return;
-  }
-  float* ws = a.ws + (((int64_t)b * gridDim.x + grp) * Rpad + r0) * DA_RS;
-  if (threadIdx.x < DA_R) {
-    ws[threadIdx.x * DA_RS + DA_HD] = m_run;
-    ws[threadIdx.x * DA_RS + DA_HD + 1] = l_run;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int rr = 4 * rg + r;
-    if (r0 + rr < R) {
-      float4* dst = reinterpret_cast<float4*>(ws + rr * DA_RS + 8 * dg);
-      dst[0] = float4{o[r][0], o[r][1], o[r][2], o[r][3]};
-      dst[1] = float4{o[r][4], o[r][5], o[r][6], o[r][7]};
-    }
-  }
 }
 
 // grid (R, B), 256 threads: thread = head dim; merges the chunks in order 0..nchunks-1
@@ -231,7 +73,7 @@ __global__ void __launch_bounds__(256) decode_attn_combine(pz_decode_attn_args a
 // ---- MFMA decode attention (default): P.V on the matrix cores --------------------------------------------
 // grid (ngroups, B * rtiles), 256 threads: workgroup = (group of nch consecutive 32-key chunks, sample b, 32-row
 // tile) with an online softmax over its chunks; ngroups == 1 writes O itself (no merge launch), otherwise fp32
-// (O, m, l) partials in decode_attn_part's workspace layout for decode_attn_combine.  Per chunk: V(c) staged
+// (O, m, l) partials (workspace rows [b][group][Rpad][DA_RS], Rpad = 32 * rtiles) for decode_attn_combine.  Per chunk: V(c) staged
 // into an LDS image read transposed (ds_read_b64_tr_b16), S^T = K Q^T on the MFMA (K fragments straight from
 // global), soft-cap + block mask into LDS, the softmax of each row by 8 lanes (4 keys each, shuffle max / sum,
 // online (m, l) kept in all 8 lanes), bf16 P, and O^T += V^T P^T on the MFMA (16 per chunk instead of the VALU
@@ -437,33 +279,23 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const int64_t rtiles = (a->T * a->nh + DA_R - 1) / DA_R;
   PZ_CHECK_ARG(a->B * rtiles < 65536, "decode_attn: grid too large");
-  // PZ_DECODE_ONE=1: one workgroup per (sample, row tile) walking every key chunk (no merge launch) -- measured
-  // SLOWER for C4 (chunk 16.2 vs 13.8 ms with the VALU P.V: the per-chunk chain is latency-bound in one
-  // workgroup, ~2.9 us per 32 keys, while the split kernels run the 9 chunks on 9 CUs at once); A/B only
-  const char* e1 = getenv("PZ_DECODE_ONE");
-  const bool one = e1 && e1[0] == '1';
   // chunks per workgroup: one (C4: 9 workgroups) until the (chunk, row tile) grid passes 256 workgroups,
-  // then groups of nch chunks (fewer partial rows for the merge)
+  // then groups of nch chunks (fewer partial rows for the merge).  One workgroup walking every chunk (no merge
+  // launch) measured slower for C4: 15.21 vs 12.81 ms per chunk (profiles/r03/decode_grouping_ab.txt)
   const int64_t wg1 = (int64_t)nchunks * a->B * rtiles;
   const char* e = getenv("PZ_DECODE_WG");  // target workgroups (A/B; read per call)
   const int64_t target = e && atoll(e) > 0 ? atoll(e) : 256;
-  int nch = one ? nchunks : (int)((wg1 + target - 1) / target);
+  int nch = (int)((wg1 + target - 1) / target);
   int ngroups = (nchunks + nch - 1) / nch;
-  // PZ_DECODE_PART=valu: the VALU P.V part kernel (A/B; read per call); default the MFMA kernel
-  const char* ep = getenv("PZ_DECODE_PART");
-  const bool mfma = !(ep && strcmp(ep, "valu") == 0);
-  const bool o_vec = mfma ? (PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0) : (PZ_ALIGNED(a->o, 16) && a->ldo % 8 == 0);
-  if (ngroups == 1 && !o_vec) {  // the direct-O paths store 8 B (MFMA) / 16 B (VALU) per lane
-    PZ_CHECK_ARG(nchunks > 1, "decode_attn: a single key chunk needs an aligned O (8 / 16 B, ldo %% 4 / 8 == 0)");
+  const bool o_vec = PZ_ALIGNED(a->o, 8) && a->ldo % 4 == 0;
+  if (ngroups == 1 && !o_vec) {  // the direct-O path stores 8 B per lane
+    PZ_CHECK_ARG(nchunks > 1, "decode_attn: a single key chunk needs an aligned O (8 B, ldo %% 4 == 0)");
     nch = (nchunks + 1) / 2;
     ngroups = (nchunks + nch - 1) / nch;
   }
-  if (mfma)
-    hipLaunchKernelGGL(decode_attn_mfma, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
-  else
-    hipLaunchKernelGGL(decode_attn_part, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
+  hipLaunchKernelGGL(decode_attn_mfma, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
   PZ_CHECK_LAUNCH();
-  if (ngroups == 1) return PZ_OK;  // the part kernel wrote O
+  if (ngroups == 1) return PZ_OK;  // the kernel wrote O
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
                      ngroups);
   PZ_CHECK_LAUNCH();

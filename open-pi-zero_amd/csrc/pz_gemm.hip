@@ -1293,324 +1293,6 @@ __global__ void __launch_bounds__(NT2, 1) gemm8p_f8_kernel(GemmP p) {
   gemm8p_body<true, true, GEGLU, KTAIL, true>(p);
 }
 
-// ---- persistent 8-phase kernel (k-contiguous A and B: the forward NT GEMMs) --------------------
-// The epilogue of the one-shot kernel is not overlapped with anything: its stores must drain before the
-// workgroup exits and frees the 128 KiB of LDS, and only then does the next tile's workgroup start its
-// prologue DMA (measured, tools/epi_probe.py: the vlm GeGLU GEMM 2.26 ms with stores vs 1.70 without; a
-// staggered first round did not help, so it is this per-CU serialisation, not a chip-wide write burst).
-// Here one workgroup per CU walks the work units blockIdx.x, +G, +2G, ... (whole tiles, then the
-// split-tail K-pieces) as ONE stream of K-steps: the LDS-DMA of the next unit's first two K-steps is
-// issued during the current unit's last two (the steady-state schedule, unchanged), and the epilogue
-// stores go straight from the accumulators to global memory (no LDS staging: both buffers are filling)
-// while those loads are in flight.  vmcnt retires in issue order, so the waits of the first K-step after
-// an epilogue count its memory ops as younger (+adj: a lower bound of the ops it issued); the second
-// K-step's waits then also retire the stores, one K-step after they were issued.
-#define PZ_WVM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
-__device__ __forceinline__ void wait_vm10(int adj) {
-  if (adj >= 48) PZ_WVM(58);
-  else if (adj >= 32) PZ_WVM(42);
-  else if (adj >= 16) PZ_WVM(26);
-  else PZ_WVM(10);
-}
-__device__ __forceinline__ void wait_vm8(int adj) {
-  if (adj >= 48) PZ_WVM(56);
-  else if (adj >= 32) PZ_WVM(40);
-  else if (adj >= 16) PZ_WVM(24);
-  else PZ_WVM(8);
-}
-__device__ __forceinline__ void wait_vm2(int adj) {
-  if (adj >= 48) PZ_WVM(50);
-  else if (adj >= 32) PZ_WVM(34);
-  else if (adj >= 16) PZ_WVM(18);
-  else PZ_WVM(2);
-}
-
-struct Unit8 {
-  int64_t m0, n0;
-  int kt0, nk, piece;  // piece < 0: a whole tile
-};
-
-template <bool GEGLU>
-__device__ __forceinline__ Unit8 unit8_of(const GemmP& p, int u, int nk_all) {
-  Unit8 r;
-  int lid = u;
-  r.piece = -1;
-  r.kt0 = 0;
-  r.nk = nk_all;
-  if (p.tail_s && lid >= p.dp_tiles) {
-    const int v = lid - p.dp_tiles;
-    r.piece = v;
-    lid = p.dp_tiles + v / p.tail_s;
-    r.kt0 = (v % p.tail_s) * p.tail_kt;
-    r.nk = min(nk_all - r.kt0, p.tail_kt);
-  }
-  int tm, tn;
-  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
-  r.m0 = (int64_t)tm * BT;
-  r.n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
-  return r;
-}
-
-template <bool GEGLU, bool KTAIL, int FM>  // FM: interior epilogue class (FM_STORE | FM_BF16; GEGLU: unused)
-__global__ void __launch_bounds__(NT2, 1) gemm8q_kernel(GemmP p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nk_all = (int)((p.K + 63) / 64);
-  const int T = p.tiles_m * p.tiles_n;
-  const int U = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
-  const int G = gridDim.x;
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  const int g4 = 4 * (lane >> 4), rl = lane & 15;
-  // thread constants of the k-contiguous LDS images (p8_src): region row (t >> 3) + 64 i, 16-B chunk
-  const int trow = t >> 3;
-  const int colofs = 8 * ((t & 7) ^ ((t >> 4) & 7));
-  const int krem = KTAIL ? (int)(p.K - (int64_t)(nk_all - 1) * 64) : 64;  // valid k of the last K-tile
-  constexpr int lds_off[4] = {0, 2 * P8_REG, 3 * P8_REG, P8_REG};
-
-  int ucur = blockIdx.x;
-  Unit8 cur = unit8_of<GEGLU>(p, ucur, nk_all);
-  int unxt = ucur + G;
-  const bool has_nxt0 = unxt < U;
-  Unit8 nxt = has_nxt0 ? unit8_of<GEGLU>(p, unxt, nk_all) : cur;
-  bool has_nxt = has_nxt0;
-  int cur_start = 0, cur_end = cur.nk;  // global K-steps [cur_start, cur_end) belong to cur
-
-  // LDS-DMA sources: per piece (0 = A region 0, 1 = B region 0, 2 = B region 1, 3 = A region 1) the two
-  // per-thread pointers of the unit whose first global K-step is pbase[piece] (its kt0 folded in).  A piece
-  // switches to the next unit the first time it is issued for a K-step of that unit (A region 1 one K-step
-  // before the others), so the K loop does one 64-bit add per DMA, like the one-shot kernel.
-  const bf16_t* src[4][2];
-  int pbase[4], plast[4];  // plast: global K-step of the reduction's last (K % 64) tile in that unit, or -1
-  auto set_src = [&](int piece, const Unit8& u, int base) {
-    const bool isA = piece == 0 || piece == 3;
-    const int region = (piece == 3 || piece == 2) ? 1 : 0;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int64_t g;
-      if (isA) {
-        g = u.m0 + i * 128 + region * 64 + trow;
-        g = g < p.M ? g : p.M - 1;
-      } else if (GEGLU) {
-        const int v = region * 128 + i * 64 + trow;
-        g = u.n0 + (v >> 6) * 32 + (v & 31);
-        g = g < p.geglu_I ? g : p.geglu_I - 1;
-        if ((v >> 5) & 1) g += p.geglu_I;
-      } else {
-        g = u.n0 + region * 128 + i * 64 + trow;
-        g = g < p.N ? g : p.N - 1;
-      }
-      src[piece][i] = (isA ? p.A + g * p.lda : p.B + g * p.ldb) + colofs + (int64_t)u.kt0 * 64;
-    }
-    pbase[piece] = base;
-    plast[piece] = (KTAIL && u.kt0 + u.nk == nk_all) ? base + u.nk - 1 : -1;
-  };
-#pragma unroll
-  for (int q = 0; q < 4; ++q) set_src(q, cur, 0);
-  // LDS-DMA of one piece of global K-step `step` (cur's, or from cur_end on nxt's)
-  auto issue = [&](int piece, int step) {
-    if (step >= cur_end && pbase[piece] != cur_end) set_src(piece, nxt, cur_end);
-    const int64_t off = (int64_t)(step - pbase[piece]) * 64;
-    char* dst = smem + (step & 1) * P8_BUF + lds_off[piece] + wave * 1024;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const bf16_t* g = src[piece][i] + off;
-      if (KTAIL && krem < 64 && step == plast[piece] && colofs >= krem) g -= colofs - (krem - 8);
-      glds16(g, dst + i * 8192);
-    }
-  };
-
-  f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[4][2], bf[2][2][2];
-  auto read_a = [&](const char* buf, int ah) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) af[i][kk] = frag<true>(buf + ah * P8_REG, wr * 4 + i, kk, lane);
-  };
-  auto read_b = [&](const char* buf, int bh) {
-    const char* reg = buf + 2 * P8_REG + (wc >> 1) * P8_REG;
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) bf[bh][j][kk] = frag<true>(reg, (wc & 1) * 4 + bh * 2 + j, kk, lane);
-  };
-  auto mask_tail_a = [&](int kt) {
-    if (KTAIL && krem < 64 && kt == nk_all - 1) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk)
-          if (kk * 32 + 8 * (lane >> 4) >= krem) af[i][kk] = bf16x8{};
-    }
-  };
-  auto mfma_quad = [&](int ah, int bh) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[ah * 4 + i][bh * 2 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[bh][j][kk], af[i][kk], acc[ah * 4 + i][bh * 2 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  // prologue: global K-steps 0 (all pieces) and 1 (A0, B0, B1); every unit has >= 2 K-steps
-  issue(0, 0);
-  issue(1, 0);
-  issue(2, 0);
-  issue(3, 0);
-  const bool two = cur.nk > 1 || has_nxt;
-  if (two) {
-    issue(0, 1);
-    issue(1, 1);
-    issue(2, 1);
-    PZ_WAIT_VM(8);
-  } else {
-    PZ_WAIT_VM(2);
-  }
-  PZ_RAW_BARRIER();
-  if (wr == 1) PZ_RAW_BARRIER();  // stagger: row-1 waves run one barrier behind
-
-  int s = 0;    // global K-step
-  int adj = 0;  // memory ops of the epilogue just before this K-step (lower bound; 0: none)
-  while (true) {
-    const int kt = cur.kt0 + (s - cur_start);
-    const char* buf = smem + (s & 1) * P8_BUF;
-    const bool n1 = s + 1 < cur_end || has_nxt, n2 = s + 2 < cur_end || has_nxt;
-    // phase 0: quadrant (0,0)
-    if (n1) issue(3, s + 1);
-    read_a(buf, 0);
-    read_b(buf, 0);
-    PZ_WAIT_LGKM0();
-    PZ_RAW_BARRIER();
-    mask_tail_a(kt);
-    mfma_quad(0, 0);
-    PZ_RAW_BARRIER();
-    // phase 1: quadrant (0,1); retire A region 1 of this K-step
-    if (n2) issue(0, s + 2);
-    read_b(buf, 1);
-    if (n2) wait_vm10(adj);
-    else if (n1) wait_vm8(adj);
-    else PZ_WAIT_VM(0);
-    PZ_WAIT_LGKM0();
-    PZ_RAW_BARRIER();
-    mfma_quad(0, 1);
-    PZ_RAW_BARRIER();
-    // phase 2: quadrant (1,1)
-    if (n2) issue(1, s + 2);
-    read_a(buf, 1);
-    PZ_WAIT_LGKM0();
-    PZ_RAW_BARRIER();
-    mask_tail_a(kt);
-    mfma_quad(1, 1);
-    PZ_RAW_BARRIER();
-    // phase 3: quadrant (1,0); retire the next K-step's phase-0 operands
-    if (n2) issue(2, s + 2);
-    if (n2) wait_vm8(adj);
-    else if (n1) wait_vm2(adj);
-    PZ_RAW_BARRIER();
-    mfma_quad(1, 0);
-    PZ_RAW_BARRIER();
-    adj = 0;
-    ++s;
-    if (s < cur_end) continue;
-
-    // ---- unit done: epilogue straight from the accumulators (no LDS), then the next unit ----
-    const bool last = !has_nxt;
-    if (last && wr == 0) PZ_RAW_BARRIER();
-    if (p.dbg != 1) {
-      if (cur.piece >= 0) {  // split tail: raw partial sums (gemm8p_tail_epilogue merges them)
-        f32x4* W = reinterpret_cast<f32x4*>(p.ws) + (int64_t)cur.piece * (32 * NT2);
-#pragma unroll
-        for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) W[(rb * 4 + cb) * NT2 + t] = acc[rb][cb];
-        adj = 32;
-      } else if (GEGLU) {
-        if (cur.m0 + BT <= p.M && cur.n0 + BT / 2 <= p.geglu_I && p.aux) {
-#pragma unroll
-          for (int rb = 0; rb < 8; ++rb) {
-            const int64_t m = cur.m0 + wr * 128 + rb * 16 + rl;
-            bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + m * p.ldc + cur.n0 + wc * 32 + g4;
-            bf16_t* Xr = p.aux + m * p.ld_aux + cur.n0 + wc * 32 + g4;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              float gg[4], uu[4], hh[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                gg[r] = acc[rb][j][r] * p.alpha;
-                uu[r] = acc[rb][2 + j][r] * p.alpha;
-                hh[r] = gelu_tanh(gg[r]) * uu[r];
-              }
-              *reinterpret_cast<u32x2*>(Cr + j * 16) = pk4(hh);
-              *reinterpret_cast<u32x2*>(Xr + j * 16) = pk4(gg);
-              *reinterpret_cast<u32x2*>(Xr + p.geglu_I + j * 16) = pk4(uu);
-            }
-          }
-          adj = 48;
-        } else {
-#pragma unroll
-          for (int rb = 0; rb < 8; ++rb) {
-            const int64_t m = cur.m0 + wr * 128 + rb * 16 + rl;
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              store_geglu4(p, 0, m, cur.n0 + wc * 32 + j * 16 + g4, acc[rb][j], acc[rb][2 + j]);
-          }
-        }
-      } else {
-        const int64_t m = cur.m0 + wr * 128 + rl, nb = cur.n0 + wc * 64 + g4;
-        if (cur.m0 + BT <= p.M && cur.n0 + BT <= p.N) {
-          epi8p_fast<FM>(p, 0, 0, m, nb, acc);
-          adj = 32;
-        } else {  // edge tile (FM_STORE: alpha * acc + bias), bounds-checked stores
-          float bias[4][4];
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) bias[cb][r] = (p.bias && nb + cb * 16 + r < p.N) ? bf2f(p.bias[nb + cb * 16 + r]) : 0.f;
-#pragma unroll
-          for (int rb = 0; rb < 8; ++rb) {
-            if (m + rb * 16 >= p.M) continue;
-            bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + (m + rb * 16) * p.ldc;
-#pragma unroll
-            for (int cb = 0; cb < 4; ++cb) {
-              const int64_t n = nb + cb * 16;
-              float v[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[cb][r];
-              if (n + 4 <= p.N) {
-                *reinterpret_cast<u32x2*>(Cr + n) = pk4(v);
-              } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  if (n + r < p.N) Cr[n + r] = f2bf(v[r]);
-              }
-            }
-          }
-        }
-      }
-    }
-    if (last) break;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    cur = nxt;
-    cur_start = cur_end;
-    cur_end = cur_start + cur.nk;
-    unxt += G;
-    has_nxt = unxt < U;
-    if (has_nxt) nxt = unit8_of<GEGLU>(p, unxt, nk_all);
-  }
-}
-
 // ---- k-half variant of the ping-pong kernel -----------------------------------
 // Same tile (256 x 256 x 64, 8 waves of 128 x 64), same accumulator layout, epilogue and split
 // tail as gemm8p_kernel, but each K-tile is consumed in TWO segments per wave -- k 0..31 then
@@ -2107,7 +1789,7 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS, PATH_2W };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
@@ -2201,32 +1883,7 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 }
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
-// allow_2w = false: never the two-workgroup kernel (pz_gemm_qkv_rope's RoPE epilogue lives in the 8-phase one)
-Plan make_plan(const pz_gemm_args* a, bool allow_2w = true);
-
-// two-resident-workgroup 256 x 128 kernel (pz_gemm_2w.hip) instead of the 8-phase 256 x 256 one for a
-// forward (NT) GEMM: its epilogue runs under the co-resident tile's main loop.  PZ_GEMM_2W=1: every
-// eligible shape, 0: never (A/B runs; read per call)
-bool use_2w(const pz_gemm_args* a, const Plan& pl) {
-  const char* e = getenv("PZ_GEMM_2W");
-  if (!(e && e[0] == '1')) return false;
-  return pl.akc && pl.bkc && a->batch == 1 && a->K % 32 == 0 && a->fp8_mode == 0 && !a->c_fp32 && !a->norm_w &&
-         a->epilogue <= PZ_EPI_SILU;
-}
-
-// pz_gemm's column split (see there): 256-tile bf16 plan, N % 256 == 128, >= one full round of whole tiles
-bool colsplit(const pz_gemm_args* a, const Plan& pl) {
-  // opt-in (PZ_GEMM_COLSPLIT=1): measured SLOWER -- the 128-column remainder on the 128-tile kernel costs more
-  // than the half-empty tile and split tail it removes (micro-batch GEMM census 234.7 vs 229.6 ms, bench 236.3
-  // vs 240.1 samples/s; profiles/r03/colsplit_ab.txt)
-  const char* e = getenv("PZ_GEMM_COLSPLIT");
-  if (!(e && e[0] == '1')) return false;
-  return pl.kind == PATH_256 && use_8phase() && a->fp8_mode == 0 && !pl.geglu && a->batch == 1 &&
-         a->epilogue != PZ_EPI_DGEGLU && !a->norm_w && a->N % 256 == 128 &&
-         pl.tiles_m * (a->N / 256) >= device_cus();
-}
-
-Plan make_plan(const pz_gemm_args* a, bool allow_2w) {
+Plan make_plan(const pz_gemm_args* a) {
   Plan pl{};
   pl.akc = a->a_kcontig != 0;
   pl.bkc = a->b_kcontig != 0;
@@ -2328,12 +1985,6 @@ Plan make_plan(const pz_gemm_args* a, bool allow_2w) {
   const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192) ? 256 : 512);
   if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= (pl.geglu ? 256 : 512)) {
     const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;
-    if (allow_2w && use_2w(a, pl)) {
-      pl.kind = PATH_2W;
-      pl.tiles_m = tm;
-      pl.tiles_n = (ncols + cw / 2 - 1) / (cw / 2);
-      return pl;
-    }
     Plan cand = pl;
     cand.kind = PATH_256;
     cand.tiles_m = tm;
@@ -2380,18 +2031,6 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   static thread_local char buf[160];
   if (!a) return "";
   const Plan pl = make_plan(a);
-  if (colsplit(a, pl)) {  // "<first N - 128 columns> | <last 128 columns>"
-    pz_gemm_args a1 = *a, a2 = *a;
-    a1.N = a->N - 128;
-    a2.N = 128;
-    char first[160];
-    snprintf(first, sizeof(first), "%s", pz_gemm_kernel_name(&a1));
-    const char* second = pz_gemm_kernel_name(&a2);
-    char tmp[160];
-    snprintf(tmp, sizeof(tmp), "%s | %s", first, second);
-    snprintf(buf, sizeof(buf), "%s", tmp);
-    return buf;
-  }
   switch (pl.kind) {
     case PATH_SKINNY:
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
@@ -2417,9 +2056,6 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
     case PATH_TILE:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
-      break;
-    case PATH_2W:
-      snprintf(buf, sizeof(buf), "gemm2w_kernel<%s>", bstr(pl.geglu));
       break;
     case PATH_ROWS:
       snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
@@ -2509,53 +2145,9 @@ static void launch_tail(const GemmP& p, int T, hipStream_t st) {
     hipLaunchKernelGGL((gemm8p_tail_epilogue<GEGLU, 8>), dim3((T - p.dp_tiles) * 16), dim3(NT2), 0, st, p);
 }
 
-// persistent 8-phase kernel (gemm8q_kernel) for k-contiguous A and B: batch 1, no fused RoPE epilogue
-// (its LDS staging), every work unit >= 2 K-steps; PZ_GEMM_PERSIST=0 keeps the one-shot kernel (A/B)
-static bool use_persist(const GemmP& p, int64_t batch, bool geglu) {
-  // opt-in (PZ_GEMM_PERSIST=1): measured SLOWER than the one-shot kernel on every Pi0 NT shape (vlm GeGLU
-  // 2.57 vs 2.12-2.19 ms, its main loop alone 1.83 vs 1.61 ms), kept for A/B runs
-  const char* e = getenv("PZ_GEMM_PERSIST");
-  if (!(e && e[0] == '1')) return false;
-  if (batch != 1 || p.rcs) return false;
-  // GeGLU and plain / bias-only outputs: the residual / activation epilogues (FM_BF16) round the Linear
-  // output to bf16 first (the reference's Linear -> add order, epi8p_staged) and load side inputs, so they
-  // keep the one-shot kernel
-  if (!geglu && fast_mode(p) != FM_STORE) return false;
-  const int nk = (int)((p.K + 63) / 64);
-  if (nk < 2) return false;
-  if (p.tail_s && nk - (p.tail_s - 1) * p.tail_kt < 2) return false;  // a 1-step last K-piece
-  return true;
-}
-
-template <bool GEGLU, bool KTAIL, int FM>
-static int launch8q(const GemmP& p, hipStream_t st) {
-  const int smem = 2 * P8_BUF;
-  auto kern = gemm8q_kernel<GEGLU, KTAIL, FM>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr_set = true;
-  }
-  const int T = p.tiles_m * p.tiles_n;
-  const int U = p.tail_s ? p.dp_tiles + (T - p.dp_tiles) * p.tail_s : T;
-  const int G = device_cus();
-  hipLaunchKernelGGL(kern, dim3((unsigned)(U < G ? U : G)), dim3(NT2), smem, st, p);
-  PZ_CHECK_LAUNCH();
-  if (p.tail_s) {
-    launch_tail<GEGLU>(p, T, st);
-    PZ_CHECK_LAUNCH();
-  }
-  return PZ_OK;
-}
-
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
-  if constexpr (AKC && BKC) {
-    if (use_persist(p, batch, GEGLU)) {
-      return launch8q<GEGLU, KTAIL, FM_STORE>(p, st);
-    }
-  }
   const bool kh = use_khalf(AKC, BKC);
   auto kern = kh ? gemm8k_kernel<AKC, BKC, GEGLU, KTAIL> : gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
   static bool attr_set[2] = {false, false};
@@ -2680,26 +2272,6 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
 
   const Plan pl = make_plan(a);
   if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
-  // column split: a 256-tile GEMM whose last column tile would be half empty (N % 256 == 128: SigLIP's
-  // 1152-wide outputs) runs its first N - 128 columns as whole 256-wide tiles (at least one full round, no
-  // split tail when the count is a multiple of the CUs) and the last 128 columns as a second GEMM on the
-  // planner's narrow path.  Every epilogue here is column-local (bias, residual, activation + aux, beta,
-  // fp32 C, activation backward).  Opt-in, PZ_GEMM_COLSPLIT=1 (A/B; read per call): see colsplit()
-  if (colsplit(a, pl)) {
-    const int64_t n1 = a->N - 128;
-    pz_gemm_args a1 = *a;
-    a1.N = n1;
-    int rc = pz_gemm(&a1, stream);
-    if (rc != PZ_OK) return rc;
-    pz_gemm_args a2 = *a;
-    a2.N = 128;
-    a2.B = (const bf16_t*)a->B + (a->b_kcontig ? n1 * a->ldb : n1);
-    a2.C = a->c_fp32 ? (void*)((float*)a->C + n1) : (void*)((bf16_t*)a->C + n1);
-    if (a->bias) a2.bias = (const bf16_t*)a->bias + n1;
-    if (a->resid) a2.resid = (const bf16_t*)a->resid + n1;
-    if (a->aux) a2.aux = (bf16_t*)a->aux + n1;
-    return pz_gemm(&a2, stream);
-  }
   if (a->norm_w)
     PZ_CHECK_ARG((pl.kind == PATH_SKINNY || pl.kind == PATH_SKINNY64) && PZ_ALIGNED(a->norm_w, 16),
                  "pz_gemm: fused RMSNorm needs the few-row paths (M <= 64, k-contiguous A/B, K %% 32 == 0 "
@@ -2734,7 +2306,6 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   p.tiles_m = (int)pl.tiles_m;
   p.tiles_n = (int)pl.tiles_n;
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
-  if (pl.kind == PATH_2W) return pz_2w_launch(p, geglu, st);
   if (pl.kind == PATH_ROWS)
     return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
   if (pl.kind == PATH_256 && use_8phase()) {
@@ -2808,7 +2379,7 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
     g.fp8_mode = 2;
     g.alpha = a->w_scale;
   }
-  const Plan pl = make_plan(&g, false);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
+  const Plan pl = make_plan(&g);  // no workspace: whole tiles only (the tail merge has no RoPE epilogue)
   // few rows (16 < M <= 64: C5's 50-row denoise chunk): the skinny-64 kernel with the RoPE epilogue, the
   // Gemma RMSNorm optionally fused (mixture.py:162-215 + utils.py:4-16 in one launch)
   if (pl.kind == PATH_SKINNY64 && pl.ksplit == 0 && a->K % 64 == 0 && a->N % 256 == 0 && a->M <= 64 &&

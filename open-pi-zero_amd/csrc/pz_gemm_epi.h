@@ -338,8 +338,5 @@ int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, bool f8w, hipStre
 // skinny-64 GEMM launcher (pz_gemm_rows.hip): 16 < M <= 64 rows (and fp8-weight W8A16), w waves, nc columns
 // per block, mb 16-row blocks
 int pz_sk64_launch(const GemmP& p, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st);
-// two-resident-workgroup 256 x 128 NT GEMM launcher (pz_gemm_2w.hip): k-contiguous A / B, K % 32 == 0, batch 1,
-// bf16 C, forward epilogues (no fused RoPE / norm)
-int pz_2w_launch(const GemmP& p, bool geglu, hipStream_t st);
 // split-K second pass (pz_gemm.hip): C = epilogue(sum of the S fp32 partial slabs in p.ws)
 int pz_splitk_epi_launch(const GemmP& p, int S, hipStream_t st);

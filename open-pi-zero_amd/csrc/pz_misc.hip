@@ -173,51 +173,6 @@ __global__ void euler_kernel(float* action, const bf16_t* __restrict__ v, int64_
   if (t && idx < B) t[idx] += dt;
 }
 
-// denoise-step tail in one launch (pizero.py:461-481 + vla/modules.py action decoder): the final action-expert
-// RMSNorm of one row (fp32 statistics, the (1 + w) scale, rounded to bf16 like pz_rmsnorm_fwd), the A-wide
-// decoder Linear (+ bias, rounded to bf16 like pz_gemm_small) and the Euler update action += dt * v; t += dt
-// once per sample.  One workgroup of 256 threads per row.
-constexpr int AHE_AMAX = 32;
-__global__ void __launch_bounds__(256) action_head_euler_kernel(const bf16_t* __restrict__ x, int64_t ldx,
-                                                                const bf16_t* __restrict__ nw, float eps,
-                                                                const bf16_t* __restrict__ W, int64_t ldw,
-                                                                const bf16_t* __restrict__ bias, float* action,
-                                                                float* t, int64_t H, int D, int A, float dt) {
-  __shared__ float red[AHE_AMAX + 1][4];
-  const int64_t r = blockIdx.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bf16_t* xr = x + r * ldx;
-  float ss = 0.f;
-  for (int e = tid; e < D; e += 256) {
-    const float v = bf2f(xr[e]);
-    ss += v * v;
-  }
-  ss = warp_sum(ss);
-  if (lane == 0) red[AHE_AMAX][wave] = ss;
-  __syncthreads();
-  const float rs = rsqrtf((red[AHE_AMAX][0] + red[AHE_AMAX][1] + red[AHE_AMAX][2] + red[AHE_AMAX][3]) / (float)D + eps);
-  float dot[AHE_AMAX];
-#pragma unroll
-  for (int a = 0; a < AHE_AMAX; ++a) dot[a] = 0.f;
-  for (int e = tid; e < D; e += 256) {
-    const float y = bf2f(f2bf(bf2f(xr[e]) * rs * (1.f + bf2f(nw[e]))));
-#pragma unroll
-    for (int a = 0; a < AHE_AMAX; ++a)
-      if (a < A) dot[a] += y * bf2f(W[a * ldw + e]);
-  }
-#pragma unroll
-  for (int a = 0; a < AHE_AMAX; ++a) {
-    if (a >= A) break;
-    const float s = warp_sum(dot[a]);
-    if (lane == 0) red[a][wave] = s;
-  }
-  __syncthreads();
-  if (tid < A) {
-    const float s = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3] + (bias ? bf2f(bias[tid]) : 0.f);
-    action[r * A + tid] += dt * bf2f(f2bf(s));
-  }
-  if (t && tid == 0 && r % H == 0) t[r / H] += dt;
-}
 
 __global__ void copy_rows_kernel(const bf16_t* __restrict__ src, int64_t sld, int64_t sbs, bf16_t* dst, int64_t dld,
                                  int64_t dbs, int64_t rows, int64_t D, float scale, int beta) {
@@ -496,18 +451,6 @@ extern "C" int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t 
   return PZ_OK;
 }
 
-extern "C" int pz_action_head_euler(const void* x, int64_t ldx, const void* norm_w, float eps, const void* W,
-                                    int64_t ldw, const void* bias, float* action, float* t, int64_t B, int64_t H,
-                                    int64_t D, int64_t A, float dt, void* stream) {
-  PZ_CHECK_ARG(x && norm_w && W && action && B > 0 && H > 0 && D > 0 && A >= 1 && A <= AHE_AMAX,
-               "action_head_euler: bad args (A <= %d)", AHE_AMAX);
-  hipLaunchKernelGGL(action_head_euler_kernel, dim3((unsigned)(B * H)), dim3(256), 0, ST, (const bf16_t*)x, ldx,
-                     (const bf16_t*)norm_w, eps, (const bf16_t*)W, ldw, (const bf16_t*)bias, action, t, H, (int)D,
-                     (int)A, dt);
-  PZ_CHECK_LAUNCH();
-  return PZ_OK;
-}
-
 extern "C" int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t dld, int64_t dbs, int64_t B,
                             int64_t rows, int64_t D, float scale, int32_t beta, void* stream) {
   PZ_CHECK_ARG(src && dst && B > 0 && rows > 0 && D > 0, "copy_rows: bad args");
@@ -515,30 +458,6 @@ extern "C" int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst
   const unsigned gx = (unsigned)(n / 256 + 1 < 1024 ? n / 256 + 1 : 1024);
   hipLaunchKernelGGL(copy_rows_kernel, dim3(gx, (unsigned)B), dim3(256), 0, ST, (const bf16_t*)src, sld, sbs,
                      (bf16_t*)dst, dld, dbs, rows, D, scale, (int)beta);
-  PZ_CHECK_LAUNCH();
-  return PZ_OK;
-}
-
-// Cache warm-up read (denoise weight prefetch): every thread reads 16-B chunks of [p, p + n16 * 16) in
-// strided order, 8 loads in flight, and keeps nothing -- the values are pinned live by an empty asm so the
-// loads are not removed; the bytes land in the MALL (and the reading XCD's L2) for the kernels that
-// stream them next.  Writes nothing.
-__global__ void __launch_bounds__(256) prefetch_kernel(const u32x4* __restrict__ p, int64_t n16) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += 8 * stride) {
-    u32x4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = i + u * stride < n16 ? p[i + u * stride] : u32x4{0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int u = 0; u < 8; ++u) asm volatile("" ::"v"(v[u]));
-  }
-}
-
-extern "C" int pz_prefetch(const void* p, int64_t bytes, int32_t workgroups, void* stream) {
-  PZ_CHECK_ARG(p && bytes >= 0 && workgroups > 0 && PZ_ALIGNED(p, 16), "prefetch: bad args");
-  const int64_t n16 = bytes / 16;
-  if (n16 == 0) return PZ_OK;
-  hipLaunchKernelGGL(prefetch_kernel, dim3((unsigned)workgroups), dim3(256), 0, ST, (const u32x4*)p, n16);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

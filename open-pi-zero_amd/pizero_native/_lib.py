@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 
-ABI_VERSION = 15  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 16  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -152,9 +152,7 @@ SIGNATURES = {
     "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
     "pz_flow_loss": [vp, i64, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
     "pz_euler_step": [vp, vp, i64, i64, vp, i64, i64, i64, f32, vp],
-    "pz_action_head_euler": [vp, i64, vp, f32, vp, i64, vp, vp, vp, i64, i64, i64, i64, f32, vp],
     "pz_copy_rows": [vp, i64, i64, vp, i64, i64, i64, i64, i64, f32, i32, vp],
-    "pz_prefetch": [vp, i64, i32, vp],
     "pz_time_embed_rows": [vp, vp, i64, i64, i64, i64, f32, i32, vp],
     "pz_clamp": [vp, i64, f32, f32, vp],
     "pz_geglu_bwd": [vp, i64, vp, i64, vp, vp, i64, i64, i64, vp],

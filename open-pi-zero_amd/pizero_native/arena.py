@@ -83,14 +83,6 @@ class Arena:
         v = b[a.offset : a.offset + n]
         return v.view(n // cols, cols) if len(a.shape) > 1 else v
 
-    def prefix_span(self, prefix, buf=None):
-        """1-D view from the first to the end of the last slot whose name starts with prefix (a layer's weights)"""
-        ss = [s for n, s in self.slots.items() if n.startswith(prefix)]
-        a = min(s.offset for s in ss)
-        z = max(s.offset + s.numel for s in ss)
-        b = self.data if buf is None else buf
-        return b[a : z]
-
     def grad_view(self, name):
         return self.view(name, self.ensure_grad())
 

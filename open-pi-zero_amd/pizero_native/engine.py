@@ -1168,11 +1168,6 @@ class Engine:
         f = self.f8.get(p + "self_attn.q_proj.weight") if self.f8 else None
         return (self.qkv_w(p), None) if f is None else (f[0], f[1])
 
-    def prefetch_weights(self):
-        """workgroups of the denoise weight prefetch (pz_prefetch of layer l+1 on a side stream while layer l
-        runs; PZ_PREFETCH=<workgroups>, 0 = off)"""
-        return int(os.environ.get("PZ_PREFETCH", "0"))
-
     def few_rows(self, M, K):
         """row counts the few-row GEMM kernels take with the RMSNorm fused (pz_gemm skinny paths:
         M <= 16 with K % 32 == 0, 16 < M <= 64 with K % 64 == 0)"""
@@ -1387,16 +1382,10 @@ class Engine:
                   False, "action")
         Q = torch.empty(B, d.H, nh * hd, device=dev, dtype=BF16)
         S = Pm = O = None
-        pf = self.prefetch_weights()
-        side = self._side_stream(dev) if pf else None
         for l in range(d.nL):
             p = f"{g.prefix}{l}."
             Kj, Vj = kcache[l], vcache[l]
             M = x.shape[0]
-            if pf:  # warm layer l+1's weights (the next step's layer 0 after the last) beside layer l's chain
-                side.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(side):
-                    ops.prefetch(self.ar.prefix_span(f"{g.prefix}{(l + 1) % d.nL}."), pf)
             nrm = (self.w(p + "input_layernorm.weight"), d.rms_eps)
             if self.gemv_ok(M, d.aH):  # one launch: RMSNorm + q|k|v GEMV + RoPE + Q / K-cache / V-cache scatter
                 ops.gemv_qkv_rope(x, self.qkv_w(p), apos, self.rope(g.theta), Q, Kj, Vj, d.H, nh, hd, d.H, 0, Lp,
@@ -1433,15 +1422,6 @@ class Engine:
             ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0,
                              rows_per_batch=d.H * nh, heads=nh, qoff=d.P + d.C, **_mask_kw(d, cnt, "act"))
             x = self._post_attn(g, p, x, Pm, Vj, B, d.H, Lp, qrow0=0)
-        if pf:
-            torch.cuda.current_stream(dev).wait_stream(side)  # join the side stream (graph capture needs it)
-        # norm + decoder + Euler update in one launch: opt-in (PZ_FUSED_HEAD=1) -- measured neutral (C4 12.89 vs
-        # 12.87 ms, C5 21.32 vs 21.32 ms, profiles/r03/fused_head_ab.txt), so the three-launch path stays the default
-        if os.environ.get("PZ_FUSED_HEAD", "0") == "1":
-            ops.action_head_euler(x, self.w("joint_model.mixtures.action.norm.weight"), d.rms_eps,
-                                  self.w("action_decoder.weight"), self.w("action_decoder.bias"), action, t, B, d.H,
-                                  1.0 / d.steps)
-            return
         y = torch.empty_like(x)
         ops.rmsnorm(x, self.w("joint_model.mixtures.action.norm.weight"), y, None, d.rms_eps)
         v = torch.empty(B * d.H, 8, device=dev, dtype=BF16)

@@ -54,7 +54,11 @@ class InferenceGraph:
         s["noise"].copy_(noise.reshape(s["noise"].shape))
 
     def capture(self):
-        self._f8 = self.m._engine().f8
+        # re-quantise stale fp8 codes first, so the codes recorded here are the ones the captured launches read
+        # (the warm-up's infer_action would otherwise replace them and force a needless re-capture)
+        e = self.m._engine()
+        e.fp8_refresh()
+        self._f8 = e.f8
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):

@@ -581,21 +581,8 @@ def euler_step(action, v, ldv, vbs, t, B, H, A, dt):
     call("pz_euler_step", _p(action), _p(v), ldv, vbs, _p(t), B, H, A, float(dt), _st())
 
 
-def action_head_euler(x, norm_w, eps, W, bias, action, t, B, H, dt):
-    """RMSNorm(x) -> decoder W [A, D] (+ bias) -> action += dt * v, t += dt: the denoise step's tail, one launch"""
-    D = x.shape[1]
-    A = W.shape[0]
-    call("pz_action_head_euler", _p(x), x.stride(0), _p(norm_w), float(eps), _p(W), W.stride(0), _p(bias),
-         _p(action), _p(t), B, H, D, A, float(dt), _st())
-
-
 def copy_rows(src, sld, sbs, dst, dld, dbs, B, rows, D, scale=1.0, beta=False):
     call("pz_copy_rows", _p(src), sld, sbs, _p(dst), dld, dbs, B, rows, D, float(scale), int(beta), _st())
-
-
-def prefetch(t, workgroups=64):
-    """read the bytes of t once into the caches (pz_prefetch), on the current stream"""
-    call("pz_prefetch", _p(t), t.numel() * t.element_size(), int(workgroups), _st())
 
 
 def clamp_(x, lo, hi):

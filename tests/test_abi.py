@@ -60,13 +60,4 @@ def test_gemm_planner_routes_without_gpu():
     assert not ops.gemm_kernel_name(64, 1024, 1024).startswith("gemm_rows")  # few-row paths keep M <= 64
     assert not ops.gemm_kernel_name(17664, 2560, 2048).startswith("gemm_rows")  # training rows: 8-phase
     assert not ops.gemm_kernel_name(320, 1024, 2048, a_kc=False).startswith("gemm_rows")  # k-strided A
-    import os
-    os.environ["PZ_GEMM_2W"] = "1"  # opt-in two-workgroup kernel: forward NT shapes with K % 32 == 0 only
-    try:
-        assert ops.gemm_kernel_name(16384, 1152, 1152) == "gemm2w_kernel<false>"
-        assert ops.gemm_kernel_name(17664, 32768, 2048, epi=geglu, geglu_inter=16384) == "gemm2w_kernel<true>"
-        assert not ops.gemm_kernel_name(16384, 1152, 4304).startswith("gemm2w")  # K % 32 != 0
-        assert not ops.gemm_kernel_name(16384, 1152, 1152, b_kc=False).startswith("gemm2w")  # dgrad layout
-    finally:
-        del os.environ["PZ_GEMM_2W"]
     assert ops.gemm_kernel_name(16384, 1152, 1152).startswith("gemm8p_kernel")

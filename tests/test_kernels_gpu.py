@@ -572,50 +572,6 @@ def test_layernorm_fwd_bwd(kern, monkeypatch):
         assert (s1.float() - s2.float()).abs().max().item() <= 2 * 2 ** -7 * s2.float().abs().max().item() + 1e-3
 
 
-@pytest.mark.parametrize("akc,bkc", [(True, True), (True, False), (False, True)])
-def test_gemm_column_split(akc, bkc, monkeypatch):
-    """N % 256 == 128 with >= one full round of 256-wide tiles (SigLIP's 1152-wide outputs at micro-batch 64):
-    the first N - 128 columns on the 8-phase kernel, the last 128 on the narrow path (pz_gemm column split,
-    opt-in PZ_GEMM_COLSPLIT=1: measured slower); every column-local epilogue against torch fp32 and against the
-    one-launch plan (PZ_GEMM_COLSPLIT=0)."""
-    from pizero_native import ops
-
-    M, N, K = 16384, 1152, 1152
-    monkeypatch.setenv("PZ_GEMM_COLSPLIT", "1")
-    name = ops.gemm_kernel_name(M, N, K, a_kc=akc, b_kc=bkc)
-    assert " | " in name, name
-    A = bf(M, K) if akc else bf(K, M)
-    Bm = bf(N, K, scale=K ** -0.5) if bkc else bf(K, N, scale=K ** -0.5)
-    lda, ldb = (K if akc else M), (K if bkc else N)
-    Af = A.float() if akc else A.float().t()
-    Bf = Bm.float() if bkc else Bm.float().t()
-    ref = Af @ Bf.t()
-    b, r = bf(N), bf(M, N)
-    outs = {}
-    for cs in ("1", "0"):
-        monkeypatch.setenv("PZ_GEMM_COLSPLIT", cs)
-        o1 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o1, N, bias=b, resid=r, ld_resid=N)
-        pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        o2 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o2, N, bias=b, epi=ops.PZ_EPI_GELU, aux=pre, ld_aux=N)
-        o3 = torch.ones(M, N, device=dev, dtype=torch.float32)
-        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o3, N, beta=True)
-        o4 = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.gemm(M, N, K, A, lda, akc, Bm, ldb, bkc, o4, N, epi=ops.PZ_EPI_DGELU, aux=r, ld_aux=N)
-        outs[cs] = (o1, pre, o2, o3, o4)
-    o1, pre, o2, o3, o4 = outs["1"]
-    close(o1, ref + b.float() + r.float(), atol=2e-2)
-    close(pre, ref + b.float())
-    close(o2, torch.nn.functional.gelu(ref + b.float(), approximate="tanh"))
-    close(o3, 1.0 + ref, rtol=1e-3, atol=1e-3)
-    xr = r.float().requires_grad_()
-    torch.nn.functional.gelu(xr, approximate="tanh").backward(torch.ones_like(xr))
-    close(o4, ref * xr.grad, atol=2e-2)
-    for a_, b_ in zip(outs["1"], outs["0"]):  # the one-launch plan (its leftover tiles sum K-pieces: not bitwise)
-        close(a_, b_, rtol=2e-2, atol=2e-2)
-
-
 def test_reduce_parts_multi_matches_single():
     """pz_reduce_parts_multi (a layer's partial-sum reductions in one launch, > 8 segments = two launches) is
     bit-identical to one pz_reduce_parts per segment, beta included."""
@@ -800,33 +756,6 @@ def test_wgrad_split_k_matches_single_pass():
     close(dW, 2 * ref, atol=0.1 * math.sqrt(M) / 16)
 
 
-@pytest.mark.parametrize("B,H,D,A", [(1, 4, 1024, 7), (1, 50, 1024, 7), (3, 5, 96, 7), (2, 4, 1024, 32)])
-def test_action_head_euler_matches_unfused(B, H, D, A):
-    """pz_action_head_euler (final action RMSNorm + decoder + Euler update in one launch) vs pz_rmsnorm_fwd +
-    pz_gemm_small + pz_euler_step: the normed row identical, v within one bf16 rounding of the reordered fp32 dot,
-    t advanced once per sample."""
-    from pizero_native import ops
-
-    x, nw = bf(B * H, D), bf(D, scale=0.1)
-    W, bias = bf(A, D, scale=D ** -0.5), bf(A, scale=0.1)
-    a0 = torch.randn(B, H, A, device=dev)
-    t0 = torch.rand(B, device=dev)
-    a1, t1 = a0.clone(), t0.clone()
-    y = torch.empty_like(x)
-    ops.rmsnorm(x, nw, y, None, 1e-6)
-    lv = max(8, A)
-    v = torch.empty(B * H, lv, device=dev, dtype=torch.bfloat16)
-    ops.small_linear(y, W, v[:, :A], bias=bias)
-    ops.euler_step(a1, v, lv, H * lv, t1, B, H, A, 0.1)
-    a2, t2 = a0.clone(), t0.clone()
-    ops.action_head_euler(x, nw, 1e-6, W, bias, a2, t2, B, H, 0.1)  # (opt-in in the engine: PZ_FUSED_HEAD=1)
-    assert torch.equal(t1, t2)
-    vmax = v[:, :A].float().abs().max().item()
-    assert (a1 - a2).abs().max().item() <= 0.1 * vmax * 2 ** -7 + 1e-6
-    ref = (y.float() @ W.float().t() + bias.float()).view(B, H, A)
-    close(a2, a0 + 0.1 * ref, rtol=1e-2, atol=1e-3)
-
-
 @pytest.mark.parametrize("mode", [False, True])
 def test_time_embed_rows_matches_embed_plus_concat(mode):
     """pz_time_embed_rows (inference: the embedding written into the concat input's first D columns, H rows per
@@ -871,21 +800,17 @@ def test_time_embed_modes_match_reference():
         assert outs[1] < outs[0], outs
 
 
-@pytest.mark.parametrize("mode", ["mfma", "one", "valu", "mfma_wg64"])
+@pytest.mark.parametrize("mode", ["mfma", "mfma_wg64"])
 @pytest.mark.parametrize("B,T,cnts,P", [(1, 4, [270], 276), (2, 4, [276, 259], 276), (1, 2, [100], 276),
                                           (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276)])
 def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
     with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
     P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  mode "mfma": the
-    key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default); "one": one workgroup walks
-    every key chunk (no merge launch); "valu": the VALU P.V part kernel; "mfma_wg64": several chunks per
-    workgroup (online softmax across chunks) + merge"""
+    key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default); "mfma_wg64": several chunks
+    per workgroup (online softmax across chunks) + merge"""
     from pizero_native import ops
 
-    monkeypatch.setenv("PZ_DECODE_ONE", "1" if mode == "one" else "0")
-    if mode == "valu":
-        monkeypatch.setenv("PZ_DECODE_PART", "valu")
     if mode == "mfma_wg64":
         monkeypatch.setenv("PZ_DECODE_WG", "4")
     C, nh, hd = 1, 8, 256
@@ -1004,127 +929,3 @@ def test_gemm_qkv_rope_bit_identical_to_gemm_plus_split(B, T, off):
         assert torch.equal(a, b), (nm, float((a.float() - b.float()).abs().max()))
     if T >= 256:  # the rows the fused epilogue did not own are untouched
         assert (outs[0][0][:, T + off:] == 7.0).all() and (outs[0][1][:, T + off:] == 7.0).all()
-
-
-@pytest.mark.parametrize("case", ["geglu_4416", "geglu_300", "plain_qkv", "resid_oproj", "sig_fc1_gelu_aux",
-                                  "sig_fc2_ktail_resid", "sig_out_tail_bias_resid", "plain_edge_rows_cols"])
-def test_persistent_8phase_bit_identical_to_one_shot(case, monkeypatch):
-    """gemm8q_kernel (persistent 8-phase: one workgroup per CU walking tiles + split-tail K-pieces as one
-    K-step stream, epilogue stores straight from the accumulators) against the one-shot gemm8p_kernel
-    (PZ_GEMM_PERSIST=0): the same per-tile K order, so every output (C, saved aux) is bit-identical --
-    GeGLU, plain, residual, GELU + bias + saved pre-activation, a K % 64 tail, split-tail shapes and
-    partial edge tiles.  Both are also checked against torch fp32."""
-    from pizero_native import ops
-
-    M, N, K, kw = {
-        "geglu_4416": (4416, 2 * 4096, 2048, dict(geglu=True)),
-        "geglu_300": (300, 2 * 16384, 2048, dict(geglu=True)),
-        "plain_qkv": (4416, 2560, 2048, {}),
-        "resid_oproj": (17664, 2048, 2048, dict(resid=True)),
-        "sig_fc1_gelu_aux": (16384, 4304, 1152, dict(bias=True, gelu=True)),
-        "sig_fc2_ktail_resid": (16384, 1152, 4304, dict(bias=True, resid=True)),
-        "sig_out_tail_bias_resid": (16384, 1152, 1152, dict(bias=True, resid=True)),
-        "plain_edge_rows_cols": (2000, 1000, 1024, {}),
-    }[case]
-    x, W = bf(M, K), bf(N, K, scale=K ** -0.5)
-    b = bf(N) if kw.get("bias") else None
-    r = bf(M, N) if kw.get("resid") else None
-    name = ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU if kw.get("geglu") else
-                                (ops.PZ_EPI_GELU if kw.get("gelu") else ops.PZ_EPI_NONE), geglu_inter=N // 2)
-    assert name.startswith("gemm8p_kernel"), name  # an 8-phase shape (the persistent kernel replaces it)
-
-    def run():
-        if kw.get("geglu"):
-            out = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
-            aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            ops.linear(x, W, out, epi=ops.PZ_EPI_GEGLU, aux=aux)
-            return out, aux
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        aux = torch.empty(M, N, device=dev, dtype=torch.bfloat16) if kw.get("gelu") else None
-        ops.linear(x, W, out, bias=b, resid=r, epi=ops.PZ_EPI_GELU if kw.get("gelu") else ops.PZ_EPI_NONE, aux=aux)
-        return out, aux
-
-    monkeypatch.setenv("PZ_GEMM_PERSIST", "0")
-    o1, a1 = run()
-    monkeypatch.setenv("PZ_GEMM_PERSIST", "1")  # opt-in A/B kernel (not the default: measured slower)
-    o2, a2 = run()
-    torch.cuda.synchronize()
-    assert torch.equal(o1, o2), float((o1.float() - o2.float()).abs().max())
-    if a1 is not None:
-        assert torch.equal(a1, a2), float((a1.float() - a2.float()).abs().max())
-    rows = slice(0, min(M, 512))  # fp32 reference on a row slice
-    pre = x[rows].float() @ W.float().t()
-    if kw.get("geglu"):
-        g, u = pre[:, : N // 2], pre[:, N // 2:]
-        close(o2[rows], torch.nn.functional.gelu(g, approximate="tanh") * u, rtol=3e-2, atol=3e-2)
-    else:
-        if b is not None:
-            pre = pre + b.float()
-        ref = torch.nn.functional.gelu(pre, approximate="tanh") if kw.get("gelu") else pre
-        if r is not None:
-            ref = ref + r[rows].float()
-        close(o2[rows], ref, rtol=3e-2, atol=3e-2)
-
-
-@pytest.mark.parametrize("M,N,K", [(1024, 1152, 1152), (512, 3456, 1152), (768, 2048, 2048), (512, 1024, 32),
-                                   (512, 768, 64), (600, 1000, 416), (1300, 520, 96)])
-def test_gemm2w_forward_epilogues(M, N, K, monkeypatch):
-    """Two-resident-workgroup 256 x 128 NT GEMM (pz_gemm_2w.hip, PZ_GEMM_2W=1): every forward epilogue (bias,
-    residual, GELU / SiLU + saved pre-activation, bf16 beta accumulation, GeGLU + saved g|u), 1- and 2-K-tile
-    pipelines, row / column edge tiles; against torch fp32 and -- interior-only shapes -- bit-identical to the
-    8-phase kernel without its split tail (same k order, same epilogue rounding)."""
-    from pizero_native import ops
-
-    x, W, b, r = bf(M, K), bf(N, K, scale=K ** -0.5), bf(N), bf(M, N)
-    c0 = bf(M, N)
-    I = N // 2 // 4 * 4
-
-    def run():
-        outs = []
-        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.linear(x, W, o, bias=b, resid=r)
-        outs.append(o)
-        o, pre = torch.empty(M, N, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.linear(x, W, o, bias=b, epi=ops.PZ_EPI_GELU, aux=pre)
-        outs += [o, pre]
-        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.linear(x, W, o, epi=ops.PZ_EPI_SILU)
-        outs.append(o)
-        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-        ops.linear(x, W, o)
-        outs.append(o)
-        o = c0.clone()
-        ops.gemm(M, N, K, x, K, True, W, K, True, o, N, beta=True)
-        outs.append(o)
-        if I * 2 == N:
-            h, gu = torch.empty(M, I, device=dev, dtype=torch.bfloat16), torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            ops.linear(x, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
-            outs += [h, gu]
-        return outs
-
-    monkeypatch.setenv("PZ_GEMM_2W", "1")
-    monkeypatch.setenv("PZ_GEMM_256_MINM", "256")
-    monkeypatch.setenv("PZ_GEMM_256_MINUNITS", "1")
-    monkeypatch.setenv("PZ_GEMM_ROWS", "0")
-    assert ops.gemm_kernel_name(M, N, K) == "gemm2w_kernel<false>", ops.gemm_kernel_name(M, N, K)
-    if I * 2 == N:
-        assert ops.gemm_kernel_name(M, N, K, epi=ops.PZ_EPI_GEGLU, geglu_inter=I) == "gemm2w_kernel<true>"
-    got = run()
-    ref = x.float() @ W.float().t()
-    close(got[0], ref + b.float() + r.float(), atol=2e-2)
-    close(got[1], torch.nn.functional.gelu(ref + b.float(), approximate="tanh"))
-    close(got[2], ref + b.float())
-    close(got[3], torch.nn.functional.silu(ref))
-    close(got[4], ref)
-    close(got[5], c0.float() + ref, atol=2e-2)
-    if I * 2 == N:
-        close(got[7], ref)
-        close(got[6], torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:], rtol=3e-2, atol=3e-2)
-    if M % 256 == 0 and N % 256 == 0:
-        monkeypatch.setenv("PZ_GEMM_2W", "0")
-        monkeypatch.setenv("PZ_GEMM_TAIL", "0")
-        assert ops.gemm_kernel_name(M, N, K).startswith("gemm8p_kernel"), ops.gemm_kernel_name(M, N, K)
-        want = run()
-        torch.cuda.synchronize()
-        for i, (a, c) in enumerate(zip(got, want)):
-            assert torch.equal(a, c), (i, float((a.float() - c.float()).abs().max()))

@@ -39,6 +39,17 @@ PY
     c5prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/c5prof" -o c5 \
         -- python3 tools/c5_bench.py --iters 20 > "$OUT/c5prof.log" 2>&1 ;;
+    ddpab)  # same box, same build: plain vs the forced world-1 DDP path (RCCL bucket all-reduce on the comm stream)
+      timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
+        > "$OUT/ab_plain.log" 2>&1
+      timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline --force-ddp \
+        > "$OUT/ab_ddp.log" 2>&1
+      timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
+        > "$OUT/ab_plain2.log" 2>&1 ;;
+    ddpprof)  # kernel trace of the forced-DDP step (compare with prof's plain-step stats)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ddpprof" -o ddp \
+        -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline --force-ddp > "$OUT/ddpprof.log" 2>&1
+      rm -f "$OUT"/ddpprof/*/*kernel_trace.csv "$OUT"/ddpprof/*kernel_trace.csv ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     flashbench)

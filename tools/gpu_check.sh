@@ -22,7 +22,11 @@ for s in $STEPS; do
       # dominant GEMM only (grid split / duration check) and the stats summary
       python3 - "$OUT/prof" <<'PY'
 import csv, glob, os, sys
+import subprocess
 for f in glob.glob(os.path.join(sys.argv[1], "*kernel_trace.csv")):
+    with open(f.replace("kernel_trace.csv", "gaps.txt"), "w") as g:
+        subprocess.run([sys.executable, "tools/trace_gaps.py", f, "--after-ms", os.environ.get("GAPS_AFTER_MS", "0")],
+                       stdout=g, stderr=subprocess.STDOUT)
     with open(f) as fi, open(f.replace("kernel_trace", "dominant_trace"), "w", newline="") as fo:
         r = csv.DictReader(fi)
         w = csv.DictWriter(fo, fieldnames=r.fieldnames)
@@ -49,7 +53,16 @@ PY
     ddpprof)  # kernel trace of the forced-DDP step (compare with prof's plain-step stats)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/ddpprof" -o ddp \
         -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline --force-ddp > "$OUT/ddpprof.log" 2>&1
-      rm -f "$OUT"/ddpprof/*/*kernel_trace.csv "$OUT"/ddpprof/*kernel_trace.csv ;;
+      for f in "$OUT"/ddpprof/*kernel_trace.csv "$OUT"/ddpprof/*/*kernel_trace.csv; do
+        if [ -f "$f" ]; then python3 tools/trace_gaps.py "$f" > "${f%kernel_trace.csv}gaps.txt" 2>&1; rm -f "$f"; fi
+      done ;;
+    gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels
+      timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/gaps" -o gaps \
+        -- python3 bench.py --steps 2 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/gaps.log" 2>&1
+      for f in "$OUT"/gaps/*kernel_trace.csv "$OUT"/gaps/*/*kernel_trace.csv; do
+        if [ -f "$f" ]; then python3 tools/trace_gaps.py "$f" --last-ms ${GAPS_LAST_MS:-8000} --top 40 \
+          > "$OUT/gaps.txt" 2>&1; rm -f "$f"; fi
+      done ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 ;;
     flashbench)

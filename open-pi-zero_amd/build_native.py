@@ -21,7 +21,7 @@ OUT = os.path.join(HERE, "libpizero_hip.so")
 BUILD = os.path.join(HERE, "build")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-SOURCES = ["pz_gemm.hip", "pz_gemm_rows.hip", "pz_norm.hip", "pz_attn.hip", "pz_misc.hip", "pz_flash.hip", "pz_optim.hip", "pz_gemv.hip", "pz_decode.hip", "pz_quant.hip"]
+SOURCES = ["pz_gemm.hip", "pz_gemm_rows.hip", "pz_gemm_tall.hip", "pz_norm.hip", "pz_attn.hip", "pz_misc.hip", "pz_flash.hip", "pz_optim.hip", "pz_gemv.hip", "pz_decode.hip", "pz_quant.hip"]
 HEADERS = [os.path.join(CSRC, "pz_common.h"), os.path.join(CSRC, "pz_gemm_epi.h"), os.path.join(ROOT, "include", "pz_abi.h")]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result",
          "-Wno-unused-value", "-munsafe-fp-atomics"]

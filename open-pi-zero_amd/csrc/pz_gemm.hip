@@ -1789,7 +1789,7 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc);
 
 namespace {
-enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS };
+enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS, PATH_TALL };
 struct Plan {
   PathKind kind;
   bool akc, bkc, geglu;
@@ -1798,6 +1798,7 @@ struct Plan {
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
   int rows_w, rows_tnb, rows_tmb;  // row-slab kernel: waves, 16-column / 16-row blocks per tile
   bool rows_f8;                    // ... with e4m3 weight codes (W8A16)
+  int tall_mi;                     // tall-tile kernel: 64 * tall_mi rows per tile (4 | 5)
 };
 
 // compute units of the current device (the "wave" of resident 8-phase workgroups: 1 per CU)
@@ -1879,6 +1880,40 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   pl.rows_tmb = tmb;
   pl.tiles_m = tm;
   pl.tiles_n = (ncols + 16 * tnb - 1) / (16 * tnb);
+  return true;
+}
+
+// tall-tile kernel (pz_gemm_tall.hip): 64 < M <= 1024 rows, k-contiguous A and B, batch 1, bf16 operands, forward
+// epilogues: one 256- or 320-row tile covers up to 320 rows (the B = 1 prefill's 276 rows in ONE row tile instead of
+// the 8-phase kernel's two 256-row tiles), 64 output columns per tile, K split over blockIdx.y until the grid
+// reaches ~256 workgroups.  PZ_GEMM_TALL=1: every eligible shape, 0: never (A/B runs; read per call)
+bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
+  const char* e = getenv("PZ_GEMM_TALL");
+  if (!(e && e[0] == '1')) return false;
+  if (!pl.akc || !pl.bkc || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
+      a->M <= 64 || a->M > 1024 || a->K % 8 != 0)
+    return false;
+  const int64_t t5 = (a->M + 319) / 320, t4 = (a->M + 255) / 256;
+  pl.tall_mi = t5 * 320 <= t4 * 256 ? 5 : 4;
+  pl.tiles_m = pl.tall_mi == 5 ? t5 : t4;
+  pl.tiles_n = (ncols + 63) / 64;
+  const int64_t bkt = pl.geglu ? 32 : 64;
+  const int64_t nk = (a->K + bkt - 1) / bkt;
+  const int64_t units = pl.tiles_m * pl.tiles_n;
+  int64_t S = (256 + units - 1) / units;
+  S = S < nk / 4 ? S : nk / 4;  // >= 4 K-tiles per split
+  S = S < 16 ? S : 16;
+  if (S >= 2) {
+    const int64_t per = (nk + S - 1) / S;
+    const int64_t Se = (nk + per - 1) / per;
+    const int64_t ldw = pl.geglu ? 2 * a->geglu_inter : (a->N + 3) / 4 * 4;
+    if (Se >= 2 && a->workspace && PZ_ALIGNED(a->workspace, 16) && Se * a->M * ldw * 4 <= a->ws_bytes) {
+      pl.splits = (int)Se;
+      pl.ksplit = per * bkt;
+      pl.ldw = ldw;
+    }
+  }
+  pl.kind = PATH_TALL;
   return true;
 }
 
@@ -1972,6 +2007,7 @@ Plan make_plan(const pz_gemm_args* a) {
     return pl;
   }
   const int64_t cw = pl.geglu ? BT / 2 : BT;
+  if (plan_tall(pl, a, ncols)) return pl;
   // the row-slab kernel before the 256-tile kernels (action-expert gate|up at 320 rows); PZ_ROWS_FIRST=1 for
   // every shape it takes (A/B runs; read per call)
   {
@@ -2060,6 +2096,10 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
     case PATH_ROWS:
       snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
                bstr(pl.geglu), bstr(pl.rows_f8));
+      break;
+    case PATH_TALL:
+      snprintf(buf, sizeof(buf), "gemm_tall_kernel<%d, %d, %d, %d, %s>%s", pl.tall_mi, pl.geglu ? 4 : 2,
+               pl.geglu ? 32 : 64, pl.geglu ? 4 : 3, bstr(pl.geglu), pl.splits > 1 ? "+splitk_epilogue_kernel" : "");
       break;
     case PATH_SPLIT:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
@@ -2308,6 +2348,14 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   PZ_CHECK_ARG(pl.tiles_m * pl.tiles_n < (1LL << 31) && a->batch < 65536, "pz_gemm: grid too large");
   if (pl.kind == PATH_ROWS)
     return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, pl.geglu, pl.rows_f8, st);
+  if (pl.kind == PATH_TALL) {
+    if (pl.splits > 1) {
+      p.ws = (float*)a->workspace;
+      p.ksplit = pl.ksplit;
+      p.ldw = pl.ldw;
+    }
+    return pz_tall_launch(p, pl.tall_mi, geglu, pl.splits > 1 ? pl.splits : 1, st);
+  }
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {
       p.ws = (float*)a->workspace;

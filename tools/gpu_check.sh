@@ -56,6 +56,13 @@ PY
       for f in "$OUT"/ddpprof/*kernel_trace.csv "$OUT"/ddpprof/*/*kernel_trace.csv; do
         if [ -f "$f" ]; then python3 tools/trace_gaps.py "$f" > "${f%kernel_trace.csv}gaps.txt" 2>&1; rm -f "$f"; fi
       done ;;
+    mbab)  # micro-batch 128 x accumulation 8 against the default 64 x 16 (same box)
+      timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
+        --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1
+      timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
+        > "$OUT/ab_mb64.log" 2>&1 ;;
+    tallbench)
+      timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels
       timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/gaps" -o gaps \
         -- python3 bench.py --steps 2 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/gaps.log" 2>&1

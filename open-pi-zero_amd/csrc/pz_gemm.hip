@@ -1890,7 +1890,7 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   const char* e = getenv("PZ_GEMM_TALL");
   if (!(e && e[0] == '1')) return false;
-  if (!pl.akc || !pl.bkc || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
+  if (!pl.akc || (!pl.bkc && pl.geglu) || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
       a->M <= 64 || a->M > 1024 || a->K % 8 != 0)
     return false;
   const int64_t t5 = (a->M + 319) / 320, t4 = (a->M + 255) / 256;
@@ -2098,8 +2098,9 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
                bstr(pl.geglu), bstr(pl.rows_f8));
       break;
     case PATH_TALL:
-      snprintf(buf, sizeof(buf), "gemm_tall_kernel<%d, %d, %d, %d, %s>%s", pl.tall_mi, pl.geglu ? 4 : 2,
-               pl.geglu ? 32 : 64, pl.geglu ? 4 : 3, bstr(pl.geglu), pl.splits > 1 ? "+splitk_epilogue_kernel" : "");
+      snprintf(buf, sizeof(buf), "gemm_tall_kernel<%d, %d, %d, %d, %s, %s>%s", pl.tall_mi, pl.geglu ? 4 : 2,
+               pl.geglu ? 32 : 64, pl.geglu ? 4 : 3, bstr(pl.geglu), bstr(pl.bkc),
+               pl.splits > 1 ? "+splitk_epilogue_kernel" : "");
       break;
     case PATH_SPLIT:
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>+splitk_epilogue_kernel(S=%d)", bstr(pl.akc),
@@ -2354,7 +2355,7 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
       p.ksplit = pl.ksplit;
       p.ldw = pl.ldw;
     }
-    return pz_tall_launch(p, pl.tall_mi, geglu, pl.splits > 1 ? pl.splits : 1, st);
+    return pz_tall_launch(p, pl.tall_mi, geglu, pl.bkc, pl.splits > 1 ? pl.splits : 1, st);
   }
   if (pl.kind == PATH_256 && use_8phase()) {
     if (pl.tail_s) {

@@ -338,7 +338,8 @@ int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, bool f8w, hipStre
 // skinny-64 GEMM launcher (pz_gemm_rows.hip): 16 < M <= 64 rows (and fp8-weight W8A16), w waves, nc columns
 // per block, mb 16-row blocks
 int pz_sk64_launch(const GemmP& p, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st);
-// tall-tile GEMM launcher (pz_gemm_tall.hip): 64 * mi rows per tile, split-K over blockIdx.y when splits > 1
-int pz_tall_launch(const GemmP& p, int mi, bool geglu, int splits, hipStream_t st);
+// tall-tile GEMM launcher (pz_gemm_tall.hip): 64 * mi rows per tile, k-contiguous A, B k-contiguous or (plain
+// epilogues) k-strided, split-K over blockIdx.y when splits > 1
+int pz_tall_launch(const GemmP& p, int mi, bool geglu, bool bkc, int splits, hipStream_t st);
 // split-K second pass (pz_gemm.hip): C = epilogue(sum of the S fp32 partial slabs in p.ws)
 int pz_splitk_epi_launch(const GemmP& p, int S, hipStream_t st);

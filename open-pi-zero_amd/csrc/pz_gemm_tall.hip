@@ -65,6 +65,30 @@ __device__ __forceinline__ void tl_wait_vm(int n) {  // wave-uniform count -> im
   }
 }
 
+// k-strided B image [BKT k][64 columns] (128-B k-rows) for ds_read_b64_tr_b16: the 8-B column unit u of k-row k
+// sits at u ^ tl_swtr(k) -- conflict-free for the 32 lanes of a transposed read (8 k-rows x 4 units)
+__device__ __forceinline__ int tl_swtr(int k) { return 4 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)); }
+
+// transposed fragment (inline asm: the builtin makes hipcc drain vmcnt -- the in-flight LDS-DMA -- before every read;
+// callers wait lgkmcnt(0) before the first use)
+__device__ __forceinline__ bf16x8 tl_frag_tr(const char* img, int rb, int kk, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  s16x8 out;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int k = kk * 32 + 8 * (lane >> 4) + 4 * t + q;
+    const unsigned a = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)(img + k * 128 +
+                                                                                         (((4 * rb + p) ^ tl_swtr(k)) << 3));
+    s16x4 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+    out[4 * t + 0] = v[0];
+    out[4 * t + 1] = v[1];
+    out[4 * t + 2] = v[2];
+    out[4 * t + 3] = v[3];
+  }
+  return __builtin_bit_cast(bf16x8, out);
+}
+
 template <int MI, int NI, int BKT, int NSTAGE, bool GEGLU>
 struct TallCfg {
   static constexpr int TR = 64 * MI;               // tile rows
@@ -80,9 +104,11 @@ struct TallCfg {
   static_assert((NSTAGE - 2) * NPW <= 24, "vmcnt immediates");
 };
 
-template <int MI, int NI, int BKT, int NSTAGE, bool GEGLU>
+// BKC = false: B k-strided [K][N] (nn.Linear dgrad dY . W), plain epilogues only (64-column image of 128-B k-rows)
+template <int MI, int NI, int BKT, int NSTAGE, bool GEGLU, bool BKC = true>
 __global__ void __launch_bounds__(512, 1) gemm_tall_kernel(GemmP p) {
   using C = TallCfg<MI, NI, BKT, NSTAGE, GEGLU>;
+  static_assert(BKC || (!GEGLU && C::TCB == 64), "k-strided B: 64-column plain tiles");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -106,6 +132,15 @@ __global__ void __launch_bounds__(512, 1) gemm_tall_kernel(GemmP p) {
     const int i = min(wave + 8 * s, C::NA + C::NB - 1);
     const bool isA = i < C::NA;
     const int j = isA ? i : i - C::NA;
+    dst[s] = (isA ? 0 : C::IMG_A) + j * 1024;
+    if (!BKC && !isA) {  // k-strided B: instruction j = k-rows 8j .. 8j + 7 of 128 B (8 columns per lane)
+      const int k = 8 * j + (lane >> 3);
+      const int lc = (lane & 7) ^ (tl_swtr(k) >> 1);
+      const int64_t c = min(n0 + 8 * lc, p.N - 8);
+      kl[s] = -1 - k;  // (marks a k-row source: the K tail clamps the row, not a chunk)
+      src[s] = p.B + (kbeg + k) * p.ldb + c;
+      continue;
+    }
     const int r = RPI * j + lane / CPR;                // image row
     const int ch = (lane % CPR) ^ tl_swz<BKT>(r);      // logical 16-B chunk this lane fetches
     kl[s] = 8 * ch;
@@ -119,15 +154,21 @@ __global__ void __launch_bounds__(512, 1) gemm_tall_kernel(GemmP p) {
       grow = min(n0 + r, p.N - 1);
     }
     src[s] = (isA ? p.A + grow * p.lda : p.B + grow * p.ldb) + kbeg + kl[s];
-    dst[s] = (isA ? 0 : C::IMG_A) + j * 1024;
   }
   auto issue = [&](int kt) {
     char* st = smem + (kt % NSTAGE) * C::STAGE;
     const bool last = kt == nk - 1 && krem < BKT;
 #pragma unroll
     for (int s = 0; s < C::NPW; ++s) {
-      const bf16_t* g = src[s] + (int64_t)kt * BKT;
-      if (last && kl[s] >= krem) g -= kl[s] - (krem - 8);  // past K: an in-bounds chunk (A side zeroed below)
+      const bf16_t* g;
+      if (!BKC && kl[s] < 0) {  // k-strided B row k: past K it re-reads the last valid k-row (A side zeroed)
+        const int k = -1 - kl[s];
+        g = src[s] + (int64_t)kt * BKT * p.ldb;
+        if (last && k >= krem) g -= (int64_t)(k - (krem - 1)) * p.ldb;
+      } else {
+        g = src[s] + (int64_t)kt * BKT;
+        if (last && kl[s] >= krem) g -= kl[s] - (krem - 8);  // past K: an in-bounds chunk (A side zeroed below)
+      }
       tl_glds16(g, st + dst[s]);
     }
   };
@@ -155,7 +196,11 @@ __global__ void __launch_bounds__(512, 1) gemm_tall_kernel(GemmP p) {
     for (int kk = 0; kk < BKT / 32; ++kk) {
       bf16x8 bf[NI];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) bf[j] = frag(ib, brow(j), kk);
+      for (int j = 0; j < NI; ++j) bf[j] = BKC ? frag(ib, brow(j), kk) : tl_frag_tr(ib, NI * wc + j, kk, lane);
+      if (!BKC) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         bf16x8 af = frag(ia, wr * MI + i, kk);
@@ -220,10 +265,10 @@ __global__ void __launch_bounds__(512, 1) gemm_tall_kernel(GemmP p) {
 
 }  // namespace
 
-template <int MI, int NI, int BKT, int NSTAGE, bool GEGLU>
+template <int MI, int NI, int BKT, int NSTAGE, bool GEGLU, bool BKC = true>
 static int launch_tall_k(const GemmP& p, int splits, hipStream_t st) {
   using C = TallCfg<MI, NI, BKT, NSTAGE, GEGLU>;
-  auto kern = gemm_tall_kernel<MI, NI, BKT, NSTAGE, GEGLU>;
+  auto kern = gemm_tall_kernel<MI, NI, BKT, NSTAGE, GEGLU, BKC>;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, C::SMEM);
@@ -237,7 +282,8 @@ static int launch_tall_k(const GemmP& p, int splits, hipStream_t st) {
 
 // plain: 64-column tiles, 64-deep K-tiles in a 3-slot ring; GeGLU: 64 output columns (128 B rows), 32-deep
 // K-tiles in a 4-slot ring.  mi = 4 (256-row tiles) or 5 (320-row tiles).
-int pz_tall_launch(const GemmP& p, int mi, bool geglu, int splits, hipStream_t st) {
+int pz_tall_launch(const GemmP& p, int mi, bool geglu, bool bkc, int splits, hipStream_t st) {
+  if (!bkc) return mi == 4 ? launch_tall_k<4, 2, 64, 3, false, false>(p, splits, st) : launch_tall_k<5, 2, 64, 3, false, false>(p, splits, st);
   if (geglu) return mi == 4 ? launch_tall_k<4, 4, 32, 4, true>(p, splits, st) : launch_tall_k<5, 4, 32, 4, true>(p, splits, st);
   return mi == 4 ? launch_tall_k<4, 2, 64, 3, false>(p, splits, st) : launch_tall_k<5, 2, 64, 3, false>(p, splits, st);
 }

@@ -965,3 +965,9 @@ def test_gemm_tall_forward_epilogues(M, N, K, geglu, monkeypatch):
     c = torch.ones(M, N, device=dev, dtype=torch.float32)
     ops.gemm(M, N, K, x, K, True, W, K, True, c, N, beta=True)
     close(c, 1.0 + ref, rtol=1e-3, atol=1e-3)
+    if N % 8 == 0:  # NN (dgrad layout: B k-strided [K][N], transposed LDS reads)
+        Wt = W.t().contiguous()
+        assert ops.gemm_kernel_name(M, N, K, b_kc=False).startswith("gemm_tall_kernel")
+        o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        ops.gemm(M, N, K, x, K, True, Wt, N, False, o, N, resid=r, ld_resid=N)
+        close(o, ref + r.float(), atol=2e-2)

@@ -60,6 +60,37 @@ def main():
             os.environ.pop("PZ_GEMM_TALL")
         d = (outs[0] - outs[1]).abs().max().item()
         print(f"{name:12s} {M}x{N}x{K}: " + " | ".join(res) + f" | max|d| {d:.3g}", flush=True)
+    main_nn(a.n)
+
+
+NN_SHAPES = [  # dgrad layout (B = W [K][N] k-strided): the action expert's 320 training rows
+    ("act dgate|up", 320, 1024, 8192), ("act ddown", 320, 4096, 1024), ("act do", 320, 2048, 1024),
+    ("act dqkv", 320, 1024, 2560),
+]
+
+
+def main_nn(n):
+    dev = "cuda"
+    for name, M, N, K in NN_SHAPES:
+        dy = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        W = (torch.randn(K, N, device=dev) * K ** -0.5).to(torch.bfloat16)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+        def run():
+            ops.gemm(M, N, K, dy, K, True, W, N, False, out, N)
+
+        res, outs = [], []
+        for label, env in [("default", {"PZ_GEMM_TALL": "0"}), ("tall", {"PZ_GEMM_TALL": "1"})]:
+            os.environ.update(env)
+            kn = ops.gemm_kernel_name(M, N, K, b_kc=False)
+            run()
+            torch.cuda.synchronize()
+            outs.append(out.float().clone())
+            t = graph_us(run, n)
+            res.append(f"{label} {t:7.2f} us ({2 * M * N * K / t / 1e6:5.0f} TF/s) [{kn}]")
+            os.environ.pop("PZ_GEMM_TALL")
+        d = (outs[0] - outs[1]).abs().max().item()
+        print(f"{name:12s} NN {M}x{N}x{K}: " + " | ".join(res) + f" | max|d| {d:.3g}", flush=True)
 
 
 if __name__ == "__main__":

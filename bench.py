@@ -67,9 +67,12 @@ def synthetic_batch(model, B, device, gen):
 
 def pmc_traffic(kname, shape):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (profiles/r03/pmc_dominant.json, tools/pmc_dominant.sh + tools/pmc_summary.py): FETCH_SIZE x2
-    (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another kernel/shape."""
-    path = os.path.join(ROOT, "profiles", "r03", "pmc_dominant.json")
+    (profiles/r04/pmc_dominant.json, else the round-3 file; tools/pmc_dominant.sh + tools/pmc_summary.py):
+    FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another
+    kernel/shape."""
+    path = os.path.join(ROOT, "profiles", "r04", "pmc_dominant.json")
+    if not os.path.exists(path):
+        path = os.path.join(ROOT, "profiles", "r03", "pmc_dominant.json")
     try:
         with open(path) as f:
             pm = json.load(f)
@@ -78,7 +81,7 @@ def pmc_traffic(kname, shape):
     if not kname.startswith(pm.get("kernel", "?")) or list(pm.get("shape_MNK", [])) != list(shape):
         return {"traffic": None}
     return {"traffic": pm["traffic_bytes"], "traffic_unit": "bytes/launch",
-            "traffic_algorithmic": pm["algorithmic_bytes"], "traffic_source": "profiles/r03/pmc_dominant.json"}
+            "traffic_algorithmic": pm["algorithmic_bytes"], "traffic_source": os.path.relpath(path, ROOT)}
 
 
 def cpu_baseline(seconds_budget=25.0):
@@ -271,7 +274,9 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=1024)
-    ap.add_argument("--micro-batch", type=int, default=64)
+    # 128: whole 256-tile rounds for the 35328-row vlm GEMMs and fewer per-micro-batch fixed costs -- measured
+    # 255.7 vs 248.0 samples/s for 64 x 16 on one box (profiles/r04/mb_ab.txt); 133 GB peak of the 288 GB
+    ap.add_argument("--micro-batch", type=int, default=128)
     ap.add_argument("--infer-iters", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")

@@ -1886,10 +1886,17 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 // tall-tile kernel (pz_gemm_tall.hip): 64 < M <= 1024 rows, k-contiguous A and B, batch 1, bf16 operands, forward
 // epilogues: one 256- or 320-row tile covers up to 320 rows (the B = 1 prefill's 276 rows in ONE row tile instead of
 // the 8-phase kernel's two 256-row tiles), 64 output columns per tile, K split over blockIdx.y until the grid
-// reaches ~256 workgroups.  PZ_GEMM_TALL=1: every eligible shape, 0: never (A/B runs; read per call)
+// reaches ~256 workgroups.  Taken by default where it measured faster (tools/tall_bench.py,
+// profiles/r04/tall_bench.log): <= 320 rows against the wide GeGLU gate|up (276 x 32768 x 2048: 57.9 -> 55.4 us) and
+// the long-K narrow projections (Gemma down 276 x 2048 x 16384: 49.8 -> 44.8 us, SigLIP fc2 256 x 1152 x 4304: 18.7
+// -> 18.1 us); slower on the short-K / narrow shapes the row-slab kernel takes and at 788 rows (the 8-phase kernel's
+// 256-row tiles are then mostly full).  PZ_GEMM_TALL=1: every eligible shape, 0: never (A/B runs; read per call)
 bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   const char* e = getenv("PZ_GEMM_TALL");
-  if (!(e && e[0] == '1')) return false;
+  if (e && e[0] == '0') return false;
+  if (!(e && e[0] == '1') &&
+      !(a->M <= 320 && pl.bkc && ((pl.geglu && ncols >= 8192) || (!pl.geglu && a->K >= 4300 && ncols <= 2048))))
+    return false;
   if (!pl.akc || (!pl.bkc && pl.geglu) || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
       a->M <= 64 || a->M > 1024 || a->K % 8 != 0)
     return false;

@@ -44,10 +44,12 @@ class GradReducer:
         self.final = dict(self.done)
         self.handles = []
 
-    def _launch(self, region, lo, hi):
+    def _launch(self, region, lo, hi, streams=()):
         g = self.arena.grad[lo:hi]
         if self.stream is None or dist.get_backend(self.group) != "nccl":
-            # gloo (CPU tests / single-GPU rehearsal): synchronous SUM then scale
+            # gloo (CPU tests / single-GPU rehearsal): synchronous SUM then scale, after the side streams' work
+            for s in streams:
+                torch.cuda.current_stream().wait_stream(s)
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
             g.mul_(1.0 / dist.get_world_size(self.group))
             self.log.append((False, hi - lo))
@@ -56,6 +58,8 @@ class GradReducer:
         ev.record()
         with torch.cuda.stream(self.stream):
             self.stream.wait_event(ev)
+            for s in streams:  # gradients of this slice also produced there (the engine's expert stream)
+                self.stream.wait_stream(s)
             if self.timing:
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -69,7 +73,7 @@ class GradReducer:
             g.record_stream(self.stream)
         self.log.append((True, hi - lo))
 
-    def notify(self, stage, layer):
+    def notify(self, stage, layer, streams=()):
         if not self.enabled:
             return
         ends = self.marks.get((stage, layer))
@@ -79,7 +83,7 @@ class GradReducer:
         for region, end in ends.items():
             self.final[region] = max(self.final[region], end)
             if (self.final[region] - self.done[region]) * elt >= self.bucket:
-                self._launch(region, self.done[region], self.final[region])
+                self._launch(region, self.done[region], self.final[region], streams)
                 self.done[region] = self.final[region]
 
     def finish(self):

@@ -976,9 +976,9 @@ class Engine:
                 with self._on(side, g):
                     self._qkv_backward(g, st["g"][g.name], f"{g.prefix}{l}.", dQ, dK, dV, dX, dXm, pos, B, L, Lp, beta,
                                        rpp, nh, hd, dev)
-            if side is not None and self.hook is not None:
-                main.wait_stream(side)  # DDP buckets are reduced from the main stream: the layer's expert grads first
-            self._notify("joint", l)
+            # the layer's expert gradients were produced on the side stream: the reducer's communication stream waits
+            # for both streams before it reads them (the compute streams keep running; no main <- side join per layer)
+            self._notify("joint", l, (side,) if side is not None else ())
         if side is not None:
             main.wait_stream(side)
             for t in dX.values():
@@ -1442,9 +1442,10 @@ class Engine:
         return action
 
     # --------------------------------------------------------------- hooks --
-    hook = None  # called as hook(stage, layer) when a layer's parameter gradients are final
+    hook = None  # called as hook(stage, layer, streams) when a layer's parameter gradients are final
     post_backward = None  # called once at the end of train_backward (gradient all-reduce flush)
 
-    def _notify(self, stage, layer):
+    def _notify(self, stage, layer, streams=()):
+        """streams: side streams (besides the current one) whose enqueued work produced some of those gradients"""
         if self.hook is not None:
-            self.hook(stage, layer)
+            self.hook(stage, layer, streams)

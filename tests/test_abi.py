@@ -57,6 +57,14 @@ def test_gemm_planner_routes_without_gpu():
     assert not ops.gemm_kernel_name(256, 4304, 1152).startswith("gemm_rows")  # SigLIP fc1
     assert not ops.gemm_kernel_name(256, 1152, 4304).startswith("gemm_rows")  # SigLIP fc2
     assert not ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_rows")
+    # tall-tile kernel where it measured faster: B = 1 Gemma gate|up / down, SigLIP fc2; not the action expert's
+    # 320-row down (K = 4096), not C5's 788 rows, not the training rows
+    assert ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_tall_kernel<5, 4")
+    assert ops.gemm_kernel_name(276, 2048, 16384).startswith("gemm_tall_kernel<5, 2")
+    assert ops.gemm_kernel_name(256, 1152, 4304).startswith("gemm_tall_kernel<4, 2")
+    assert not ops.gemm_kernel_name(320, 1024, 4096).startswith("gemm_tall")
+    assert not ops.gemm_kernel_name(789, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_tall")
+    assert not ops.gemm_kernel_name(35328, 2048, 16384).startswith("gemm_tall")
     assert not ops.gemm_kernel_name(64, 1024, 1024).startswith("gemm_rows")  # few-row paths keep M <= 64
     assert not ops.gemm_kernel_name(17664, 2560, 2048).startswith("gemm_rows")  # training rows: 8-phase
     assert not ops.gemm_kernel_name(320, 1024, 2048, a_kc=False).startswith("gemm_rows")  # k-strided A

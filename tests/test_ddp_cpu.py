@@ -48,7 +48,7 @@ def _worker(rank, world, port, q):
         order += [("vision", i) for i in reversed(range(vL))] + [("vision", -1)]
         launched = []
         orig = red._launch
-        red._launch = lambda region, lo, hi: (launched.append((region, lo, hi)), orig(region, lo, hi))
+        red._launch = lambda region, lo, hi, streams=(): (launched.append((region, lo, hi)), orig(region, lo, hi, streams))
         for st, l in order:
             red.notify(st, l)
         red.finish()

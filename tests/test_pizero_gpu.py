@@ -282,6 +282,22 @@ def test_microbatch64_batch_invariance(b16):
     _check_grads(g, m, "micro-batch 64")
 
 
+def test_microbatch128_batch_invariance(b16):
+    """The bench's default micro-batch 128 (gbsz 1024 = 128 x 8 on one GPU, 128 x 1 per rank on eight) = the 16
+    fixture samples x 8 in 8 different row orders, no sample at the same slot in two copies: same loss / gradients
+    as B = 16 (35328-row GEMMs: whole 256-tile rounds and tails of another shape than at 64)."""
+    from tests.pizero_gpu_helpers import dealias_orders
+
+    d, g, m = b16
+    orders = dealias_orders(16, 8)
+    assert all((orders[a] != orders[b]).all() for a in range(8) for b in range(a))
+    gi = gpu_inputs(m, d, 16, repeat=8)
+    assert gi["input_ids"].shape[0] == 128
+    loss = run_loss(m, gi)
+    _check_loss(g, loss.item())
+    _check_grads(g, m, "micro-batch 128")
+
+
 @pytest.mark.parametrize("which", ["tiny", "full"])
 def test_loss_and_grads_fused_joint_attention(which, request):
     """the fused (flash) joint attention path against the same fixtures"""

@@ -1924,6 +1924,16 @@ bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   return true;
 }
 
+// pz_gemm's column split (see there): a 256-tile bf16 plan with N % 256 == 128 (SigLIP's 1152-wide outputs) whose
+// first N - 128 columns fill whole rounds of the CUs.  PZ_GEMM_COLSPLIT=1 (A/B; read per call).  Measured slower at
+// micro-batch 64 (one round + a split tail: GEMM census 234.7 vs 229.6 ms, profiles/r03/colsplit_ab.txt)
+bool colsplit(const pz_gemm_args* a, const Plan& pl) {
+  const char* e = getenv("PZ_GEMM_COLSPLIT");
+  if (!(e && e[0] == '1')) return false;
+  return pl.kind == PATH_256 && use_8phase() && a->fp8_mode == 0 && !pl.geglu && a->batch == 1 &&
+         a->epilogue != PZ_EPI_DGEGLU && !a->norm_w && a->N % 256 == 128 && pl.tiles_m * (a->N / 256) >= device_cus();
+}
+
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
 Plan make_plan(const pz_gemm_args* a) {
   Plan pl{};
@@ -2074,6 +2084,18 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   static thread_local char buf[160];
   if (!a) return "";
   const Plan pl = make_plan(a);
+  if (colsplit(a, pl)) {  // "<first N - 128 columns> | <last 128 columns>"
+    pz_gemm_args a1 = *a, a2 = *a;
+    a1.N = a->N - 128;
+    a2.N = 128;
+    char first[160];
+    snprintf(first, sizeof(first), "%s", pz_gemm_kernel_name(&a1));
+    const char* second = pz_gemm_kernel_name(&a2);
+    char tmp[160];
+    snprintf(tmp, sizeof(tmp), "%s | %s", first, second);
+    snprintf(buf, sizeof(buf), "%s", tmp);
+    return buf;
+  }
   switch (pl.kind) {
     case PATH_SKINNY:
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
@@ -2320,6 +2342,25 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
 
   const Plan pl = make_plan(a);
   if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
+  // column split: a 256-tile GEMM whose last column tile would be half empty (N % 256 == 128: SigLIP's 1152-wide
+  // outputs) runs its first N - 128 columns as whole 256-wide tiles and the last 128 columns as a second GEMM on the
+  // planner's narrow path; every epilogue here is column-local (bias, residual, activation + aux, beta, fp32 C,
+  // activation backward)
+  if (colsplit(a, pl)) {
+    const int64_t n1 = a->N - 128;
+    pz_gemm_args a1 = *a;
+    a1.N = n1;
+    int rc = pz_gemm(&a1, stream);
+    if (rc != PZ_OK) return rc;
+    pz_gemm_args a2 = *a;
+    a2.N = 128;
+    a2.B = (const bf16_t*)a->B + (a->b_kcontig ? n1 * a->ldb : n1);
+    a2.C = a->c_fp32 ? (void*)((float*)a->C + n1) : (void*)((bf16_t*)a->C + n1);
+    if (a->bias) a2.bias = (const bf16_t*)a->bias + n1;
+    if (a->resid) a2.resid = (const bf16_t*)a->resid + n1;
+    if (a->aux) a2.aux = (bf16_t*)a->aux + n1;
+    return pz_gemm(&a2, stream);
+  }
   if (a->norm_w)
     PZ_CHECK_ARG((pl.kind == PATH_SKINNY || pl.kind == PATH_SKINNY64) && PZ_ALIGNED(a->norm_w, 16),
                  "pz_gemm: fused RMSNorm needs the few-row paths (M <= 64, k-contiguous A/B, K %% 32 == 0 "

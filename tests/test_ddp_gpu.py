@@ -70,9 +70,9 @@ def _worker(rank, world, port, q):
         orig_launch, orig_finish = w.reducer._launch, w.reducer.finish
         phase = {"flushing": False}
 
-        def launch(region, lo, hi):
+        def launch(region, lo, hi, streams=()):
             launched.append(phase["flushing"])
-            return orig_launch(region, lo, hi)
+            return orig_launch(region, lo, hi, streams)
 
         def finish():
             phase["flushing"] = True

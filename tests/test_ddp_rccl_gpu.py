@@ -63,10 +63,10 @@ def _worker(port, q):
         phase = {"flushing": False, "during": 0}
         orig_launch, orig_finish = red._launch, red.finish
 
-        def launch(region, lo, hi):
+        def launch(region, lo, hi, streams=()):
             if not phase["flushing"]:
                 phase["during"] += 1
-            return orig_launch(region, lo, hi)
+            return orig_launch(region, lo, hi, streams)
 
         def finish():
             phase["flushing"] = True

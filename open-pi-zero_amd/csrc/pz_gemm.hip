@@ -1829,7 +1829,11 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   // a leftover round at least half full runs about as fast as its K-pieces would (less contention);
   // after many rounds the workgroups no longer run in lockstep and the leftover tiles fill the gaps
   // (measured: split worse at q = 17, better at q <= 4)
-  if (r == 0 || (q > 0 && 2 * r >= G) || q > 8) return;
+  // PZ_TAIL_HALF=1 (A/B; read per call): also split a leftover round exactly half full (micro-batch 128's SigLIP
+  // 1152-wide GEMMs: 640 tiles = 2 rounds + 128)
+  const char* eh = getenv("PZ_TAIL_HALF");
+  const bool half = eh && eh[0] == '1';
+  if (r == 0 || (q > 0 && (half ? 2 * r > G : 2 * r >= G)) || q > 8) return;
   int64_t s = G / r;
   s = s < 16 ? s : 16;
   // no split below 8 K-tiles: a piece writes (and the merge re-reads) a 256 KiB fp32 partial, which a short

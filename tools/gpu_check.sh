@@ -86,7 +86,11 @@ PY
       PZ_GEMM_COLSPLIT=1 timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
         > "$OUT/ab_colsplit.log" 2>&1
       timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
-        > "$OUT/ab_nocolsplit.log" 2>&1 ;;
+        > "$OUT/ab_nocolsplit.log" 2>&1
+      PZ_TAIL_HALF=1 timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 \
+        > "$OUT/gemm_census_tailhalf.log" 2>&1
+      PZ_TAIL_HALF=1 timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
+        > "$OUT/ab_tailhalf.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "step $s ok"

@@ -1995,16 +1995,6 @@ Plan make_plan(const pz_gemm_args* a) {
         }
       }
     }
-    {  // PZ_SK64_NARROW=1 (A/B; read per call): narrow outputs take 4-column blocks (>= 256 workgroups, every block
-       // re-reads the activation rows from L2) instead of the K split + splitk_epilogue launch
-      const char* e = getenv("PZ_SK64_NARROW");
-      if (e && e[0] == '1' && pl.ksplit > 0) {
-        pl.ksplit = 0;
-        pl.splits = 0;
-        pl.ldw = 0;
-        pl.skinny_nc = 4;
-      }
-    }
     {  // A/B overrides (read per call): PZ_SK64_NC = 4|8|16 columns per block, PZ_SK64_W = 4|8 waves
       const char* e = getenv("PZ_SK64_NC");
       if (e && (atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) pl.skinny_nc = atoi(e);

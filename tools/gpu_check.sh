@@ -61,9 +61,6 @@ PY
         --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1
       timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
         > "$OUT/ab_mb64.log" 2>&1 ;;
-    c5ab)  # C5 chunk: default vs narrow 4-column skinny blocks without the K split (PZ_SK64_NARROW=1)
-      timeout -k 10 300 python -u tools/c5_bench.py --iters 50 > "$OUT/c5_default.log" 2>&1
-      PZ_SK64_NARROW=1 timeout -k 10 300 python -u tools/c5_bench.py --iters 50 > "$OUT/c5_narrow.log" 2>&1 ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels

@@ -768,19 +768,6 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
   const int g4 = 4 * (lane >> 4), rl = lane & 15;
   const int64_t nb = n0 + wc * 64 + g4;
   char* img = smem + (wc >> 1) * 65536;
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (FM == FM_BF16 && p.bias) unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias);
-#pragma unroll
-    for (int rb = 0; rb < 8; ++rb) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[r];
-      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
-    }
-  }
-  lds_sync();
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0;
   const bf16_t* X0 = nullptr;  // side input 0: aux (DACT: pre-activation, DGEGLU: g) or old C
   const bf16_t* X1 = nullptr;  // side input 1: resid or DGEGLU u
@@ -802,29 +789,58 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
       ld1 = p.ld_resid;
     }
   }
+  // side inputs in batches of CB chunks, issued one batch ahead of their use (the first right after the accumulators
+  // went to LDS, so its latency hides under the barrier; each later one under the previous batch's math) -- the
+  // DGEGLU epilogue reads 256 KiB of g|u per tile.  Batches touch disjoint chunks, so a side input aliasing C (old C
+  // with beta, DGEGLU in place) is always read before its chunk is stored.  2-chunk batches keep the two in-flight
+  // batches within the registers the 4-chunk batches took (no spill beside the 8-phase main loop).
+  constexpr int CB = 2, NBATCH = 16 / CB;
+  u32x4 s0[2][CB], s1[2][CB];
+  auto side = [&](int bt, u32x4 (&d0)[CB], u32x4 (&d1)[CB]) {
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int c = threadIdx.x + (bt * CB + i) * NT2;  // 0 .. 8191 over the two images
+      const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
+      const int col = im * 128 + ch * 8;
+      d0[i] = X0 ? *reinterpret_cast<const u32x4*>(X0 + row * ld0 + col) : u32x4{0u, 0u, 0u, 0u};
+      d1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (FM == FM_BF16 && p.bias) unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[r];
+      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+    }
+  }
+  side(0, s0[0], s1[0]);  // (the accumulators are in LDS: the registers they held are free)
+  lds_sync();
   const bool act = FM == FM_BF16 && (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU);
   const bool gelu = p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_DGELU;
 #pragma unroll
-  for (int half = 0; half < 4; ++half) {  // 4 batches of 4 chunks: a batch's loads issued together
-    u32x4 a0[4], a1[4], iv[4];
+  for (int bt = 0; bt < NBATCH; ++bt) {
+    if (bt + 1 < NBATCH) side(bt + 1, s0[(bt + 1) & 1], s1[(bt + 1) & 1]);
+    u32x4 iv[CB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = threadIdx.x + (half * 4 + i) * NT2;  // 0 .. 8191 over the two images
+    for (int i = 0; i < CB; ++i) {
+      const int c = threadIdx.x + (bt * CB + i) * NT2;
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
-      const int col = im * 128 + ch * 8;
       iv[i] = *reinterpret_cast<const u32x4*>(smem + im * 65536 + row * 256 + ((ch ^ (row & 15)) << 4));
-      a0[i] = X0 ? *reinterpret_cast<const u32x4*>(X0 + row * ld0 + col) : u32x4{0u, 0u, 0u, 0u};
-      a1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = threadIdx.x + (half * 4 + i) * NT2;
+    for (int i = 0; i < CB; ++i) {
+      const int c = threadIdx.x + (bt * CB + i) * NT2;
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
       const int col = im * 128 + ch * 8;
       float v[8], x0[8], x1[8];
       unpack8(iv[i], v);
-      unpack8(a0[i], x0);
-      unpack8(a1[i], x1);
+      unpack8(s0[bt & 1][i], x0);
+      unpack8(s1[bt & 1][i], x1);
       bf16_t* Cp = C + row * p.ldc + col;
       if (FM == FM_DGEGLU) {
         float dg[8], du[8];

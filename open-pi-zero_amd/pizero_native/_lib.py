@@ -11,6 +11,9 @@ import os
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
+# A/B runs only (tools/): another in-tree build of the same ABI, e.g. a baseline of a kernel change
+if os.environ.get("PZ_LIB_PATH"):
+    LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ["PZ_LIB_PATH"]))
 
 ABI_VERSION = 16  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3

@@ -61,6 +61,15 @@ PY
         --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1
       timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
         > "$OUT/ab_mb64.log" 2>&1 ;;
+    libab)  # baseline library (open-pi-zero_amd/libpizero_hip_base.so, same ABI) vs the in-tree one: GEMM census + bench
+      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 \
+        > "$OUT/census_base.log" 2>&1
+      timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 > "$OUT/census_new.log" 2>&1
+      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
+        --no-cpu-baseline > "$OUT/ab_base.log" 2>&1
+      timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_new.log" 2>&1
+      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
+        --no-cpu-baseline > "$OUT/ab_base2.log" 2>&1 ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels

@@ -952,6 +952,33 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
       }
       return;
     }
+    if (p.dbg == 5 && m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
+      // measurement (PZ_GEMM_DBG=5): h and g staged through the two LDS images, u stored straight from the
+      // accumulators (8 B per lane) in the same pass -- one image round instead of two
+#pragma unroll
+      for (int rb = 0; rb < 8; ++rb) {
+        const int64_t m = m0 + wr * 128 + rb * 16 + rl;
+        bf16_t* Ur = p.aux + m * p.ld_aux + p.geglu_I + n0 + wc * 32 + g4;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          float gg[4], hh[4], uu[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            gg[r] = acc[rb][j][r] * p.alpha;
+            uu[r] = acc[rb][2 + j][r] * p.alpha;
+            hh[r] = gelu_tanh(gg[r]) * uu[r];
+          }
+          const int row = wr * 128 + rb * 16 + rl, col = wc * 32 + j * 16 + g4;
+          img_put(smem, row, col, u32x2{pack2bf(hh[0], hh[1]), pack2bf(hh[2], hh[3])});
+          img_put(smem + 65536, row, col, u32x2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])});
+          *reinterpret_cast<u32x2*>(Ur + j * 16) = pk4(uu);
+        }
+      }
+      lds_sync();
+      img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc, p.nt_store);
+      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_aux);
+      return;
+    }
     if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
       // pass 1: h (smem) -> C and g (smem + 64 KiB) -> aux[:, :I]; pass 2: u (smem) -> aux[:, I:]
 #pragma unroll
@@ -1055,7 +1082,7 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL, bool F8>
 __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (p.dbg >= 2 && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
+  if ((p.dbg == 2 || p.dbg == 3) && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
     const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
     for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
   }
@@ -1364,7 +1391,7 @@ __device__ __forceinline__ bf16x8 kh_frag(const char* opbase, int h, int rb, int
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (p.dbg >= 2 && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
+  if ((p.dbg == 2 || p.dbg == 3) && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
     const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
     for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
   }
@@ -1845,11 +1872,9 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   // a leftover round at least half full runs about as fast as its K-pieces would (less contention);
   // after many rounds the workgroups no longer run in lockstep and the leftover tiles fill the gaps
   // (measured: split worse at q = 17, better at q <= 4)
-  // PZ_TAIL_HALF=1 (A/B; read per call): also split a leftover round exactly half full (micro-batch 128's SigLIP
-  // 1152-wide GEMMs: 640 tiles = 2 rounds + 128)
-  const char* eh = getenv("PZ_TAIL_HALF");
-  const bool half = eh && eh[0] == '1';
-  if (r == 0 || (q > 0 && (half ? 2 * r > G : 2 * r >= G)) || q > 8) return;
+  // (splitting a leftover round exactly half full -- micro-batch 128's SigLIP 1152-wide GEMMs, 640 tiles = 2 rounds +
+  // 128 -- measured within noise: profiles/r04/siglip_1152_ab.txt)
+  if (r == 0 || (q > 0 && 2 * r >= G) || q > 8) return;
   int64_t s = G / r;
   s = s < 16 ? s : 16;
   // no split below 8 K-tiles: a piece writes (and the merge re-reads) a 256 KiB fp32 partial, which a short
@@ -1907,15 +1932,17 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 // epilogues: one 256- or 320-row tile covers up to 320 rows (the B = 1 prefill's 276 rows in ONE row tile instead of
 // the 8-phase kernel's two 256-row tiles), 64 output columns per tile, K split over blockIdx.y until the grid
 // reaches ~256 workgroups.  Taken by default where it measured faster (tools/tall_bench.py,
-// profiles/r04/tall_bench.log): <= 320 rows against the wide GeGLU gate|up (276 x 32768 x 2048: 57.9 -> 55.4 us) and
-// the long-K narrow projections (Gemma down 276 x 2048 x 16384: 49.8 -> 44.8 us, SigLIP fc2 256 x 1152 x 4304: 18.7
-// -> 18.1 us); slower on the short-K / narrow shapes the row-slab kernel takes and at 788 rows (the 8-phase kernel's
-// 256-row tiles are then mostly full).  PZ_GEMM_TALL=1: every eligible shape, 0: never (A/B runs; read per call)
+// profiles/r04/tall_bench.log, and inside the B = 1 chunk, profiles/r04/infer_trace_split.txt): <= 320 rows against
+// the long-K narrow projections (Gemma down 276 x 2048 x 16384: 49.8 -> 44.8 us isolated, 54.5 -> 44.0 us in the
+// chunk incl. the merge; SigLIP fc2 256 x 1152 x 4304: 18.7 -> 18.1 us).  Not the B = 1 GeGLU gate|up: 55.4 vs
+// 57.9 us isolated (weights L2/MALL-warm over the repeats) but 65.2 vs 60.7 us in the chunk, where they stream
+// cold from HBM; slower on the short-K / narrow shapes the row-slab kernel takes and at 788 rows (the 8-phase
+// kernel's 256-row tiles are then mostly full).  PZ_GEMM_TALL=1: every eligible shape, 0: never (A/B runs)
 bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   const char* e = getenv("PZ_GEMM_TALL");
   if (e && e[0] == '0') return false;
   if (!(e && e[0] == '1') &&
-      !(a->M <= 320 && pl.bkc && ((pl.geglu && ncols >= 8192) || (!pl.geglu && a->K >= 4300 && ncols <= 2048))))
+      !(a->M <= 320 && pl.bkc && !pl.geglu && a->K >= 4300 && ncols <= 2048))
     return false;
   if (!pl.akc || (!pl.bkc && pl.geglu) || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
       a->M <= 64 || a->M > 1024 || a->K % 8 != 0)
@@ -1942,16 +1969,6 @@ bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   }
   pl.kind = PATH_TALL;
   return true;
-}
-
-// pz_gemm's column split (see there): a 256-tile bf16 plan with N % 256 == 128 (SigLIP's 1152-wide outputs) whose
-// first N - 128 columns fill whole rounds of the CUs.  PZ_GEMM_COLSPLIT=1 (A/B; read per call).  Measured slower at
-// micro-batch 64 (one round + a split tail: GEMM census 234.7 vs 229.6 ms, profiles/r03/colsplit_ab.txt)
-bool colsplit(const pz_gemm_args* a, const Plan& pl) {
-  const char* e = getenv("PZ_GEMM_COLSPLIT");
-  if (!(e && e[0] == '1')) return false;
-  return pl.kind == PATH_256 && use_8phase() && a->fp8_mode == 0 && !pl.geglu && a->batch == 1 &&
-         a->epilogue != PZ_EPI_DGEGLU && !a->norm_w && a->N % 256 == 128 && pl.tiles_m * (a->N / 256) >= device_cus();
 }
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
@@ -2104,18 +2121,6 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   static thread_local char buf[160];
   if (!a) return "";
   const Plan pl = make_plan(a);
-  if (colsplit(a, pl)) {  // "<first N - 128 columns> | <last 128 columns>"
-    pz_gemm_args a1 = *a, a2 = *a;
-    a1.N = a->N - 128;
-    a2.N = 128;
-    char first[160];
-    snprintf(first, sizeof(first), "%s", pz_gemm_kernel_name(&a1));
-    const char* second = pz_gemm_kernel_name(&a2);
-    char tmp[160];
-    snprintf(tmp, sizeof(tmp), "%s | %s", first, second);
-    snprintf(buf, sizeof(buf), "%s", tmp);
-    return buf;
-  }
   switch (pl.kind) {
     case PATH_SKINNY:
       snprintf(buf, sizeof(buf), "gemm_skinny_kernel<%d, %d>", pl.skinny_w, pl.skinny_nc);
@@ -2362,25 +2367,6 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
 
   const Plan pl = make_plan(a);
   if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
-  // column split: a 256-tile GEMM whose last column tile would be half empty (N % 256 == 128: SigLIP's 1152-wide
-  // outputs) runs its first N - 128 columns as whole 256-wide tiles and the last 128 columns as a second GEMM on the
-  // planner's narrow path; every epilogue here is column-local (bias, residual, activation + aux, beta, fp32 C,
-  // activation backward)
-  if (colsplit(a, pl)) {
-    const int64_t n1 = a->N - 128;
-    pz_gemm_args a1 = *a;
-    a1.N = n1;
-    int rc = pz_gemm(&a1, stream);
-    if (rc != PZ_OK) return rc;
-    pz_gemm_args a2 = *a;
-    a2.N = 128;
-    a2.B = (const bf16_t*)a->B + (a->b_kcontig ? n1 * a->ldb : n1);
-    a2.C = a->c_fp32 ? (void*)((float*)a->C + n1) : (void*)((bf16_t*)a->C + n1);
-    if (a->bias) a2.bias = (const bf16_t*)a->bias + n1;
-    if (a->resid) a2.resid = (const bf16_t*)a->resid + n1;
-    if (a->aux) a2.aux = (bf16_t*)a->aux + n1;
-    return pz_gemm(&a2, stream);
-  }
   if (a->norm_w)
     PZ_CHECK_ARG((pl.kind == PATH_SKINNY || pl.kind == PATH_SKINNY64) && PZ_ALIGNED(a->norm_w, 16),
                  "pz_gemm: fused RMSNorm needs the few-row paths (M <= 64, k-contiguous A/B, K %% 32 == 0 "

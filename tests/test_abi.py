@@ -57,9 +57,9 @@ def test_gemm_planner_routes_without_gpu():
     assert not ops.gemm_kernel_name(256, 4304, 1152).startswith("gemm_rows")  # SigLIP fc1
     assert not ops.gemm_kernel_name(256, 1152, 4304).startswith("gemm_rows")  # SigLIP fc2
     assert not ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_rows")
-    # tall-tile kernel where it measured faster: B = 1 Gemma gate|up / down, SigLIP fc2; not the action expert's
-    # 320-row down (K = 4096), not C5's 788 rows, not the training rows
-    assert ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm_tall_kernel<5, 4")
+    # tall-tile kernel where it measured faster: B = 1 Gemma down, SigLIP fc2; not the B = 1 gate|up (slower inside
+    # the chunk), not the action expert's 320-row down (K = 4096), not C5's 788 rows, not the training rows
+    assert ops.gemm_kernel_name(276, 32768, 2048, epi=geglu, geglu_inter=16384).startswith("gemm8p_kernel")
     assert ops.gemm_kernel_name(276, 2048, 16384).startswith("gemm_tall_kernel<5, 2")
     assert ops.gemm_kernel_name(256, 1152, 4304).startswith("gemm_tall_kernel<4, 2")
     assert not ops.gemm_kernel_name(320, 1024, 4096).startswith("gemm_tall")

@@ -89,17 +89,6 @@ PY
       bash tools/pmc_dominant.sh "$OUT/pmc" ;;
     census)
       timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-128} > "$OUT/gemm_census.log" 2>&1 ;;
-    colsplitab)  # column split of the 1152-wide SigLIP GEMMs at the default micro-batch: census + bench
-      PZ_GEMM_COLSPLIT=1 timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 \
-        > "$OUT/gemm_census_colsplit.log" 2>&1
-      PZ_GEMM_COLSPLIT=1 timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
-        > "$OUT/ab_colsplit.log" 2>&1
-      timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
-        > "$OUT/ab_nocolsplit.log" 2>&1
-      PZ_TAIL_HALF=1 timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 \
-        > "$OUT/gemm_census_tailhalf.log" 2>&1
-      PZ_TAIL_HALF=1 timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline \
-        > "$OUT/ab_tailhalf.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "step $s ok"

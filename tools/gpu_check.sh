@@ -70,6 +70,8 @@ PY
       timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_new.log" 2>&1
       PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
         --no-cpu-baseline > "$OUT/ab_base2.log" 2>&1 ;;
+    gegluab)
+      timeout -k 10 300 python -u tools/geglu_epi_ab.py > "$OUT/geglu_epi_ab.log" 2>&1 ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels

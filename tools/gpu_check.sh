@@ -70,6 +70,14 @@ PY
       timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_new.log" 2>&1
       PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
         --no-cpu-baseline > "$OUT/ab_base2.log" 2>&1 ;;
+    mb256)  # micro-batch 256 x 4 (peak HBM ~250 GB of 288) against the default 128 x 8, same box
+      set +e  # an out-of-memory exception (exit 1) is a result here; a timeout / crash still ends the script
+      timeout -k 10 500 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline --micro-batch 256 \
+        > "$OUT/ab_mb256.log" 2>&1
+      rc=$?
+      set -e
+      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+      timeout -k 10 500 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_mb128.log" 2>&1 ;;
     gegluab)
       timeout -k 10 300 python -u tools/geglu_epi_ab.py > "$OUT/geglu_epi_ab.log" 2>&1 ;;
     tallbench)

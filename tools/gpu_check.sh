@@ -82,6 +82,8 @@ PY
       timeout -k 10 300 python -u tools/geglu_epi_ab.py > "$OUT/geglu_epi_ab.log" 2>&1 ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
+    ldpad)  # SigLIP 4304-wide operands: natural 8608-B row pitch vs padded to 4352 elements
+      timeout -k 10 300 python -u tools/ld_pad_ab.py > "$OUT/ld_pad_ab.log" 2>&1 ;;
     gaps)  # GPU idle time inside the training step (plain run, no inference legs): the last ~2 steps' kernels
       timeout -k 10 600 rocprofv3 --kernel-trace --output-format csv -d "$OUT/gaps" -o gaps \
         -- python3 bench.py --steps 2 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/gaps.log" 2>&1

@@ -274,9 +274,11 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=1024)
-    # 128: whole 256-tile rounds for the 35328-row vlm GEMMs and fewer per-micro-batch fixed costs -- measured
-    # 255.7 vs 248.0 samples/s for 64 x 16 on one box (profiles/r04/mb_ab.txt); 133 GB peak of the 288 GB
-    ap.add_argument("--micro-batch", type=int, default=128)
+    # 256 x 4 on one GPU: every per-micro-batch fixed cost (launch tails, norm / reduction passes, the loss, the
+    # expert stream's join) paid 4 instead of 8 times and the 70656-row vlm GEMMs in whole 256-tile rounds --
+    # measured 260.5 vs 252.5 samples/s for 128 x 8 on one box (profiles/r04/mb256_ab.txt; 247 GB peak of the
+    # 288 GB), 128 x 8 255.7 vs 64 x 16 248.0 (profiles/r04/mb_ab.txt).  At 8 GPUs each rank runs 128 x 1.
+    ap.add_argument("--micro-batch", type=int, default=256)
     ap.add_argument("--infer-iters", type=int, default=100)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-infer", action="store_true")
@@ -401,6 +403,8 @@ def main():
 
     infer = None
     if not args.no_infer and rank == 0:
+        batches = None
+        torch.cuda.empty_cache()  # the training step's activation blocks (micro-batch 256: ~240 GB) go back
         model.eval()
         gi = synthetic_batch(model, 1, dev, torch.Generator().manual_seed(7))
         itp, amask = model.split_full_mask_into_submasks(gi["causal_mask"])

@@ -768,6 +768,19 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
   const int g4 = 4 * (lane >> 4), rl = lane & 15;
   const int64_t nb = n0 + wc * 64 + g4;
   char* img = smem + (wc >> 1) * 65536;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (FM == FM_BF16 && p.bias) unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias);
+#pragma unroll
+    for (int rb = 0; rb < 8; ++rb) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[r];
+      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
+    }
+  }
+  lds_sync();
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0;
   const bf16_t* X0 = nullptr;  // side input 0: aux (DACT: pre-activation, DGEGLU: g) or old C
   const bf16_t* X1 = nullptr;  // side input 1: resid or DGEGLU u
@@ -789,58 +802,29 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
       ld1 = p.ld_resid;
     }
   }
-  // side inputs in batches of CB chunks, issued one batch ahead of their use (the first right after the accumulators
-  // went to LDS, so its latency hides under the barrier; each later one under the previous batch's math) -- the
-  // DGEGLU epilogue reads 256 KiB of g|u per tile.  Batches touch disjoint chunks, so a side input aliasing C (old C
-  // with beta, DGEGLU in place) is always read before its chunk is stored.  2-chunk batches keep the two in-flight
-  // batches within the registers the 4-chunk batches took (no spill beside the 8-phase main loop).
-  constexpr int CB = 2, NBATCH = 16 / CB;
-  u32x4 s0[2][CB], s1[2][CB];
-  auto side = [&](int bt, u32x4 (&d0)[CB], u32x4 (&d1)[CB]) {
-#pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = threadIdx.x + (bt * CB + i) * NT2;  // 0 .. 8191 over the two images
-      const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
-      const int col = im * 128 + ch * 8;
-      d0[i] = X0 ? *reinterpret_cast<const u32x4*>(X0 + row * ld0 + col) : u32x4{0u, 0u, 0u, 0u};
-      d1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    float bias[4] = {0.f, 0.f, 0.f, 0.f};
-    if (FM == FM_BF16 && p.bias) unpack4(*reinterpret_cast<const u32x2*>(p.bias + nb + cb * 16), bias);
-#pragma unroll
-    for (int rb = 0; rb < 8; ++rb) {
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][r] * p.alpha + bias[r];
-      img_put(img, wr * 128 + rb * 16 + rl, (wc & 1) * 64 + cb * 16 + g4, u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])});
-    }
-  }
-  side(0, s0[0], s1[0]);  // (the accumulators are in LDS: the registers they held are free)
-  lds_sync();
   const bool act = FM == FM_BF16 && (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU);
   const bool gelu = p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_DGELU;
 #pragma unroll
-  for (int bt = 0; bt < NBATCH; ++bt) {
-    if (bt + 1 < NBATCH) side(bt + 1, s0[(bt + 1) & 1], s1[(bt + 1) & 1]);
-    u32x4 iv[CB];
+  for (int half = 0; half < 4; ++half) {  // 4 batches of 4 chunks: a batch's loads issued together
+    u32x4 a0[4], a1[4], iv[4];
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = threadIdx.x + (bt * CB + i) * NT2;
+    for (int i = 0; i < 4; ++i) {
+      const int c = threadIdx.x + (half * 4 + i) * NT2;  // 0 .. 8191 over the two images
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
+      const int col = im * 128 + ch * 8;
       iv[i] = *reinterpret_cast<const u32x4*>(smem + im * 65536 + row * 256 + ((ch ^ (row & 15)) << 4));
+      a0[i] = X0 ? *reinterpret_cast<const u32x4*>(X0 + row * ld0 + col) : u32x4{0u, 0u, 0u, 0u};
+      a1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int c = threadIdx.x + (bt * CB + i) * NT2;
+    for (int i = 0; i < 4; ++i) {
+      const int c = threadIdx.x + (half * 4 + i) * NT2;
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
       const int col = im * 128 + ch * 8;
       float v[8], x0[8], x1[8];
       unpack8(iv[i], v);
-      unpack8(s0[bt & 1][i], x0);
-      unpack8(s1[bt & 1][i], x1);
+      unpack8(a0[i], x0);
+      unpack8(a1[i], x1);
       bf16_t* Cp = C + row * p.ldc + col;
       if (FM == FM_DGEGLU) {
         float dg[8], du[8];
@@ -930,31 +914,11 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
   }
   const int g4 = 4 * (lane >> 4), rl = lane & 15;
   if (GEGLU) {
-    if (p.dbg == 4 && m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {  // measurement: direct 8-B stores
-#pragma unroll
-      for (int rb = 0; rb < 8; ++rb) {
-        const int64_t m = m0 + wr * 128 + rb * 16 + rl;
-        bf16_t* Cr = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n0 + wc * 32 + g4;
-        bf16_t* Xr = p.aux + m * p.ld_aux + n0 + wc * 32 + g4;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float gg[4], uu[4], hh[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            gg[r] = acc[rb][j][r] * p.alpha;
-            uu[r] = acc[rb][2 + j][r] * p.alpha;
-            hh[r] = gelu_tanh(gg[r]) * uu[r];
-          }
-          *reinterpret_cast<u32x2*>(Cr + j * 16) = pk4(hh);
-          *reinterpret_cast<u32x2*>(Xr + j * 16) = pk4(gg);
-          *reinterpret_cast<u32x2*>(Xr + p.geglu_I + j * 16) = pk4(uu);
-        }
-      }
-      return;
-    }
-    if (p.dbg == 5 && m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
-      // measurement (PZ_GEMM_DBG=5): h and g staged through the two LDS images, u stored straight from the
-      // accumulators (8 B per lane) in the same pass -- one image round instead of two
+    if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
+      // h and g staged through the two 64 KiB LDS images (16-B row stores), u stored straight from the
+      // accumulators (8 B per lane) in the same pass: one image round instead of two (u needs no LDS round
+      // trip of its own; 4.03 vs 4.08-4.24 ms at 35328 x 32768 x 2048, bitwise equal,
+      // profiles/r04/geglu_epi_ab.log; all three through direct 8-B stores measured 4.64 ms)
 #pragma unroll
       for (int rb = 0; rb < 8; ++rb) {
         const int64_t m = m0 + wr * 128 + rb * 16 + rl;
@@ -977,40 +941,6 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
       lds_sync();
       img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc, p.nt_store);
       img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_aux);
-      return;
-    }
-    if (m0 + BT <= p.M && n0 + BT / 2 <= p.geglu_I && p.aux) {
-      // pass 1: h (smem) -> C and g (smem + 64 KiB) -> aux[:, :I]; pass 2: u (smem) -> aux[:, I:]
-#pragma unroll
-      for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float gg[4], hh[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            gg[r] = acc[rb][j][r] * p.alpha;
-            hh[r] = gelu_tanh(gg[r]) * (acc[rb][2 + j][r] * p.alpha);
-          }
-          const int row = wr * 128 + rb * 16 + rl, col = wc * 32 + j * 16 + g4;
-          img_put(smem, row, col, u32x2{pack2bf(hh[0], hh[1]), pack2bf(hh[2], hh[3])});
-          img_put(smem + 65536, row, col, u32x2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])});
-        }
-      lds_sync();
-      img_flush(smem, reinterpret_cast<bf16_t*>(p.C) + cofs + m0 * p.ldc + n0, p.ldc, p.nt_store);
-      img_flush(smem + 65536, p.aux + m0 * p.ld_aux + n0, p.ld_aux, p.nt_aux);
-      lds_sync();
-#pragma unroll
-      for (int rb = 0; rb < 8; ++rb)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          float uu[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) uu[r] = acc[rb][2 + j][r] * p.alpha;
-          img_put(smem, wr * 128 + rb * 16 + rl, wc * 32 + j * 16 + g4,
-                  u32x2{pack2bf(uu[0], uu[1]), pack2bf(uu[2], uu[3])});
-        }
-      lds_sync();
-      img_flush(smem, p.aux + m0 * p.ld_aux + p.geglu_I + n0, p.ld_aux, p.nt_aux);
       return;
     }
 #pragma unroll
@@ -1082,10 +1012,6 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL, bool F8>
 __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((p.dbg == 2 || p.dbg == 3) && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
-    const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {  // split tail: one K-piece of a leftover tile
@@ -1391,10 +1317,6 @@ __device__ __forceinline__ bf16x8 kh_frag(const char* opbase, int h, int rb, int
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if ((p.dbg == 2 || p.dbg == 3) && blockIdx.x < 256 && blockIdx.y == 0) {  // measurement: desynchronise the first round
-    const int n = ((blockIdx.x >> 3) & 7) * (p.dbg - 1);
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {

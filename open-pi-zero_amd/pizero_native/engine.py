@@ -208,6 +208,12 @@ class Engine:
         # 239.3 samples/s), and its expert GEMMs then share the CUs with the vlm GeGLU GEMM (the dominant
         # kernel: live roofline 2.32 vs 2.19 ms per launch), so off by default
         self.expert_stream_fwd = os.environ.get("PZ_EXPERT_STREAM_FWD", "0") == "1"
+        # row pitch of SigLIP's MLP activations (fc1 output / pre-activation / their gradient, 4304 wide): rounded up
+        # to 64 elements, so every row starts on a 128-B line (8704 B instead of 8608 B).  The GEMMs that stream
+        # these rows run 2-8 % faster with bitwise-equal results (profiles/r04/ld_pad_ab.txt); the pad columns are
+        # never read (K tails clamp their sources into the row).  PZ_SIG_PITCH=0: natural pitch (A/B)
+        vI = self.d.vI
+        self.sig_pitch = vI if os.environ.get("PZ_SIG_PITCH", "1") == "0" else (vI + 63) // 64 * 64
         self._side = {}
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
@@ -381,6 +387,10 @@ class Engine:
         return stack
 
     # ================================================================ SigLIP ==
+    def _sig_rows(self, M, dev):
+        """[M, vI] bf16 rows at the SigLIP MLP row pitch (a view of [M, sig_pitch])"""
+        return torch.empty(M, self.sig_pitch, device=dev, dtype=BF16)[:, : self.d.vI]
+
     def siglip_forward(self, pix, save):
         """siglip.py:34-300 + projector (siglip.py:9-31). pix bf16 [B,3,H,W] or [B,n_images,3,H,W] ->
         img [B*n_img, proj] (a sample's images' tokens consecutive, in image order)."""
@@ -436,8 +446,8 @@ class Engine:
             mu2 = torch.empty(M, device=dev, dtype=F32)
             r2 = torch.empty(M, device=dev, dtype=F32)
             ops.layernorm(xm, self.w(p + "layer_norm2.weight"), self.w(p + "layer_norm2.bias"), h2, mu2, r2, d.ln_eps)
-            a1 = torch.empty(M, d.vI, device=dev, dtype=BF16) if save is not None else None
-            g1 = torch.empty(M, d.vI, device=dev, dtype=BF16)
+            a1 = self._sig_rows(M, dev) if save is not None else None
+            g1 = self._sig_rows(M, dev)
             L(h2, "mlp.fc1.weight", self.w(p + "mlp.fc1.weight"), g1, bias=self.w(p + "mlp.fc1.bias"), epi=PZ_EPI_GELU,
               aux=a1)
             xn = torch.empty_like(x)
@@ -494,7 +504,7 @@ class Engine:
         nh, hd = d.vheads, d.vH // d.vheads
         Np = d.img_tok
         W3 = 3 * d.vH
-        dg = torch.empty(M, d.vI, device=dev, dtype=BF16)
+        dg = self._sig_rows(M, dev)
         delta = torch.empty(B * nh, Np, device=dev, dtype=F32)
         dqkv = torch.empty(M, W3, device=dev, dtype=BF16)
         dh = torch.empty(M, d.vH, device=dev, dtype=BF16)

@@ -282,20 +282,29 @@ def test_microbatch64_batch_invariance(b16):
     _check_grads(g, m, "micro-batch 64")
 
 
-def test_microbatch128_batch_invariance(b16):
-    """The bench's default micro-batch 128 (gbsz 1024 = 128 x 8 on one GPU, 128 x 1 per rank on eight) = the 16
-    fixture samples x 8 in 8 different row orders, no sample at the same slot in two copies: same loss / gradients
-    as B = 16 (35328-row GEMMs: whole 256-tile rounds and tails of another shape than at 64)."""
+@pytest.mark.parametrize("repeat", [8, 16])
+def test_microbatch_batch_invariance(b16, repeat):
+    """The bench's micro-batches (gbsz 1024 = 256 x 4 on one GPU, 128 x 1 per rank on eight) = the 16 fixture
+    samples x ``repeat`` in different row orders, no sample at the same slot in two copies: same loss / gradients
+    as B = 16 (35328- / 70656-row GEMMs: whole 256-tile rounds and tails of another shape than at 64)."""
     from tests.pizero_gpu_helpers import dealias_orders
 
     d, g, m = b16
-    orders = dealias_orders(16, 8)
-    assert all((orders[a] != orders[b]).all() for a in range(8) for b in range(a))
-    gi = gpu_inputs(m, d, 16, repeat=8)
-    assert gi["input_ids"].shape[0] == 128
+    orders = dealias_orders(16, repeat)
+    assert all((orders[a] != orders[b]).all() for a in range(repeat) for b in range(a))
+    if repeat > 8:  # micro-batch 256 needs ~240 GB of activations
+        torch.cuda.empty_cache()
+        free, _ = torch.cuda.mem_get_info()
+        if free < 250e9:
+            pytest.skip(f"micro-batch {16 * repeat} needs ~250 GB free, {free / 1e9:.0f} GB free")
+    gi = gpu_inputs(m, d, 16, repeat=repeat)
+    assert gi["input_ids"].shape[0] == 16 * repeat
     loss = run_loss(m, gi)
     _check_loss(g, loss.item())
-    _check_grads(g, m, "micro-batch 128")
+    _check_grads(g, m, f"micro-batch {16 * repeat}")
+    del gi, loss
+    m.zero_grad(set_to_none=True)
+    torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("which", ["tiny", "full"])

@@ -56,30 +56,11 @@ PY
       for f in "$OUT"/ddpprof/*kernel_trace.csv "$OUT"/ddpprof/*/*kernel_trace.csv; do
         if [ -f "$f" ]; then python3 tools/trace_gaps.py "$f" > "${f%kernel_trace.csv}gaps.txt" 2>&1; rm -f "$f"; fi
       done ;;
-    mbab)  # micro-batch 128 x accumulation 8 against the default 64 x 16 (same box)
-      timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
-        --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1
-      timeout -k 10 400 python -u bench.py --steps ${AB_STEPS:-5} --warmup 1 --no-infer --no-cpu-baseline \
-        > "$OUT/ab_mb64.log" 2>&1 ;;
-    libab)  # baseline library (open-pi-zero_amd/libpizero_hip_base.so, same ABI) vs the in-tree one: GEMM census + bench
-      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 \
-        > "$OUT/census_base.log" 2>&1
-      timeout -k 10 300 python -u tools/gemm_census.py --micro-batch 128 > "$OUT/census_new.log" 2>&1
-      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
-        --no-cpu-baseline > "$OUT/ab_base.log" 2>&1
-      timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_new.log" 2>&1
-      PZ_LIB_PATH=libpizero_hip_base.so timeout -k 10 500 python -u bench.py --steps 4 --warmup 1 --no-infer \
-        --no-cpu-baseline > "$OUT/ab_base2.log" 2>&1 ;;
-    mb256)  # micro-batch 256 x 4 (peak HBM ~250 GB of 288) against the default 128 x 8, same box
-      set +e  # an out-of-memory exception (exit 1) is a result here; a timeout / crash still ends the script
-      timeout -k 10 500 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline --micro-batch 256 \
+    mbab)  # the default micro-batch (256 x 4) against 128 x 8, same box
+      timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-infer --no-cpu-baseline \
         > "$OUT/ab_mb256.log" 2>&1
-      rc=$?
-      set -e
-      if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-      timeout -k 10 500 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/ab_mb128.log" 2>&1 ;;
-    gegluab)
-      timeout -k 10 300 python -u tools/geglu_epi_ab.py > "$OUT/geglu_epi_ab.log" 2>&1 ;;
+      timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-infer --no-cpu-baseline \
+        --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1 ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     ldpad)  # SigLIP 4304-wide operands: natural 8608-B row pitch vs padded to 4352 elements
@@ -100,7 +81,7 @@ PY
     pmc)
       bash tools/pmc_dominant.sh "$OUT/pmc" ;;
     census)
-      timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-128} > "$OUT/gemm_census.log" 2>&1 ;;
+      timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-256} > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
   echo "step $s ok"

@@ -38,7 +38,7 @@ def mean(x):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    M, N, K = int(os.environ.get("PMC_M", "35328")), 32768, 2048
+    M, N, K = int(os.environ.get("PMC_M", "70656")), 32768, 2048
     kern = sys.argv[3] if len(sys.argv) > 3 else "gemm8p_kernel<true, true, true"
     name, fetch, d1 = per_dispatch(os.path.join(src, "fetch", "fetch_counter_collection.csv"), kern)
     _, write, d2 = per_dispatch(os.path.join(src, "write", "write_counter_collection.csv"), kern)

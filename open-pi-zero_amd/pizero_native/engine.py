@@ -1210,17 +1210,6 @@ class Engine:
         pos = {"vlm": vpos, "proprio": ppos}
         Q = torch.empty(B, L1, nh * hd, device=dev, dtype=BF16)
         S = Pm = None
-        # the proprio token's layers (few-row GEMV launches, latency-bound) on the second stream, concurrent with
-        # the vlm rows' GEMMs: the two groups meet only in each layer's joint attention (the side stream's q|k|v
-        # before it, its output after it).  PZ_EXPERT_STREAM=0: one stream
-        flash = self.infer_flash and not isinstance(cnt, GeneralMask)
-        side = self._side_stream(dev) if (self.expert_stream and flash and dev.type == "cuda" and
-                                          self.gemv_ok(B * d.C, d.aH)) else None
-        keep = []  # main-stream tensors the side stream reads: alive until the join below
-        if side is not None:
-            self.rope(groups[1].theta)  # (tables built before the fork)
-            keep.append(Xp)
-            side.wait_stream(torch.cuda.current_stream(dev))
         for l in range(d.nL):
             last = l == d.nL - 1
             Kj, Vj = kcache[l], vcache[l]
@@ -1230,13 +1219,12 @@ class Engine:
                 x = X[g.name]
                 M = x.shape[0]
                 if self.gemv_ok(M, x.shape[1]):  # few rows (the proprio token): one fused launch
-                    with self._on(side, g):
-                        if last:
-                            self._kv_only_gemv(x, p, pos[g.pos_key], g, Kj, Vj, L1, Lp)
-                        else:
-                            ops.gemv_qkv_rope(x, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, g.T,
-                                              nh, hd, L1, g.off, Lp, g.off,
-                                              norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+                    if last:
+                        self._kv_only_gemv(x, p, pos[g.pos_key], g, Kj, Vj, L1, Lp)
+                    else:
+                        ops.gemv_qkv_rope(x, self.qkv_w(p), pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, g.T, nh,
+                                          hd, L1, g.off, Lp, g.off,
+                                          norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
                     continue
                 h = torch.empty_like(x)
                 ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
@@ -1259,19 +1247,13 @@ class Engine:
                                    Lp, g.off)
             if last:
                 break
-            if flash:  # fused attention over the L1 prefix keys
+            if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over the L1 prefix keys
                 Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
-                if side is not None:
-                    torch.cuda.current_stream(dev).wait_stream(side)
                 ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, g.T, Os[g.name]) for g in groups], L1, L1, 0,
                                                      cnt, B))
-                if side is not None:
-                    side.wait_stream(torch.cuda.current_stream(dev))
-                    keep.append(Os["proprio"])
-                for g in sorted(groups, key=lambda g_: g_.name != "proprio"):  # the side stream's launches first
+                for g in groups:
                     p = f"{g.prefix}{l}."
-                    with self._on(side, g):
-                        X[g.name] = self._post_attn_O(g, p, X[g.name], Os[g.name])
+                    X[g.name] = self._post_attn_O(g, p, X[g.name], Os[g.name])
                 continue
             if S is None:
                 S = torch.empty(B, L1 * nh, Lp, device=dev, dtype=F32)
@@ -1284,9 +1266,6 @@ class Engine:
                 p = f"{g.prefix}{l}."
                 x = X[g.name]
                 X[g.name] = self._post_attn(g, p, x, Pm, Vj, B, L1, Lp)
-        if side is not None:
-            torch.cuda.current_stream(dev).wait_stream(side)
-            keep.clear()
         return kcache, vcache
 
     # ========================================================= text generation ==

@@ -61,16 +61,6 @@ PY
         > "$OUT/ab_mb256.log" 2>&1
       timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-infer --no-cpu-baseline \
         --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1 ;;
-    infab)  # prefill's proprio layers on the second stream (default) vs one stream: C4 and C5 graph ms, same box
-      for s in 0 1 0 1; do
-        PZ_EXPERT_STREAM=$s timeout -k 10 200 python -u tools/infer_bench.py --iters 100 > "$OUT/infab_$s.tmp" 2>&1
-        echo "PZ_EXPERT_STREAM=$s $(tail -1 "$OUT/infab_$s.tmp")" >> "$OUT/infab.log"
-      done
-      for s in 0 1; do
-        PZ_EXPERT_STREAM=$s timeout -k 10 300 python -u tools/c5_bench.py --iters 50 > "$OUT/infab_c5_$s.tmp" 2>&1
-        echo "PZ_EXPERT_STREAM=$s $(tail -1 "$OUT/infab_c5_$s.tmp" | cut -c1-160)" >> "$OUT/infab.log"
-      done
-      rm -f "$OUT"/infab_*.tmp ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     ldpad)  # SigLIP 4304-wide operands: natural 8608-B row pitch vs padded to 4352 elements

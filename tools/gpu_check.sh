@@ -61,6 +61,18 @@ PY
         > "$OUT/ab_mb256.log" 2>&1
       timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-infer --no-cpu-baseline \
         --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1 ;;
+    knobab)  # engine knobs at the default micro-batch, same box: one bench line each (--no-infer)
+      for kv in base PZ_SPLIT_DGEGLU=1 PZ_SPLIT_DACT=0 PZ_EXPERT_STREAM=0 PZ_JOINT_ATTN=gemm base; do
+        if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
+        env "${envs[@]}" timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline \
+          > "$OUT/knob.tmp" 2>&1
+        echo "$kv $(grep -o '"value": [0-9.]*' "$OUT/knob.tmp")" >> "$OUT/knobab.log"
+      done
+      rm -f "$OUT/knob.tmp" ;;
+    trainprof)  # kernel stats of the training step alone (1 warm-up + 1 timed step, no inference legs)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trainprof" -o train \
+        -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/trainprof.log" 2>&1
+      rm -f "$OUT"/trainprof/*kernel_trace.csv "$OUT"/trainprof/*/*kernel_trace.csv ;;
     tallbench)
       timeout -k 10 300 python -u tools/tall_bench.py > "$OUT/tall_bench.log" 2>&1 ;;
     ldpad)  # SigLIP 4304-wide operands: natural 8608-B row pitch vs padded to 4352 elements

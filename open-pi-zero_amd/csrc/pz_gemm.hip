@@ -1001,14 +1001,6 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
   }
 }
 
-// GemmP::ds_sleeps / ds_groups: stagger the first round of workgroups (see pz_gemm_epi.h)
-__device__ __forceinline__ void first_round_offset(const GemmP& p) {
-  if (p.ds_sleeps > 0 && blockIdx.x < 256 && blockIdx.y == 0) {
-    const int n = ((blockIdx.x >> 3) % p.ds_groups) * p.ds_sleeps;
-    for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-}
-
 // F8: fp8 (OCP e4m3) A and B, both k-contiguous, staged by the same byte-identical pipeline: the
 // caller passes K, lda, ldb in units of 2 codes ("bf16-sized" elements), so a 64-unit K-tile is 128
 // codes, and each (row block, column block) of a K-tile is ONE v_mfma_f32_16x16x128_f8f6f4 on the two
@@ -1020,7 +1012,6 @@ __device__ __forceinline__ void first_round_offset(const GemmP& p) {
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL, bool F8>
 __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  first_round_offset(p);
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {  // split tail: one K-piece of a leftover tile
@@ -1326,7 +1317,6 @@ __device__ __forceinline__ bf16x8 kh_frag(const char* opbase, int h, int rb, int
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  first_round_offset(p);
   const int nk_all = (int)((p.K + 63) / 64);
   int lid = blockIdx.x, piece = -1, kt0 = 0, nk = nk_all;
   if (p.tail_s && lid >= p.dp_tiles) {
@@ -2294,18 +2284,6 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
     p.nt_store = e ? atoi(e) : 0;
     e = getenv("PZ_GEMM_NT_AUX");
     p.nt_aux = p.nt_store || (e && atoi(e) != 0);
-    // PZ_GEMM_DESYNC="sleeps,groups[,all]": first-round phase offsets for the DGEGLU epilogue launches (all = every
-    // 8-phase launch); measurement knob
-    p.ds_sleeps = 0;
-    p.ds_groups = 1;
-    e = getenv("PZ_GEMM_DESYNC");
-    if (e && (a->epilogue == PZ_EPI_DGEGLU || strstr(e, "all"))) {
-      int s_ = 0, g_ = 1;
-      if (sscanf(e, "%d,%d", &s_, &g_) >= 1 && s_ > 0 && g_ > 0) {
-        p.ds_sleeps = s_;
-        p.ds_groups = g_;
-      }
-    }
   }
   hipStream_t st = (hipStream_t)stream;
 

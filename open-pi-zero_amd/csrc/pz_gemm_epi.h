@@ -48,10 +48,6 @@ struct GemmP {
   // ... and for the saved activations only (aux: GeGLU g|u, GELU / SiLU pre-activation -- read again only by the
   // backward, long after; PZ_GEMM_NT_AUX, read per call)
   int nt_aux;
-  // first-round phase offsets (8-phase kernels): the first 256 workgroups wait ((blockIdx >> 3) % ds_groups) x
-  // ds_sleeps x s_sleep(127) (~4.3 us each) before their main loop, so the CUs' epilogue bursts (the DGEGLU tile's
-  // 256 KiB of g|u read + 256 KiB written) fall at different times in the following rounds too; 0: off
-  int ds_sleeps, ds_groups;
 };
 
 namespace {

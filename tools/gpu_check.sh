@@ -69,8 +69,6 @@ PY
         echo "$kv $(grep -o '"value": [0-9.]*' "$OUT/knob.tmp")" >> "$OUT/knobab.log"
       done
       rm -f "$OUT/knob.tmp" ;;
-    desync)  # first-round phase offsets on the DGEGLU / GeGLU launches (PZ_GEMM_DESYNC)
-      timeout -k 10 300 python -u tools/desync_ab.py > "$OUT/desync_ab.log" 2>&1 ;;
     trainprof)  # kernel stats of the training step alone (1 warm-up + 1 timed step, no inference legs)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trainprof" -o train \
         -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/trainprof.log" 2>&1

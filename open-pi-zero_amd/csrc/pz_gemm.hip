@@ -1828,9 +1828,7 @@ bool plan_rows(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   if ((er && er[0] == '0') || a->M <= 64 || a->M > maxm || !pl.akc || !pl.bkc || a->batch != 1 ||
       a->epilogue >= PZ_EPI_DGELU || a->norm_w)
     return false;
-  const char* en = getenv("PZ_ROWS_MAXN");  // output-column limit (A/B runs; read per call)
-  const int64_t maxn = en ? atoll(en) : 4096;
-  if (!(er && er[0] == '1') && (a->K > 2048 || ncols > maxn)) return false;
+  if (!(er && er[0] == '1') && (a->K > 2048 || ncols > 4096)) return false;
   // e4m3 weights with bf16 rows (W8A16): 64-chunks of whole 16-code loads
   if (a->fp8_mode == 2 && (a->K % 64 != 0 || a->ldb % 16 != 0)) return false;
   pl.rows_f8 = a->fp8_mode == 2;

@@ -214,8 +214,7 @@ def rows_w8a16_ok(M, K, ncols):
     if os.environ.get("PZ_GEMM_ROWS") == "0" or os.environ.get("PZ_ROWS_W8A16") == "0":
         return False
     maxm = int(os.environ.get("PZ_ROWS_MAXM", "1024"))
-    maxn = int(os.environ.get("PZ_ROWS_MAXN", "4096"))
-    return 64 < M <= maxm and K % 64 == 0 and (os.environ.get("PZ_GEMM_ROWS") == "1" or (K <= 2048 and ncols <= maxn))
+    return 64 < M <= maxm and K % 64 == 0 and (os.environ.get("PZ_GEMM_ROWS") == "1" or (K <= 2048 and ncols <= 4096))
 
 
 def linear_dgrad(dy, W, dx, *, beta=False, resid=None, epi=PZ_EPI_NONE, aux=None):

@@ -69,16 +69,6 @@ PY
         echo "$kv $(grep -o '"value": [0-9.]*' "$OUT/knob.tmp")" >> "$OUT/knobab.log"
       done
       rm -f "$OUT/knob.tmp" ;;
-    c5knob)  # planner knobs on the C5 / C4 inference graphs, same box
-      for kv in base PZ_ROWS_MAXN=4352 PZ_GEMM_TAIL=0 base; do
-        if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
-        env "${envs[@]}" timeout -k 10 300 python -u tools/c5_bench.py --iters 50 > "$OUT/c5knob.tmp" 2>&1
-        echo "$kv C5 $(tail -1 "$OUT/c5knob.tmp" | grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' | tr '\n' ' ')" \
-          >> "$OUT/c5knob.log"
-        env "${envs[@]}" timeout -k 10 200 python -u tools/infer_bench.py --iters 100 > "$OUT/c5knob.tmp" 2>&1
-        echo "$kv C4 $(tail -1 "$OUT/c5knob.tmp")" >> "$OUT/c5knob.log"
-      done
-      rm -f "$OUT/c5knob.tmp" ;;
     trainprof)  # kernel stats of the training step alone (1 warm-up + 1 timed step, no inference legs)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trainprof" -o train \
         -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/trainprof.log" 2>&1

@@ -1166,189 +1166,6 @@ __global__ void __launch_bounds__(JP_NW * 64) flash_fwd_probs_kernel(pz_flash_ar
   }
 }
 
-// ---- joint forward, 32 query rows per wave ---------------------------------------------------------
-// flash_fwd_probs_kernel with 4 waves x 32 rows per workgroup (the same 128-row blocks and grid): every K
-// fragment read from LDS feeds the S MFMAs of two 16-row blocks and every V^T fragment their two O MFMAs --
-// half the LDS fragment reads per score, which bound the one-block-per-wave kernel (its K / V reads are
-// 64 KiB per 16 rows per K / V pass).  One wave per SIMD: the accumulators take the AGPR half of the
-// register file.  Per row the same operands in the same order: outputs bitwise equal.
-constexpr int JP2_NW = 4;
-template <int HD>
-__global__ void __launch_bounds__(JP2_NW * 64) flash_fwd_probs2_kernel(pz_flash_args a, bf16_t* P, bf16_t* TC,
-                                                                        int64_t ldp) {
-  using D = FaDims<HD>;
-  constexpr int NT = JP2_NW * 64, RPW = JP2_NW * 32;
-  __shared__ __attribute__((aligned(16))) bf16_t Ts2[2][FA_KB * D::ROW];  // K blocks, then V blocks
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  int64_t zh;
-  int qblk;
-  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
-  const int64_t b = zh / a.H, h = zh % a.H;
-  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
-  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
-  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
-  const FaMask mk(a, b);
-  const FaFast ff(a);
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ts2[bi]);
-  TileStager<HD, D::ROW, FA_KB, NT> st;
-  st.load(K, a.ldk, 0, a.nk);
-  int64_t r[2];
-  bool live[2];
-  bf16x8 qf[2][D::NKS];
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    r[rb] = (int64_t)qblk * RPW + wave * 32 + rb * 16 + (lane & 15);  // this lane's query row of block rb
-    live[rb] = r[rb] < a.nq;
-#pragma unroll
-    for (int ks = 0; ks < D::NKS; ++ks) {
-      const int c = ks * 32 + 8 * g;
-      qf[rb][ks] = (live[rb] && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + r[rb] * a.ldq + c) : bf16x8{};
-    }
-  }
-  const int full_keys = fa_full_keys(mk);
-  __syncthreads();  // pad columns zeroed
-  st.store(Ts2[0]);
-  __syncthreads();
-  // pass 1: S^T[key][q] for every key of both row blocks (stage kb = K block kb)
-  f32x4 sc[2][JP_MAXKB][4];
-  const f32x4 zero4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    if (kb >= nkb) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sc[0][kb][i] = sc[1][kb][i] = zero4;
-    } else {
-      const bf16_t* Ks = Ts2[kb & 1];
-      if (kb + 1 < nkb) st.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
-      else st.load(V, a.ldv, 0, a.nk);  // stage nkb: V block 0
-      // key sub-block i outer (same ks order per accumulator); the empty asm keeps the scheduler from
-      // hoisting every fragment read of the block ahead (register pressure of 32 fragments)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int ks = 0; ks < D::NKS; ++ks) {
-          const bf16x8 kf = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
-          // (the first product starts from a zero accumulator: no zero-initialised registers live early)
-          sc[0][kb][i] = mfma(kf, qf[0][ks], ks == 0 ? zero4 : sc[0][kb][i]);
-          sc[1][kb][i] = mfma(kf, qf[1][ks], ks == 0 ? zero4 : sc[1][kb][i]);
-        }
-        asm volatile("" ::: "memory");
-      }
-      st.store(Ts2[(kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  // per row block: logits (log2 domain) + the tanh(cap) export, the exact row softmax, the P export
-  bf16x8 pf[2][JP_MAXKB][2];
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int t = mk.token((int)r[rb]);
-    const bool dead = mk.dead(t);
-    const int rbits = fa_row_bits(mk, t);
-    bf16_t* prow = P + (b * a.nq + r[rb]) * ldp;
-    bf16_t* trow = TC ? TC + (b * a.nq + r[rb]) * ldp : nullptr;
-    float mx = -INFINITY;
-#pragma unroll
-    for (int kb = 0; kb < JP_MAXKB; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float tv[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = kb * FA_KB + i * 16 + 4 * g + e;
-          const float sv = sc[rb][kb][i][e];
-          float th = 0.f, x2;
-          if (a.cap > 0.f) {
-            th = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(sv * ff.k2) + 1.f), 1.f);
-            x2 = th * ff.crow_live;
-          } else {
-            x2 = sv * ff.crow_live;
-          }
-          const bool ok = j < (int)a.nk && (j < full_keys || ((rbits >> fa_key_class(mk, j)) & 1));
-          x2 = ok ? x2 : -INFINITY;
-          sc[rb][kb][i][e] = x2;
-          mx = fmaxf(mx, x2);
-          tv[e] = (dead || j >= (int)a.nk) ? 0.f : th;
-        }
-        const int j0 = kb * FA_KB + i * 16 + 4 * g;
-        if (trow && live[rb] && kb < nkb && j0 < ldp)
-          *reinterpret_cast<u32x2*>(trow + j0) = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < JP_MAXKB; ++kb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pv = __builtin_amdgcn_exp2f(sc[rb][kb][i][e] - mx);  // exp2(-inf) = 0
-          sc[rb][kb][i][e] = pv;
-          sum += pv;
-        }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    // fully masked (dead) rows: uniform over the N keys (the finfo.min mask absorbs the logits)
-    const float inv = 1.f / sum, uni = 1.f / (float)a.nk;
-#pragma unroll
-    for (int kb = 0; kb < JP_MAXKB; ++kb) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int j = kb * FA_KB + i * 16 + 4 * g + e;
-          sc[rb][kb][i][e] = dead ? (j < (int)a.nk ? uni : 0.f) : sc[rb][kb][i][e] * inv;
-        }
-        const int j0 = kb * FA_KB + i * 16 + 4 * g;
-        if (live[rb] && kb < nkb && j0 < ldp)
-          *reinterpret_cast<u32x2*>(prow + j0) =
-              u32x2{pack2bf(sc[rb][kb][i][0], sc[rb][kb][i][1]), pack2bf(sc[rb][kb][i][2], sc[rb][kb][i][3])};
-      }
-      pf[rb][kb][0] = pack8(sc[rb][kb][0], sc[rb][kb][1]);
-      pf[rb][kb][1] = pack8(sc[rb][kb][2], sc[rb][kb][3]);
-    }
-  }
-  // pass 2: O^T[d][q] = V^T[d][key] P^T[key][q] with the bf16 P (stage nkb + kb = V block kb)
-  f32x4 o[2][D::NDB];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    if (kb < nkb) {
-      const bf16_t* Vs = Ts2[(nkb + kb) & 1];
-      const bool more = kb + 1 < nkb;
-      if (more) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-#pragma unroll
-        for (int db = 0; db < D::NDB; ++db) {
-          const bf16x8 vf = frag_tr<D::ROW>(Vs, k2 * 32, db * 16, lane);
-          const bool first = kb == 0 && k2 == 0;  // (key block 0 always exists: nk >= 1)
-          o[0][db] = mfma(vf, pf[0][kb][k2], first ? zero4 : o[0][db]);
-          o[1][db] = mfma(vf, pf[1][kb][k2], first ? zero4 : o[1][db]);
-          if (db % 4 == 3) asm volatile("" ::: "memory");
-        }
-      }
-      if (more) st.store(Ts2[(nkb + kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  const FaRow fr{&a};
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    if (!live[rb]) continue;
-    const int gi = fr.grp(r[rb]);
-    bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, r[rb], gi);
-#pragma unroll
-    for (int db = 0; db < D::NDB; ++db) {
-      const int d = db * 16 + 4 * g;
-      if (d < HD)
-        *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(o[rb][db][0], o[rb][db][1]), pack2bf(o[rb][db][2], o[rb][db][3])};
-    }
-  }
-}
-
 // ---- joint backward: dS from the exported softmax (training default) --------------------------
 // dP^T = V dO^T for every key of a 16-row block in registers (V staged through LDS, dO rows straight
 // into MFMA B fragments), delta = sum_j P dP over the whole row, dS = P (dP - delta) scale (1 - tc^2)
@@ -2390,13 +2207,8 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
                "flash_fwd_probs: operands need 16-byte aligned rows");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z * a->H < 65536, "flash_fwd_probs: nq / units too large");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
-  const char* e = getenv("PZ_FLASH_PROBS2");  // "1": 4 waves x 32 rows per workgroup (A/B; read per call)
-  if (e && e[0] == '1')
-    hipLaunchKernelGGL(flash_fwd_probs2_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP2_NW * 64), 0,
-                       (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
-  else
-    hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
-                       (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
+  hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
+                     (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -69,8 +69,6 @@ PY
         echo "$kv $(grep -o '"value": [0-9.]*' "$OUT/knob.tmp")" >> "$OUT/knobab.log"
       done
       rm -f "$OUT/knob.tmp" ;;
-    probs2)  # joint forward: one vs two 16-row blocks per wave (PZ_FLASH_PROBS2)
-      timeout -k 10 300 python -u tools/probs2_ab.py > "$OUT/probs2_ab.log" 2>&1 ;;
     trainprof)  # kernel stats of the training step alone (1 warm-up + 1 timed step, no inference legs)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trainprof" -o train \
         -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/trainprof.log" 2>&1

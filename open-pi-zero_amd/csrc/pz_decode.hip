@@ -3,14 +3,14 @@
 // so every (token, head) is a query row of the same keys) against every cached key (vlm + proprio +
 // the action tokens themselves).
 //
-// decode_attn_mfma: one workgroup per (group of 32-key chunks, 32-row tile) of one sample (C4: one row tile
-// holds all 4 tokens x 8 heads; C5's chunk of 50 tokens = 13 row tiles), S^T and P.V on the MFMA with an
-// online softmax over the group's chunks, fp32 (O, m, l) partials to the caller's workspace (one group: O
-// written directly); the last workgroup of a (sample, row tile) to arrive (an arrival counter) merges the
-// groups' partials in fixed group order -- deterministic: the counter only elects the merger, the sum order
-// never depends on arrival.  PZ_DECODE_MERGE=launch: the merge as its own launch (decode_attn_combine, one
-// workgroup per query row).  The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of
-// once per head.
+// Two launches, each short and wide:
+//   decode_attn_mfma: one workgroup per (group of 32-key chunks, 32-row tile) of one sample (C4: one row
+//     tile holds all 4 tokens x 8 heads; C5's chunk of 50 tokens = 13 row tiles), S^T and P.V on the MFMA
+//     with an online softmax over the group's chunks, fp32 (O, m, l) partials to the caller's workspace
+//     (one group: O written directly, no second launch);
+//   decode_attn_combine: one workgroup per query row merges the groups' (m, l, O) in fixed order.
+// The K/V cache of a sample is read once (spread over nk/32 workgroups) instead of once per head.
+// Deterministic (no atomics).
 #include <stdlib.h>
 #include <string.h>
 
@@ -23,12 +23,6 @@ constexpr int DA_R = 32;     // query rows per row tile (tokens x heads)
 constexpr int DA_RMAX = 1024;  // query rows per sample
 constexpr int DA_HD = 256;   // head dim (Gemma)
 constexpr int DA_RS = DA_HD + 4;  // workspace row: O[256], m, l (16-byte aligned rows)
-constexpr int DA_MAXTILES = 65536;  // (sample, row tile) pairs per launch (grid.y limit, host-checked)
-
-// arrival counters of the in-kernel merge (one per (sample, row tile)): zero at load, returned to zero by the
-// workgroup that merges, so every launch starts from zero.  Launches of pz_decode_attn therefore must not
-// overlap in time (one stream; the engine runs every decode attention on its compute stream).
-__device__ unsigned int da_arrive[DA_MAXTILES];
 
 __device__ __forceinline__ bool da_allowed(int t, int j, int nk, int cnt, int P, int C) {
   if (j >= nk) return false;
@@ -104,7 +98,7 @@ __device__ __forceinline__ bf16x8 da_vfrag(const char* img, int dt, int lane) {
   return __builtin_bit_cast(bf16x8, out);
 }
 
-__global__ void __launch_bounds__(256) decode_attn_mfma(pz_decode_attn_args a, int nch, int tail_merge) {
+__global__ void __launch_bounds__(256) decode_attn_mfma(pz_decode_attn_args a, int nch) {
   __shared__ float S[DA_R][DA_KC + 1];
   __shared__ __attribute__((aligned(16))) bf16_t Pm[DA_R][DA_KC + 8];  // bf16 probabilities [row][key]
   __shared__ __attribute__((aligned(16))) char Vimg[DA_KC * 512];       // one chunk of V, transposed reads
@@ -264,67 +258,6 @@ __global__ void __launch_bounds__(256) decode_attn_mfma(pz_decode_attn_args a, i
       }
     }
   }
-  if (direct || !tail_merge) return;
-  // in-kernel merge: the last workgroup of this (sample, row tile) to arrive sums every group's partials in
-  // group order (agent-scope release of the partials before the arrival, acquire after it)
-  __shared__ int last_s;
-  __threadfence();
-  __syncthreads();
-  const int tile = blockIdx.y;
-  if (threadIdx.x == 0) {
-    const unsigned prev = atomicAdd(&da_arrive[tile], 1u);
-    last_s = prev == gridDim.x - 1;
-    if (last_s) atomicExch(&da_arrive[tile], 0u);
-  }
-  __syncthreads();
-  if (!last_s) return;
-  __threadfence();
-  // 8 threads per row (32 dims each), batches of 4 groups: (m, l) and 8 x 16 B of O per group in flight
-  const int rl = threadIdx.x >> 3, part = threadIdx.x & 7, rr = r0 + rl;
-  if (rr >= R) return;
-  const float* w0 = a.ws + ((int64_t)b * gridDim.x * Rpad + r0 + rl) * DA_RS + part * 32;
-  const int64_t gs = (int64_t)Rpad * DA_RS;  // group stride
-  constexpr int GB = 4;
-  float M = -INFINITY, l = 0.f;
-  f32x4 o[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) o[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int c0 = 0; c0 < (int)gridDim.x; c0 += GB) {
-    float mv[GB], lv[GB];
-    f32x4 ov[GB][8];
-#pragma unroll
-    for (int u = 0; u < GB; ++u) {
-      const bool ok = c0 + u < (int)gridDim.x;
-      const float* w = w0 + (int64_t)(ok ? c0 + u : 0) * gs;
-      mv[u] = ok ? w[DA_HD - part * 32] : -INFINITY;
-      lv[u] = ok ? w[DA_HD + 1 - part * 32] : 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) ov[u][q] = ok ? *reinterpret_cast<const f32x4*>(w + 4 * q) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    float Mn = M;
-#pragma unroll
-    for (int u = 0; u < GB; ++u) Mn = fmaxf(Mn, mv[u]);
-    const float sc = M == -INFINITY ? 0.f : __expf(M - Mn);
-    l *= sc;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) o[q] *= sc;
-#pragma unroll
-    for (int u = 0; u < GB; ++u) {
-      const float sw = mv[u] == -INFINITY ? 0.f : __expf(mv[u] - Mn);
-      l += sw * lv[u];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) o[q] += sw * ov[u][q];
-    }
-    M = Mn;
-  }
-  const float il = l > 0.f ? 1.f / l : 0.f;
-  const int tt = rr / nh, hh = rr % nh;
-  bf16_t* out = (bf16_t*)a.o + ((int64_t)b * a.T + tt) * a.ldo + (int64_t)hh * DA_HD + part * 32;
-#pragma unroll
-  for (int q = 0; q < 8; q += 2)
-    *reinterpret_cast<u32x4*>(out + 4 * q) = u32x4{pack2bf(o[q][0] * il, o[q][1] * il), pack2bf(o[q][2] * il, o[q][3] * il),
-                                                   pack2bf(o[q + 1][0] * il, o[q + 1][1] * il),
-                                                   pack2bf(o[q + 1][2] * il, o[q + 1][3] * il)};
 }
 
 }  // namespace
@@ -360,15 +293,9 @@ extern "C" int pz_decode_attn(const pz_decode_attn_args* a, void* stream) {
     nch = (nchunks + 1) / 2;
     ngroups = (nchunks + nch - 1) / nch;
   }
-  // the partial merge: in the kernel by the last workgroup of each (sample, row tile) to finish (default), or
-  // PZ_DECODE_MERGE=launch: the separate decode_attn_combine launch (A/B; read per call)
-  const char* em = getenv("PZ_DECODE_MERGE");
-  const bool tail_merge = ngroups > 1 && !(em && strcmp(em, "launch") == 0) && PZ_ALIGNED(a->o, 16) && a->ldo % 8 == 0;
-  PZ_CHECK_ARG(a->B * rtiles <= DA_MAXTILES, "decode_attn: too many (sample, row tile) pairs");
-  hipLaunchKernelGGL(decode_attn_mfma, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch,
-                     (int)tail_merge);
+  hipLaunchKernelGGL(decode_attn_mfma, dim3((unsigned)ngroups, (unsigned)(a->B * rtiles)), dim3(256), 0, st, *a, nch);
   PZ_CHECK_LAUNCH();
-  if (ngroups == 1 || tail_merge) return PZ_OK;  // the kernel wrote O
+  if (ngroups == 1) return PZ_OK;  // the kernel wrote O
   hipLaunchKernelGGL(decode_attn_combine, dim3((unsigned)(a->T * a->nh), (unsigned)a->B), dim3(256), 0, st, *a,
                      ngroups);
   PZ_CHECK_LAUNCH();

@@ -802,23 +802,19 @@ def test_time_embed_modes_match_reference():
         assert outs[1] < outs[0], outs
 
 
-@pytest.mark.parametrize("mode", ["mfma", "mfma_wg64", "mfma_launch"])
+@pytest.mark.parametrize("mode", ["mfma", "mfma_wg64"])
 @pytest.mark.parametrize("B,T,cnts,P", [(1, 4, [270], 276), (2, 4, [276, 259], 276), (1, 2, [100], 276),
                                           (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276)])
 def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
     with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
     P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  mode "mfma": the
-    key-split MFMA kernel (P.V on the matrix cores), the partials merged in fixed group order by the last
-    workgroup of each row tile to arrive (default); "mfma_wg64": several chunks per workgroup (online softmax
-    across chunks); "mfma_launch": the merge as its own launch (PZ_DECODE_MERGE=launch).  Repeated calls: the
-    arrival counters return to zero (every call merges)."""
+    key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default); "mfma_wg64": several chunks
+    per workgroup (online softmax across chunks) + merge"""
     from pizero_native import ops
 
     if mode == "mfma_wg64":
         monkeypatch.setenv("PZ_DECODE_WG", "4")
-    if mode == "mfma_launch":
-        monkeypatch.setenv("PZ_DECODE_MERGE", "launch")
     C, nh, hd = 1, 8, 256
     nk = P + C + T
     Lp = (nk + 7) // 8 * 8
@@ -827,12 +823,6 @@ def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     cnt = torch.tensor(cnts, device=dev, dtype=torch.int32)
     o = torch.empty(B * T, nh * hd, device=dev, dtype=torch.bfloat16)
     ops.decode_attn(q, T, 0, k, v, o, B, nh, T, nk, 1 / 16.0, 50.0, cnt, P, C, P + C)
-    o2 = torch.full_like(o, float("nan"))
-    for _ in range(3):  # same inputs again: bitwise the same output, written by every call
-        o2.fill_(float("nan"))
-        ops.decode_attn(q, T, 0, k, v, o2, B, nh, T, nk, 1 / 16.0, 50.0, cnt, P, C, P + C)
-        torch.cuda.synchronize()
-        assert torch.equal(o2, o)
     qf = q.float().view(B, T, nh, hd)
     s = torch.einsum("bthd,bjd->bhtj", qf, k.float()[:, :nk]) / 16.0
     s = 50.0 * torch.tanh(s / 50.0)

@@ -69,16 +69,6 @@ PY
         echo "$kv $(grep -o '"value": [0-9.]*' "$OUT/knob.tmp")" >> "$OUT/knobab.log"
       done
       rm -f "$OUT/knob.tmp" ;;
-    mergeab)  # decode attention: in-kernel last-arriver merge (default) vs the separate combine launch
-      for kv in base PZ_DECODE_MERGE=launch base PZ_DECODE_MERGE=launch; do
-        if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
-        env "${envs[@]}" timeout -k 10 200 python -u tools/infer_bench.py --iters 100 > "$OUT/merge.tmp" 2>&1
-        echo "$kv C4 $(tail -1 "$OUT/merge.tmp")" >> "$OUT/mergeab.log"
-        env "${envs[@]}" timeout -k 10 300 python -u tools/c5_bench.py --iters 50 > "$OUT/merge.tmp" 2>&1
-        echo "$kv C5 $(tail -1 "$OUT/merge.tmp" | grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' | tr '\n' ' ')" \
-          >> "$OUT/mergeab.log"
-      done
-      rm -f "$OUT/merge.tmp" ;;
     trainprof)  # kernel stats of the training step alone (1 warm-up + 1 timed step, no inference legs)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trainprof" -o train \
         -- python3 bench.py --steps 1 --warmup 1 --no-infer --no-cpu-baseline > "$OUT/trainprof.log" 2>&1

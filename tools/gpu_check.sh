@@ -62,7 +62,7 @@ PY
       timeout -k 10 500 python -u bench.py --steps ${AB_STEPS:-3} --warmup 1 --no-infer --no-cpu-baseline \
         --micro-batch 128 > "$OUT/ab_mb128.log" 2>&1 ;;
     knobab)  # engine knobs at the default micro-batch, same box: one bench line each (--no-infer)
-      for kv in base PZ_SPLIT_DGEGLU=1 PZ_SPLIT_DACT=0 PZ_EXPERT_STREAM=0 PZ_JOINT_ATTN=gemm base; do
+      for kv in ${KNOBS:-base PZ_SPLIT_DGEGLU=1 PZ_SPLIT_DACT=0 PZ_EXPERT_STREAM=0 PZ_JOINT_ATTN=gemm base}; do
         if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
         env "${envs[@]}" timeout -k 10 400 python -u bench.py --steps 3 --warmup 1 --no-infer --no-cpu-baseline \
           > "$OUT/knob.tmp" 2>&1

@@ -979,3 +979,55 @@ def test_gemm_tall_forward_epilogues(M, N, K, geglu, monkeypatch):
         o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         ops.gemm(M, N, K, x, K, True, Wt, N, False, o, N, resid=r, ld_resid=N)
         close(o, ref + r.float(), atol=2e-2)
+
+
+@pytest.mark.parametrize("M", [256, 4096])
+def test_siglip_mlp_row_pitch_bitwise(M):
+    """SigLIP's 4304-wide MLP activations at the engine's 4352-element row pitch (engine.Engine._sig_rows):
+    every GEMM that reads or writes them -- fc1 forward + GELU (output and saved pre-activation), fc2 forward
+    (K = 4304: the K-tail clamps its loads into the row), the fc2 dgrad writing d(fc1 out), the fc1 dgrad and
+    both weight gradients reading them -- gives bitwise the contiguous result, and the pad columns are neither
+    read (NaN there changes nothing) nor written (they stay NaN)."""
+    from pizero_native import ops
+
+    D, F, P = 1152, 4304, 4352
+
+    def padded(t):
+        buf = torch.full((t.shape[0], P), float("nan"), device=dev, dtype=t.dtype)
+        buf[:, :F].copy_(t)
+        return buf, buf[:, :F]
+
+    x, dy = bf(M, D), bf(M, D)
+    w1, w2 = bf(F, D, scale=0.05), bf(D, F, scale=0.05)
+    b1, b2 = bf(F), bf(D)
+    # fc1 forward + GELU, output and pre-activation at the padded pitch
+    h0, a0 = torch.empty(M, F, device=dev, dtype=torch.bfloat16), torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    ops.linear(x, w1, h0, bias=b1, epi=ops.PZ_EPI_GELU, aux=a0)
+    hb, h1 = padded(torch.zeros(M, F, device=dev, dtype=torch.bfloat16))
+    ab, a1 = padded(torch.zeros(M, F, device=dev, dtype=torch.bfloat16))
+    ops.linear(x, w1, h1, bias=b1, epi=ops.PZ_EPI_GELU, aux=a1)
+    assert torch.equal(h1, h0) and torch.equal(a1, a0)
+    assert torch.isnan(hb[:, F:].float()).all() and torch.isnan(ab[:, F:].float()).all()
+    # fc2 forward reading the padded rows (K = 4304)
+    y0, y1 = torch.empty(M, D, device=dev, dtype=torch.bfloat16), torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    ops.linear(h0, w2, y0, bias=b2, resid=x)
+    ops.linear(h1, w2, y1, bias=b2, resid=x)
+    assert torch.equal(y1, y0)
+    # fc2 dgrad into padded rows; fc1 dgrad and both weight gradients reading them
+    g0 = torch.empty(M, F, device=dev, dtype=torch.bfloat16)
+    ops.linear_dgrad(dy, w2, g0)
+    gb, g1 = padded(torch.zeros(M, F, device=dev, dtype=torch.bfloat16))
+    ops.linear_dgrad(dy, w2, g1)
+    assert torch.equal(g1, g0) and torch.isnan(gb[:, F:].float()).all()
+    d0, d1 = torch.empty(M, D, device=dev, dtype=torch.bfloat16), torch.empty(M, D, device=dev, dtype=torch.bfloat16)
+    ops.linear_dgrad(g0, w1, d0)
+    ops.linear_dgrad(g1, w1, d1)
+    assert torch.equal(d1, d0)
+    wg0, wg1 = torch.empty(D, F, device=dev, dtype=torch.bfloat16), torch.empty(D, F, device=dev, dtype=torch.bfloat16)
+    ops.linear_wgrad(dy, h0, wg0)  # fc2 weight gradient: dy^T h
+    ops.linear_wgrad(dy, h1, wg1)
+    assert torch.equal(wg1, wg0)
+    v0, v1 = torch.empty(F, D, device=dev, dtype=torch.bfloat16), torch.empty(F, D, device=dev, dtype=torch.bfloat16)
+    ops.linear_wgrad(g0, x, v0)
+    ops.linear_wgrad(g1, x, v1)
+    assert torch.equal(v1, v0)

@@ -2,7 +2,8 @@
 
     python tools/gemm_one.py --layout TN --M 17664 --N 2048 --K 2048 [--variant 8phase|2stage] [--iters 5]
 M, N, K = the forward nn.Linear shape; layouts NT (fwd), NN (dgrad), TN (wgrad) as in tools/gemm_bench.py;
-GEGLU = the vlm gate|up GEMM with the GeGLU epilogue and saved g|u (N = 2 * intermediate).
+GEGLU = the vlm gate|up GEMM with the GeGLU epilogue and saved g|u (N = 2 * intermediate); DGEGLU = the down-proj
+dgrad with the GeGLU derivative (M x N x K = tokens x hidden x intermediate, e.g. --M 70656 --N 2048 --K 16384).
 """
 
 import argparse
@@ -38,7 +39,10 @@ def main():
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
     dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
     dW = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
-    if a.layout == "GEGLU":  # the bench's dominant launch: gate|up GEMM + GeGLU, saved g|u (engine.py)
+    if a.layout == "DGEGLU":  # the vlm down-proj dgrad with the GeGLU derivative: reads g|u, writes d(g|u) in place
+        gu = rnd(M, 2 * K)
+        fn = lambda: ops.linear_dgrad(dy, w, gu, epi=ops.PZ_EPI_DGEGLU, aux=gu)  # noqa: E731
+    elif a.layout == "GEGLU":  # the bench's dominant launch: gate|up GEMM + GeGLU, saved g|u (engine.py)
         hm = torch.empty(M, N // 2, device=dev, dtype=torch.bfloat16)
         fn = lambda: ops.linear(x, w, hm, epi=ops.PZ_EPI_GEGLU, aux=y)  # noqa: E731
     else:

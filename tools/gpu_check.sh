@@ -92,6 +92,9 @@ PY
       timeout -k 10 400 python -u tools/gemm_bench.py --iters 10 > "$OUT/gemm_bench.log" 2>&1 ;;
     pmc)
       bash tools/pmc_dominant.sh "$OUT/pmc" ;;
+    pmcdgeglu)  # the same counter passes on the DGEGLU dgrad (down-proj dgrad + GeGLU derivative, micro-batch 256)
+      PMC_CMD="python3 tools/gemm_one.py --layout DGEGLU --M 70656 --N 2048 --K 16384 --iters 3" \
+        bash tools/pmc_dominant.sh "$OUT/pmcd" ;;
     census)
       timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-256} > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -6,7 +6,7 @@
 set -e
 OUT=${1:-gpurun_out/pmc}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-CMD="python3 tools/gemm_one.py --layout GEGLU --M ${PMC_M:-70656} --N 32768 --K 2048 --iters 3"
+CMD=${PMC_CMD:-"python3 tools/gemm_one.py --layout GEGLU --M ${PMC_M:-70656} --N 32768 --K 2048 --iters 3"}
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d "$OUT/fetch" -o fetch \
   --pmc FETCH_SIZE GRBM_GUI_ACTIVE -- $CMD > "$OUT.fetch.log" 2>&1
 timeout -s KILL 90 rocprofv3 --kernel-trace --output-format csv -d "$OUT/write" -o write \

@@ -268,9 +268,84 @@ def _graph_ms(fn, iters):
     return e0.elapsed_time(e1) / iters
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def rank_envs(n, port, base=None):
+    """The torchrun-style environment of each of n local ranks (reference: slurm/train_multi_gpu.sh:26-42 launches
+    one process per GPU; scripts/run.py:39-47 reads LOCAL_RANK / WORLD_SIZE and sets the device from LOCAL_RANK)."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` started without a launcher: run N copies of this script, one per GPU, as children
+    (before this process touches the GPU), inheriting stdout/stderr so rank 0's JSON line is the output.  A
+    child that fails ends the others (they would wait in a collective); returns the worst exit code."""
+    import signal
+    import subprocess
+
+    if "PZ_DEVICE" not in os.environ:
+        have = torch.cuda.device_count()  # does not initialise HIP on this image
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+
+    def pdeathsig():  # a child outlives neither a killed parent nor its timeout
+        import ctypes
+
+        ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+
+    port = _free_port()
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e, preexec_fn=pdeathsig)
+             for e in rank_envs(n, port)]
+
+    def stop_all(*_):
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.time() + 20
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    signal.signal(signal.SIGTERM, lambda *a: (stop_all(), sys.exit(143)))
+    worst = 0
+    while any(p.poll() is None for p in procs):
+        for p in procs:
+            rc = p.poll()
+            if rc not in (None, 0) and worst == 0:
+                worst = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                stop_all()
+        time.sleep(0.2)
+    for p in procs:
+        if p.returncode != 0 and worst == 0:
+            worst = p.returncode if p.returncode > 0 else 128 - p.returncode
+    return worst
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); without WORLD_SIZE in the environment bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--global-batch", type=int, default=1024)
@@ -289,6 +364,12 @@ def main():
                          "comm stream) even at world size 1 (single-GPU check of the N>1 code path)")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and args.gpus is not None and int(env_world) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (launcher mismatch)", file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -383,6 +464,17 @@ def main():
     el = float(elt.item())
     comm = None
     if ddp:
+        # data parallelism keeps every replica's weights identical: a checksum of each rank's parameter arena
+        # after the timed steps (outside the timed region)
+        data = model._arena.data
+        cs = torch.zeros(1, dtype=torch.float64, device=dev)
+        for i in range(0, data.numel(), 1 << 26):
+            cs += data[i:i + (1 << 26)].float().sum(dtype=torch.float64)
+        css = [torch.zeros_like(cs) for _ in range(world)]
+        dist.all_gather(css, cs)
+        replicas_equal = all(torch.equal(c, css[0]) for c in css)
+        if not replicas_equal:
+            log(f"[bench] replica weight checksums differ: {[float(c) for c in css]}")
         meta.reducer.timing = False
         comm = meta.reducer.timing_summary(args.steps)
         if comm is not None:  # max over ranks (the slowest rank's communication sets the step)
@@ -464,7 +556,8 @@ def main():
             "ddp": None if not ddp else {
                 "backend": dist.get_backend(), "buckets_reduced_per_step": sum(1 for _ in meta.reducer.log) / max(
                     1, args.steps + args.warmup), "async_rccl_buckets": sum(1 for a, _ in meta.reducer.log if a),
-                "forced_at_world_1": bool(args.force_ddp and world == 1), **(comm or {})},
+                "forced_at_world_1": bool(args.force_ddp and world == 1), "replica_weights_equal": replicas_equal,
+                **(comm or {})},
             "mfma_frac_step": samples_s * TRAIN_FLOP_PER_SAMPLE / (world * PEAK_BF16_TFLOPS * 1e12),
             "roofline": {"bound": "mfma", "kernel": kname + " (vlm gate|up GeGLU GEMM)",
                          "shape_MNK": [Mg, Ng, Kg], "launches_timed": len(durs), "avg_launch_ms": kern_ms,

@@ -1,8 +1,8 @@
-"""Microbenchmark of the fused attention kernels at the bench shapes (micro-batch 64).
+"""Microbenchmark of the fused attention kernels at the bench shapes (micro-batch 256).
 
-    python tools/flash_bench.py [--iters 10]
-joint: 64 samples x (281 tokens x 8 heads) queries, 281 keys, head 256, soft-cap + block mask;
-siglip: 64 x 16 heads x 256 x 256, head 72.  Prints fwd / bwd ms and TF/s (algorithmic
+    python tools/flash_bench.py [--iters 10] [--batch 256] [--default-only]
+joint: B samples x (281 tokens x 8 heads) queries, 281 keys, head 256, soft-cap + block mask;
+siglip: B x 16 heads x 256 x 256, head 72.  Prints fwd / bwd ms and TF/s (algorithmic
 FLOP: fwd 4*nq*nk*hd per unit, bwd 2.5x fwd).
 """
 import argparse
@@ -33,9 +33,11 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--default-only", action="store_true", help="only the training-default kernels (PMC passes)")
     a = ap.parse_args()
     dev = "cuda"
-    B, P, C, H, nh, hd = 64, 276, 1, 4, 8, 256
+    B, P, C, H, nh, hd = a.batch, 276, 1, 4, 8, 256
     L = P + C + H
     Lp = (L + 7) // 8 * 8
     Q = torch.randn(B, L * nh, hd, device=dev).to(torch.bfloat16)
@@ -53,7 +55,6 @@ def main():
                         cap=50.0, mask_mode=1, cnt=cnt, prefix=P, cond=C, rows_per_token=nh, dgroups=[dOv, dOe],
                         delta=delta, dq=dQ, dk=dK, dv=dV)
     fl = 4.0 * B * L * nh * L * hd
-    tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
     Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
     tcm = torch.empty_like(Pm)
     tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
@@ -61,12 +62,13 @@ def main():
     dSm = torch.empty_like(Pm)
     td = timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters)
     print(f"joint  bwd dS {td:.3f} ms (dP = dO V^T in registers + softmax backward from P / tanh(cap))", flush=True)
-    for fast in ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
+    for fast in () if a.default_only else ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
         os.environ["PZ_FLASH_FAST"] = fast
+        tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
         tb = timeit(lambda: ops.flash_bwd(fa), a.iters)
         print(f"joint(fast={fast})  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
               f"{2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
-    os.environ.pop("PZ_FLASH_FAST")
+    os.environ.pop("PZ_FLASH_FAST", None)
     nh, hd, N = 16, 72, 256
     qkv = torch.randn(B * N, 3 * nh * hd, device=dev).to(torch.bfloat16)
     O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
@@ -76,7 +78,7 @@ def main():
     dqkv = torch.empty_like(qkv)
     sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
     fl = 4.0 * B * nh * N * N * hd
-    for unit in ("1", "0"):  # PZ_FLASH_UNIT: one workgroup per (image, head) unit vs the 2-/4-workgroup kernels
+    for unit in ("1",) if a.default_only else ("1", "0"):  # PZ_FLASH_UNIT: one workgroup per (image, head) unit vs the 2-/4-workgroup kernels
         os.environ["PZ_FLASH_UNIT"] = unit
         tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
         tb = timeit(lambda: ops.flash_bwd(sa), a.iters)

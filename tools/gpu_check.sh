@@ -95,6 +95,13 @@ PY
     pmcdgeglu)  # the same counter passes on the DGEGLU dgrad (down-proj dgrad + GeGLU derivative, micro-batch 256)
       PMC_CMD="python3 tools/gemm_one.py --layout DGEGLU --M 70656 --N 2048 --K 16384 --iters 3" \
         bash tools/pmc_dominant.sh "$OUT/pmcd" ;;
+    pmcattn)  # counter passes of the training-default attention kernels at micro-batch 256
+      bash tools/pmc_flash.sh "$OUT/pmca" && python3 tools/pmc_attn.py "$OUT/pmca" "$OUT/pmc_attn.json" \
+        > "$OUT/pmc_attn.txt" 2>&1
+      rm -f "$OUT"/pmca/*/*kernel_trace.csv ;;
+    launcher)  # bench.py --gpus 2 rehearsal: 2 gloo ranks on this card
+      timeout -k 10 900 python -u -m pytest tests/test_bench_launcher.py -m gpu -x -v --timeout 880 \
+        --timeout-method thread > "$OUT/launcher.log" 2>&1 ;;
     census)
       timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-256} > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

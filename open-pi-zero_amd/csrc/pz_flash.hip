@@ -2071,6 +2071,533 @@ __global__ void __launch_bounds__(FU_NW * 64) flash_bwd_kv_unit_kernel(pz_flash_
 
 constexpr int FU_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
 
+// ---- SigLIP attention, persistent and pipelined (training: 16 heads x 72, 256 tokens, no mask) ----------
+// PMC of the one-workgroup-per-unit kernels above (profiles/r05/pmc_attn_*.json): the waves spend 43-62 % of
+// their cycles parked at s_waitcnt / barriers -- each unit's 114 KiB LDS image holds one workgroup per CU, so
+// the staging of every unit's resident operand is exposed -- and the forward issues ~7 vector instructions
+// per MFMA (mask selects on full key blocks, a separate scale multiply).  Here a grid of one workgroup per CU
+// walks its units in turn with the resident operand images double-buffered: LDS-DMA (no VGPR staging) brings
+// unit i+1's images while unit i computes.  The images use an 80-element (160-B) row pitch, so two units'
+// K and V (or Q and dO) fit the CU's 160 KiB, and both the 16-row ds_read_b128 fragments and the 4-row
+// ds_read_b64_tr_b16 fragments are bank-conflict free (row r starts at dword 40 r: 16 consecutive rows tile
+// the 64 banks).  Each row's tenth 16-B chunk (head dims 72..79) repeats the ninth: the products that read it
+// meet zero Q / dO columns or land in discarded output columns; the 32-wide k step past column 79 reads the
+// next row's (finite) data against zero Q columns the same way.
+constexpr int FS_N = 256, FS_ROW = 80, FS_IMG = FS_N * FS_ROW * 2, FS_SMEM = 4 * FS_IMG;
+constexpr int FS_NW = 8, FS_PER = FS_N * 10 / 64 / FS_NW;  // DMA instructions per wave per image (5)
+
+__device__ __forceinline__ void fs_glds16(const bf16_t* src, char* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// unit of iteration t for this workgroup: G workgroups; with G % 8 == 0 and (G / 8) % H == 0 the G / 8
+// units an XCD runs together are whole images (all H heads: their 144-B q / k / v segments share lines)
+__device__ __forceinline__ int64_t fs_unit(const pz_flash_args& a, int G, int t) {
+  const int i = blockIdx.x;
+  if (G % 8 != 0 || (G / 8) % a.H != 0) return (int64_t)t * G + i;
+  return (int64_t)t * G + (i & 7) * (G / 8) + (i >> 3);
+}
+
+// per-lane element offsets of this wave's FS_PER DMA pieces of a [256][72] operand with row stride ld
+__device__ __forceinline__ void fs_dma_offsets(int64_t ld, int wave, int lane, int (&off)[FS_PER]) {
+#pragma unroll
+  for (int s = 0; s < FS_PER; ++s) {
+    const int c = (wave * FS_PER + s) * 64 + lane, row = c / 10, ch = c % 10;
+    off[s] = row * (int)ld + 8 * (ch < 9 ? ch : 8);
+  }
+}
+
+__device__ __forceinline__ void fs_dma(const bf16_t* base, const int (&off)[FS_PER], char* img, int wave) {
+#pragma unroll
+  for (int s = 0; s < FS_PER; ++s) fs_glds16(base + off[s], img + (wave * FS_PER + s) * 1024);
+}
+
+#define FS_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+// ds_read_b64_tr_b16 by inline asm: NOT counted by hipcc's lgkmcnt tracking -- the caller waits with an asm
+// that names the result (see the forward's V^T fragments)
+template <int OFF>  // byte offset folded into the instruction
+__device__ __forceinline__ s16x4 fs_tr(unsigned lds_addr) {
+  s16x4 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(lds_addr), "i"(OFF));
+  return v;
+}
+__device__ __forceinline__ unsigned fs_lds_addr(const void* p) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
+}
+__device__ __forceinline__ bf16x8 fs_cat(const s16x4& a, const s16x4& b) {
+  s16x8 o;
+  o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];
+  o[4] = b[0]; o[5] = b[1]; o[6] = b[2]; o[7] = b[3];
+  return __builtin_bit_cast(bf16x8, o);
+}
+// workgroup barrier without __syncthreads()'s release fence (which drains vmcnt, i.e. the next unit's
+// LDS-DMA): this wave's LDS reads are done (lgkmcnt) and its DMA pieces waited for by FS_WAIT_VM
+#define FS_BARRIER()                                   \
+  do {                                                 \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); \
+    __builtin_amdgcn_s_barrier();                      \
+    asm volatile("" ::: "memory");                     \
+  } while (0)
+
+// forward: wave w owns query rows 32w .. 32w + 31 of the unit (two 16-row blocks share each K / V
+// fragment read); log2-domain online softmax over four 64-key blocks with the scale folded into the
+// exponent's FMA (max over raw scores: scale > 0)
+__global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_args a, int G) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t units = a.Z * a.H;
+  int offk[FS_PER], offv[FS_PER];
+  fs_dma_offsets(a.ldk, wave, lane, offk);
+  fs_dma_offsets(a.ldv, wave, lane, offv);
+  const float sl2 = a.scale * FA_LOG2E;
+  // Pipeline (per workgroup, unit t in buffer t & 1): the Q fragments of unit t + 1 (inline-asm loads into
+  // qn: hipcc would drain every in-flight LDS-DMA with vmcnt(0) at the first use of an ordinary load) and its
+  // K / V images are issued before unit t's compute; one vmcnt(0) after the compute (long landed by then),
+  // before unit t's O stores, and the barrier that ends unit t publish them, so no wait stalls in steady state.
+  int64_t u = fs_unit(a, G, 0);
+  bf16x8 qn[2][3];
+  auto issue = [&](int64_t un, int t1) {  // Q fragments + K / V images of unit un into buffer t1 & 1
+    const int64_t bn = un / a.H, hn = un % a.H;
+    const bf16_t* Q = (const bf16_t*)a.q + bn * a.q_bstride + hn * a.q_hstride;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {  // head dims 72..95 (g >= 1 at ks 2) re-read dims 64..71, zeroed below
+        const bf16_t* src = Q + (wave * 32 + qb * 16 + (lane & 15)) * a.ldq + (ks < 2 || g == 0 ? ks * 32 + 8 * g : 64);
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qn[qb][ks]) : "v"(src) : "memory");
+      }
+    char* nxt = fa_smem + (t1 & 1) * 2 * FS_IMG;
+    fs_dma((const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride, offk, nxt, wave);
+    fs_dma((const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride, offv, nxt + FS_IMG, wave);
+  };
+  if (u < units) issue(u, 0);
+  FS_WAIT_VM(0);
+  FS_BARRIER();
+  for (int t = 0; u < units; ++t) {
+    const int64_t b = u / a.H, h = u % a.H;
+    bf16x8 qf[2][3];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        asm volatile("" : "+v"(qn[qb][ks]));  // landed (the vmcnt(0) before the previous barrier)
+        qf[qb][ks] = qn[qb][ks];
+      }
+      if (g != 0) qf[qb][2] = bf16x8{};
+    }
+    const int64_t un = fs_unit(a, G, t + 1);
+    if (un < units) issue(un, t + 1);  // uniform
+    const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
+    const bf16_t* Kall = reinterpret_cast<const bf16_t*>(cur);
+    const bf16_t* Vall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
+    f32x4 o[5][2];
+#pragma unroll
+    for (int db = 0; db < 5; ++db) o[db][0] = o[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};  // m: running max of the RAW scores
+#pragma unroll 1
+    for (int kb = 0; kb < FS_N / FA_KB; ++kb) {
+      const bf16_t* Ks = Kall + kb * FA_KB * FS_ROW;
+      const bf16_t* Vs = Vall + kb * FA_KB * FS_ROW;
+      f32x4 sc[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[i][0] = sc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bf16x8 kf = frag_row<FS_ROW>(Ks, i * 16, ks * 32, lane);
+          sc[i][0] = mfma(kf, qf[0][ks], sc[i][0]);
+          sc[i][1] = mfma(kf, qf[1][ks], sc[i][1]);
+        }
+      bf16x8 pf[2][2];  // [k-step of 32 keys][query block]
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        float mx = fmaxf(fmaxf(sc[0][qb][0], sc[0][qb][1]), fmaxf(sc[0][qb][2], sc[0][qb][3]));
+#pragma unroll
+        for (int i = 1; i < 4; ++i)
+          mx = fmaxf(fmaxf(mx, fmaxf(sc[i][qb][0], sc[i][qb][1])), fmaxf(sc[i][qb][2], sc[i][qb][3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mn = fmaxf(m[qb], mx), nb = -mn * sl2;
+        const float alpha = __builtin_amdgcn_exp2f((m[qb] - mn) * sl2);  // exp2(-inf) = 0 on the first block
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sc[i][qb][e], sl2, nb));
+            sc[i][qb][e] = pv;
+            sum += pv;
+          }
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        l[qb] = fmaf(l[qb], alpha, sum);
+        m[qb] = mn;
+#pragma unroll
+        for (int db = 0; db < 5; ++db) o[db][qb] *= alpha;
+        pf[0][qb] = pack8(sc[0][qb], sc[1][qb]);
+        pf[1][qb] = pack8(sc[2][qb], sc[3][qb]);
+      }
+      // V^T fragments by inline-asm transposed reads (with the builtin hipcc drains the in-flight LDS-DMA
+      // before each); the waits name the fragments so the consuming MFMAs stay behind them
+      s16x4 tv[2][5][2];
+      const unsigned va = fs_lds_addr(Vs + (4 * g + ((lane & 15) >> 2)) * FS_ROW + 4 * (lane & 3));
+#define FS_TR(k2, db, hf) tv[k2][db][hf] = fs_tr<((k2) * 32 + 16 * (hf)) * FS_ROW * 2 + (db) * 32>(va)
+#define FS_TR_DB(k2, db) FS_TR(k2, db, 0); FS_TR(k2, db, 1)
+      FS_TR_DB(0, 0); FS_TR_DB(0, 1); FS_TR_DB(0, 2); FS_TR_DB(0, 3); FS_TR_DB(0, 4);
+      FS_TR_DB(1, 0); FS_TR_DB(1, 1); FS_TR_DB(1, 2); FS_TR_DB(1, 3); FS_TR_DB(1, 4);
+#undef FS_TR_DB
+#undef FS_TR
+      asm volatile("s_waitcnt lgkmcnt(10)"
+                   : "+v"(tv[0][0][0]), "+v"(tv[0][0][1]), "+v"(tv[0][1][0]), "+v"(tv[0][1][1]), "+v"(tv[0][2][0]),
+                     "+v"(tv[0][2][1]), "+v"(tv[0][3][0]), "+v"(tv[0][3][1]), "+v"(tv[0][4][0]), "+v"(tv[0][4][1]));
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const bf16x8 vf = fs_cat(tv[0][db][0], tv[0][db][1]);
+        o[db][0] = mfma(vf, pf[0][0], o[db][0]);
+        o[db][1] = mfma(vf, pf[0][1], o[db][1]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(tv[1][0][0]), "+v"(tv[1][0][1]), "+v"(tv[1][1][0]), "+v"(tv[1][1][1]), "+v"(tv[1][2][0]),
+                     "+v"(tv[1][2][1]), "+v"(tv[1][3][0]), "+v"(tv[1][3][1]), "+v"(tv[1][4][0]), "+v"(tv[1][4][1]));
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const bf16x8 vf = fs_cat(tv[1][db][0], tv[1][db][1]);
+        o[db][0] = mfma(vf, pf[1][0], o[db][0]);
+        o[db][1] = mfma(vf, pf[1][1], o[db][1]);
+      }
+    }
+    FS_WAIT_VM(0);  // the next unit's Q fragments and images (issued before this unit's compute)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {  // one output group (host-checked)
+      const int64_t rq = wave * 32 + qb * 16 + (lane & 15);
+      const float inv = 1.f / l[qb];
+      bf16_t* O = (bf16_t*)a.g_o[0] + b * a.g_bstride[0] + rq * a.g_ld[0] + h * a.o_hstride;
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const int d = db * 16 + 4 * g;
+        if (d < 72)
+          *reinterpret_cast<u32x2*>(O + d) =
+              u32x2{pack2bf(o[db][qb][0] * inv, o[db][qb][1] * inv), pack2bf(o[db][qb][2] * inv, o[db][qb][3] * inv)};
+      }
+      if (g == 0 && a.lse) a.lse[u * FS_N + rq] = m[qb] * a.scale + __logf(l[qb]);
+    }
+    FS_BARRIER();  // this buffer's readers are done; the next unit's pieces landed in every wave
+    u = un;
+  }
+}
+
+// row fragment loads (Q / dO / O rows of one 16-row block) by inline asm; head dims 72..95 (g >= 1 at
+// ks 2) re-read dims 64..71 and are zeroed by the consumer
+__device__ __forceinline__ void fs_load_rows(bf16x8 (&f)[3], const bf16_t* row, int g) {
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+    const bf16_t* src = row + (ks < 2 || g == 0 ? ks * 32 + 8 * g : 64);
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(f[ks]) : "v"(src) : "memory");
+  }
+}
+
+// dQ with K / V resident (delta = rowsum(dO O) from flash_bwd_prep_kernel): wave w owns query rows 32w ..
+// 32w + 31; the next unit's Q / dO rows, lse and delta (inline-asm loads) and K / V images (LDS-DMA) are issued
+// before this unit's compute
+__global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash_args a, int G) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t units = a.Z * a.H;
+  int offk[FS_PER], offv[FS_PER];
+  fs_dma_offsets(a.ldk, wave, lane, offk);
+  fs_dma_offsets(a.ldv, wave, lane, offv);
+  const float sl2 = a.scale * FA_LOG2E;
+  int64_t u = fs_unit(a, G, 0);
+  bf16x8 qn[2][3], dn[2][3];
+  float ln[2], dln[2];
+  auto issue = [&](int64_t un, int t1) {
+    const int64_t bn = un / a.H, hn = un % a.H;
+    const bf16_t* Q = (const bf16_t*)a.q + bn * a.q_bstride + hn * a.q_hstride;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int64_t r = wave * 32 + qb * 16 + (lane & 15);
+      fs_load_rows(qn[qb], Q + r * a.ldq, g);
+      fs_load_rows(dn[qb], (const bf16_t*)a.g_do[0] + bn * a.g_bstride[0] + r * a.g_ld[0] + hn * a.o_hstride, g);
+      asm volatile("global_load_dword %0, %1, off" : "=v"(ln[qb]) : "v"(a.lse + un * FS_N + r) : "memory");
+      asm volatile("global_load_dword %0, %1, off" : "=v"(dln[qb]) : "v"(a.delta + un * FS_N + r) : "memory");
+    }
+    char* nxt = fa_smem + (t1 & 1) * 2 * FS_IMG;
+    fs_dma((const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride, offk, nxt, wave);
+    fs_dma((const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride, offv, nxt + FS_IMG, wave);
+  };
+  if (u < units) issue(u, 0);
+  FS_WAIT_VM(0);
+  FS_BARRIER();
+  for (int t = 0; u < units; ++t) {
+    const int64_t b = u / a.H, h = u % a.H;
+    bf16x8 qf[2][3], df[2][3];
+    float del[2], lse2[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        asm volatile("" : "+v"(qn[qb][ks]), "+v"(dn[qb][ks]));  // landed (vmcnt(0) + barrier)
+        qf[qb][ks] = qn[qb][ks];
+        df[qb][ks] = dn[qb][ks];
+      }
+      if (g != 0) qf[qb][2] = df[qb][2] = bf16x8{};
+      asm volatile("" : "+v"(ln[qb]), "+v"(dln[qb]));
+      lse2[qb] = ln[qb] * FA_LOG2E;
+      del[qb] = dln[qb];
+    }
+    const int64_t un = fs_unit(a, G, t + 1);
+    if (un < units) issue(un, t + 1);  // uniform
+    const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
+    const bf16_t* Kall = reinterpret_cast<const bf16_t*>(cur);
+    const bf16_t* Vall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
+    f32x4 dq[5][2];
+#pragma unroll
+    for (int db = 0; db < 5; ++db) dq[db][0] = dq[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kb = 0; kb < FS_N / FA_KB; ++kb) {
+      const bf16_t* Ks = Kall + kb * FA_KB * FS_ROW;
+      const bf16_t* Vs = Vall + kb * FA_KB * FS_ROW;
+      const unsigned ka = fs_lds_addr(Ks + (4 * g + ((lane & 15) >> 2)) * FS_ROW + 4 * (lane & 3));
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        f32x4 dsv[2][2];  // dS^T (without the scale) [16-key block of the k-step][query block]
+#pragma unroll
+        for (int i2 = 0; i2 < 2; ++i2) {
+          const int i = 2 * k2 + i2;
+          bf16x8 kfr[3], vfr[3];
+#pragma unroll
+          for (int ks = 0; ks < 3; ++ks) {
+            kfr[ks] = frag_row<FS_ROW>(Ks, i * 16, ks * 32, lane);
+            vfr[ks] = frag_row<FS_ROW>(Vs, i * 16, ks * 32, lane);
+          }
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb) {
+            f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 3; ++ks) {
+              sv = mfma(kfr[ks], qf[qb][ks], sv);
+              dp = mfma(vfr[ks], df[qb][ks], dp);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              dsv[i2][qb][e] = __builtin_amdgcn_exp2f(fmaf(sv[e], sl2, -lse2[qb])) * (dp[e] - del[qb]);
+          }
+        }
+        const bf16x8 sb0 = pack8(dsv[0][0], dsv[1][0]), sb1 = pack8(dsv[0][1], dsv[1][1]);
+        // dQ^T += K^T dS^T over these 32 keys: K^T fragments by inline-asm transposed reads (see the forward)
+        s16x4 tk[5][2];
+#define FS_TR(db, hf) tk[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(ka + k2 * 32 * FS_ROW * 2)
+        FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1); FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
+        FS_TR(4, 0); FS_TR(4, 1);
+#undef FS_TR
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(tk[0][0]), "+v"(tk[0][1]), "+v"(tk[1][0]), "+v"(tk[1][1]), "+v"(tk[2][0]), "+v"(tk[2][1]),
+                       "+v"(tk[3][0]), "+v"(tk[3][1]), "+v"(tk[4][0]), "+v"(tk[4][1]));
+#pragma unroll
+        for (int db = 0; db < 5; ++db) {
+          const bf16x8 kt = fs_cat(tk[db][0], tk[db][1]);
+          dq[db][0] = mfma(kt, sb0, dq[db][0]);
+          dq[db][1] = mfma(kt, sb1, dq[db][1]);
+        }
+      }
+    }
+    FS_WAIT_VM(0);  // the next unit's rows and images (issued before this unit's compute)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int64_t r = wave * 32 + qb * 16 + (lane & 15);
+      bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const int d = db * 16 + 4 * g;
+        if (d < 72)
+          *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][qb][0] * a.scale, dq[db][qb][1] * a.scale),
+                                                    pack2bf(dq[db][qb][2] * a.scale, dq[db][qb][3] * a.scale)};
+      }
+    }
+    FS_BARRIER();
+    u = un;
+  }
+}
+
+// dK, dV with Q and dO resident: wave w owns keys 32w .. 32w + 31 and sweeps the unit's query rows in steps of
+// 32.  Each Q / dO image row's tenth chunk carries lse / delta instead (rows 4j .. 4j + 3 of the row's group of
+// four, so a lane's four rows of a 16-row block come with ONE 16-B read); the head-dim-72..95 fragments that
+// would meet them are zeroed after the read.  The next unit's K / V fragments (inline-asm loads) and images
+// (LDS-DMA) are issued before this unit's compute.
+__global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flash_args a, int G) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int64_t units = a.Z * a.H;
+  int offq[FS_PER], offd[FS_PER], offl[FS_PER];
+  bool side[FS_PER];
+  {
+    const FaRow fr{&a};
+    (void)fr;
+#pragma unroll
+    for (int s2 = 0; s2 < FS_PER; ++s2) {
+      const int c = (wave * FS_PER + s2) * 64 + lane, row = c / 10, ch = c % 10;
+      side[s2] = ch == 9;
+      offq[s2] = row * (int)a.ldq + 8 * (ch < 9 ? ch : 0);
+      offd[s2] = row * (int)a.g_ld[0] + 8 * (ch < 9 ? ch : 0);
+      offl[s2] = row & ~3;
+    }
+  }
+  const float sl2 = a.scale * FA_LOG2E;
+  int64_t u = fs_unit(a, G, 0);
+  bf16x8 kfr[2][3], vfr[2][3];
+  // the wave's K / V fragments of unit un (inline-asm loads into kfr / vfr): issued in the last query step of
+  // the previous unit, right after the last products that read kfr / vfr
+  auto issue_kv = [&](int64_t un) {
+    const int64_t bn = un / a.H, hn = un % a.H;
+    const bf16_t* K = (const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride;
+    const bf16_t* V = (const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+      const int key = wave * 32 + kb2 * 16 + (lane & 15);
+      fs_load_rows(kfr[kb2], K + key * a.ldk, g);
+      fs_load_rows(vfr[kb2], V + key * a.ldv, g);
+    }
+  };
+  auto issue = [&](int64_t un, int t1) {  // the Q / dO (+ lse / delta) images of unit un into buffer t1 & 1
+    const int64_t bn = un / a.H, hn = un % a.H;
+    const bf16_t* Q = (const bf16_t*)a.q + bn * a.q_bstride + hn * a.q_hstride;
+    const bf16_t* dO = (const bf16_t*)a.g_do[0] + bn * a.g_bstride[0] + hn * a.o_hstride;
+    const float* L = a.lse + un * FS_N;
+    const float* D = a.delta + un * FS_N;
+    char* nxt = fa_smem + (t1 & 1) * 2 * FS_IMG;
+#pragma unroll
+    for (int s2 = 0; s2 < FS_PER; ++s2)
+      fs_glds16(side[s2] ? (const bf16_t*)(L + offl[s2]) : Q + offq[s2], nxt + (wave * FS_PER + s2) * 1024);
+#pragma unroll
+    for (int s2 = 0; s2 < FS_PER; ++s2)
+      fs_glds16(side[s2] ? (const bf16_t*)(D + offl[s2]) : dO + offd[s2], nxt + FS_IMG + (wave * FS_PER + s2) * 1024);
+  };
+  if (u < units) {
+    issue_kv(u);
+    issue(u, 0);
+  }
+  FS_WAIT_VM(0);
+  FS_BARRIER();
+  for (int t = 0; u < units; ++t) {
+    const int64_t b = u / a.H, h = u % a.H;
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) asm volatile("" : "+v"(kfr[kb2][ks]), "+v"(vfr[kb2][ks]));  // landed
+      if (g != 0) kfr[kb2][2] = vfr[kb2][2] = bf16x8{};
+    }
+    const int64_t un = fs_unit(a, G, t + 1);
+    if (un < units) issue(un, t + 1);  // uniform
+    const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
+    const bf16_t* Qall = reinterpret_cast<const bf16_t*>(cur);
+    const bf16_t* Dall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
+    f32x4 dk[5][2], dv[5][2];
+#pragma unroll
+    for (int db = 0; db < 5; ++db) dk[db][0] = dk[db][1] = dv[db][0] = dv[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto step = [&](int qs, bool last) {
+      const int r0 = qs * FA_QS;
+      const bf16_t* Qs = Qall + r0 * FS_ROW;
+      const bf16_t* Ds = Dall + r0 * FS_ROW;
+      unsigned pp[2][2][2], dd[2][2][2];  // bf16 pairs of P / dS [16-row query block][key block][pair]
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        // lse / delta of rows r0 + 16 i + 4g .. + 3 from the tenth chunk of row r0 + 16 i + 4g
+        const f32x4 l2r = *reinterpret_cast<const f32x4*>(Qs + (i * 16 + 4 * g) * FS_ROW + 72) * FA_LOG2E;
+        const f32x4 dlr = *reinterpret_cast<const f32x4*>(Ds + (i * 16 + 4 * g) * FS_ROW + 72);
+        bf16x8 qa[3], da[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks) {
+          qa[ks] = frag_row<FS_ROW>(Qs, i * 16, ks * 32, lane);
+          da[ks] = frag_row<FS_ROW>(Ds, i * 16, ks * 32, lane);
+        }
+        if (g != 0) qa[2] = da[2] = bf16x8{};  // dims 72..95: the lse / delta chunk and the next row
+#pragma unroll
+        for (int kb2 = 0; kb2 < 2; ++kb2) {
+          f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 3; ++ks) {
+            sv = mfma(qa[ks], kfr[kb2][ks], sv);
+            dp = mfma(da[ks], vfr[kb2][ks], dp);
+          }
+          float pe[4], de[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            pe[e] = __builtin_amdgcn_exp2f(fmaf(sv[e], sl2, -l2r[e]));
+            de[e] = pe[e] * (dp[e] - dlr[e]);  // dS without the scale (applied to dK once)
+          }
+          pp[i][kb2][0] = pack2bf(pe[0], pe[1]);
+          pp[i][kb2][1] = pack2bf(pe[2], pe[3]);
+          dd[i][kb2][0] = pack2bf(de[0], de[1]);
+          dd[i][kb2][1] = pack2bf(de[2], de[3]);
+        }
+      }
+      if (last && un < units) issue_kv(un);  // kfr / vfr are dead from here on in this unit
+      auto cat4 = [](unsigned x0, unsigned x1, unsigned x2, unsigned x3) {
+        return __builtin_bit_cast(bf16x8, u32x4{x0, x1, x2, x3});
+      };
+      const bf16x8 pb0 = cat4(pp[0][0][0], pp[0][0][1], pp[1][0][0], pp[1][0][1]);
+      const bf16x8 pb1 = cat4(pp[0][1][0], pp[0][1][1], pp[1][1][0], pp[1][1][1]);
+      const bf16x8 sb0 = cat4(dd[0][0][0], dd[0][0][1], dd[1][0][0], dd[1][0][1]);
+      const bf16x8 sb1 = cat4(dd[0][1][0], dd[0][1][1], dd[1][1][0], dd[1][1][1]);
+      // dV^T += dO^T P, dK^T += Q^T dS: dO^T / Q^T fragments by inline-asm transposed reads (see the forward)
+      const unsigned da0 = fs_lds_addr(Ds + (4 * g + ((lane & 15) >> 2)) * FS_ROW + 4 * (lane & 3));
+      const unsigned qa0 = fs_lds_addr(Qs + (4 * g + ((lane & 15) >> 2)) * FS_ROW + 4 * (lane & 3));
+      s16x4 td[5][2], tq[5][2];
+#define FS_TR(db, hf)                                             \
+  td[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(da0); \
+  tq[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(qa0)
+#define FS_MM(db)                                                                \
+  {                                                                              \
+    const bf16x8 dt = fs_cat(td[db][0], td[db][1]), qt = fs_cat(tq[db][0], tq[db][1]); \
+    dv[db][0] = mfma(dt, pb0, dv[db][0]);                                        \
+    dv[db][1] = mfma(dt, pb1, dv[db][1]);                                        \
+    dk[db][0] = mfma(qt, sb0, dk[db][0]);                                        \
+    dk[db][1] = mfma(qt, sb1, dk[db][1]);                                        \
+  }
+      FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1);
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(td[0][0]), "+v"(td[0][1]), "+v"(td[1][0]), "+v"(td[1][1]), "+v"(tq[0][0]), "+v"(tq[0][1]),
+                     "+v"(tq[1][0]), "+v"(tq[1][1]));
+      FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
+      FS_MM(0) FS_MM(1)
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(td[2][0]), "+v"(td[2][1]), "+v"(td[3][0]), "+v"(td[3][1]), "+v"(tq[2][0]), "+v"(tq[2][1]),
+                     "+v"(tq[3][0]), "+v"(tq[3][1]));
+      FS_TR(4, 0); FS_TR(4, 1);
+      FS_MM(2) FS_MM(3)
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(td[4][0]), "+v"(td[4][1]), "+v"(tq[4][0]), "+v"(tq[4][1]));
+      FS_MM(4)
+#undef FS_MM
+#undef FS_TR
+    };
+#pragma unroll 1
+    for (int qs = 0; qs < FS_N / FA_QS - 1; ++qs) step(qs, false);
+    step(FS_N / FA_QS - 1, true);
+    FS_WAIT_VM(0);  // the next unit's fragments and images (issued before this unit's compute)
+#pragma unroll
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+      const int key = wave * 32 + kb2 * 16 + (lane & 15);
+      bf16_t* dK = (bf16_t*)a.dk + b * a.k_bstride + h * a.k_hstride + (int64_t)key * a.ldk;
+      bf16_t* dV = (bf16_t*)a.dv + b * a.v_bstride + h * a.v_hstride + (int64_t)key * a.ldv;
+#pragma unroll
+      for (int db = 0; db < 5; ++db) {
+        const int d = db * 16 + 4 * g;
+        if (d < 72) {
+          *reinterpret_cast<u32x2*>(dK + d) = u32x2{pack2bf(dk[db][kb2][0] * a.scale, dk[db][kb2][1] * a.scale),
+                                                    pack2bf(dk[db][kb2][2] * a.scale, dk[db][kb2][3] * a.scale)};
+          *reinterpret_cast<u32x2*>(dV + d) =
+              u32x2{pack2bf(dv[db][kb2][0], dv[db][kb2][1]), pack2bf(dv[db][kb2][2], dv[db][kb2][3])};
+        }
+      }
+    }
+    FS_BARRIER();
+    u = un;
+  }
+}
+
 }  // namespace
 
 // head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
@@ -2116,6 +2643,29 @@ static bool fa_unit(const pz_flash_args* a) {
 // no mask, no soft-cap (SigLIP): the unit kernels' log2-domain element-wise fast path
 static bool fa_plain(const pz_flash_args* a) { return a->mask_mode == 0 && a->cap == 0.f; }
 
+// compute units of the current device (the persistent SigLIP grid: one workgroup per CU)
+static int fa_device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
+// the SigLIP training shape (256 x 256 keys, head 72, plain, one output group): the persistent pipelined
+// kernels; PZ_FLASH_SIG "0" keeps the one-workgroup-per-unit kernels (tests, A/B runs)
+static bool fa_sig(const pz_flash_args* a) {
+  const char* e = getenv("PZ_FLASH_SIG");
+  if (e && e[0] == '0') return false;
+  return fa_plain(a) && a->head_dim == 72 && a->nq == FS_N && a->nk == FS_N && a->n_groups == 1 &&
+         a->ldq * FS_N < (1 << 30) && a->ldk * FS_N < (1 << 30) && a->ldv * FS_N < (1 << 30) &&
+         a->g_ld[0] * FS_N < (1 << 30);
+}
+
 // Raise the kernel's dynamic-LDS limit once; a refusal is cleared here (the launch is checked on
 // its own) so it cannot surface as a later launch's error
 template <class Kern>
@@ -2160,8 +2710,13 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
   if (sp == 1 && fa_resident(a) && fa_unit(a)) {
     static bool attr = false;
     static bool attr2 = false;
+    static bool attr3 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
-    if (fa_plain(a)) {
+    if (fa_sig(a)) {
+      const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
+      fa_smem_attr(flash_fwd_sig_kernel, FS_SMEM, attr3);
+      hipLaunchKernelGGL(flash_fwd_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+    } else if (fa_plain(a)) {
       fa_smem_attr(flash_fwd_unit_kernel<72, true>, FR_SMEM_KQ, attr);
       hipLaunchKernelGGL((flash_fwd_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);
     } else {
@@ -2266,9 +2821,19 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
   dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
   if (fa_resident(a) && fa_unit(a)) {
-    static bool aq = false, akv = false, aq2 = false, akv2 = false;
+    static bool aq = false, akv = false, aq2 = false, akv2 = false, aq3 = false, akv3 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
-    if (fa_plain(a)) {
+    if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
+      const int64_t rows = a->Z * a->H * a->nq;
+      hipLaunchKernelGGL(flash_bwd_prep_kernel<72>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, *a);
+      PZ_CHECK_LAUNCH();
+      const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
+      fa_smem_attr(flash_bwd_q_sig_kernel, FS_SMEM, aq3);
+      fa_smem_attr(flash_bwd_kv_sig_kernel, FS_SMEM, akv3);
+      hipLaunchKernelGGL(flash_bwd_q_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+      PZ_CHECK_LAUNCH();
+      hipLaunchKernelGGL(flash_bwd_kv_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+    } else if (fa_plain(a)) {
       fa_smem_attr(flash_bwd_q_unit_kernel<72, true>, FR_SMEM_KQ, aq);
       fa_smem_attr(flash_bwd_kv_unit_kernel<72, true>, FU_SMEM_KV, akv);
       hipLaunchKernelGGL((flash_bwd_q_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);

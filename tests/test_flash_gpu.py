@@ -62,14 +62,17 @@ def ref_attention(q, k, v, scale, cap=0.0, allowed=None, dead=None):
     return p @ v, lse
 
 
-@pytest.mark.parametrize("unit", ["0", "1"])
-def test_flash_fwd_siglip(unit, monkeypatch):
-    """both SigLIP forward kernel families: 2 workgroups per unit (few units) and one (training)"""
+@pytest.mark.parametrize("unit,sig,B", [("0", "0", 3), ("1", "0", 3), ("1", "1", 3), ("1", "1", 40)])
+def test_flash_fwd_siglip(unit, sig, B, monkeypatch):
+    """the SigLIP forward kernel families: 2 workgroups per unit (few units), one workgroup per unit, and the
+    persistent pipelined kernel (B = 40: 640 units over the CUs, several units per workgroup with a ragged
+    last round, XCD-grouped unit order)"""
     from pizero_native import ops
 
     monkeypatch.setenv("PZ_FLASH_UNIT", unit)
+    monkeypatch.setenv("PZ_FLASH_SIG", sig)
 
-    B, nh, hd, N = 3, 16, 72, 256
+    nh, hd, N = 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
     O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
     lse = torch.empty(B * nh, N, device=dev)

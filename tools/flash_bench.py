@@ -78,13 +78,16 @@ def main():
     dqkv = torch.empty_like(qkv)
     sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
     fl = 4.0 * B * nh * N * N * hd
-    for unit in ("1",) if a.default_only else ("1", "0"):  # PZ_FLASH_UNIT: one workgroup per (image, head) unit vs the 2-/4-workgroup kernels
-        os.environ["PZ_FLASH_UNIT"] = unit
+    # PZ_FLASH_SIG / PZ_FLASH_UNIT: the persistent pipelined kernels (default), one workgroup per (image, head)
+    # unit, the 2-/4-workgroup resident kernels
+    for sig, unit in (("1", "1"),) if a.default_only else (("1", "1"), ("0", "1"), ("0", "0")):
+        os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig
         tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
         tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
-        print(f"siglip(unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms {2.5 * fl / tb / 1e9:.0f} TF/s",
-              flush=True)
+        print(f"siglip(sig={sig},unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
+              f"{2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
     os.environ.pop("PZ_FLASH_UNIT")
+    os.environ.pop("PZ_FLASH_SIG")
 
 
 if __name__ == "__main__":

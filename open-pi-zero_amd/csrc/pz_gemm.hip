@@ -1866,6 +1866,9 @@ bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
   if (!(e && e[0] == '1') &&
       !(a->M <= 320 && pl.bkc && !pl.geglu && a->K >= 4300 && ncols <= 2048))
     return false;
+#ifndef PZ_TALL_AB
+  if (!pl.bkc || pl.geglu) return false;  // only the plain k-contiguous form is built (pz_gemm_tall.hip)
+#endif
   if (!pl.akc || (!pl.bkc && pl.geglu) || a->batch != 1 || a->fp8_mode != 0 || a->norm_w || a->epilogue >= PZ_EPI_DGELU ||
       a->M <= 64 || a->M > 1024 || a->K % 8 != 0)
     return false;

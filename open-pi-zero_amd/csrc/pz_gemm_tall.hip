@@ -282,8 +282,14 @@ static int launch_tall_k(const GemmP& p, int splits, hipStream_t st) {
 
 // plain: 64-column tiles, 64-deep K-tiles in a 3-slot ring; GeGLU: 64 output columns (128 B rows), 32-deep
 // K-tiles in a 4-slot ring.  mi = 4 (256-row tiles) or 5 (320-row tiles).
+// Only the plain k-contiguous form is planned by default; the GeGLU and k-strided-B (NN dgrad) forms measured
+// slower on every Pi0 shape (profiles/r04/tall_bench.log) and are compiled only with -DPZ_TALL_AB (A/B builds).
 int pz_tall_launch(const GemmP& p, int mi, bool geglu, bool bkc, int splits, hipStream_t st) {
+#ifdef PZ_TALL_AB
   if (!bkc) return mi == 4 ? launch_tall_k<4, 2, 64, 3, false, false>(p, splits, st) : launch_tall_k<5, 2, 64, 3, false, false>(p, splits, st);
   if (geglu) return mi == 4 ? launch_tall_k<4, 4, 32, 4, true>(p, splits, st) : launch_tall_k<5, 4, 32, 4, true>(p, splits, st);
+#else
+  if (!bkc || geglu) return PZ_ERR_UNSUPPORTED;  // not planned (plan_tall)
+#endif
   return mi == 4 ? launch_tall_k<4, 2, 64, 3, false>(p, splits, st) : launch_tall_k<5, 2, 64, 3, false>(p, splits, st);
 }

@@ -14,6 +14,10 @@ LIB_PATH = os.path.join(_HERE, "libpizero_hip.so")
 # A/B runs only (tools/): another in-tree build of the same ABI, e.g. a baseline of a kernel change
 if os.environ.get("PZ_LIB_PATH"):
     LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ["PZ_LIB_PATH"]))
+    import sys as _sys
+
+    print(f"[pizero_native] PZ_LIB_PATH override: loading {LIB_PATH} instead of the default libpizero_hip.so",
+          file=_sys.stderr, flush=True)
 
 ABI_VERSION = 16  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3

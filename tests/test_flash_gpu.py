@@ -252,13 +252,14 @@ def _grads(q, k, v, dO, scale, cap=0.0, allowed=None, dead=None):
     return q.grad, k.grad, v.grad
 
 
-@pytest.mark.parametrize("unit", ["0", "1"])
-def test_flash_bwd_siglip(unit, monkeypatch):
+@pytest.mark.parametrize("unit,sig,B", [("0", "0", 2), ("1", "0", 2), ("1", "1", 2), ("1", "1", 40)])
+def test_flash_bwd_siglip(unit, sig, B, monkeypatch):
     from pizero_native import ops
 
     monkeypatch.setenv("PZ_FLASH_UNIT", unit)
+    monkeypatch.setenv("PZ_FLASH_SIG", sig)
 
-    B, nh, hd, N = 2, 16, 72, 256
+    nh, hd, N = 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
     O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
     lse = torch.empty(B * nh, N, device=dev)

@@ -21,6 +21,8 @@
 // query-parallel pass (no atomics: deterministic).
 #include "pz_common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int FA_KB = 64;   // keys per staged block (forward, dQ) / per dK-dV workgroup
@@ -2598,6 +2600,242 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
   }
 }
 
+// ---- joint forward with the softmax exported: LDS-DMA key / value ring (training default) -----------------------
+// flash_fwd_probs_kernel's math and contract (P, tanh(cap), O) with the staging and the element-wise work rebuilt
+// after its PMC (profiles/r05/pmc_attn_*.json: waves parked 45 % of their cycles, 11 vector instructions per
+// MFMA, most of them the register staging's address arithmetic / LDS stores and per-score mask selects):
+//   * the 5 K blocks then the 5 V blocks of 64 keys stream by LDS-DMA into a 4-slot ring of 32 KiB images,
+//     three blocks ahead (stage s in slot s % 4; s + 3 issued once every wave has passed stage s's barrier);
+//     512-B rows XOR-swizzled through the global source address: K chunk c of row r at c ^ (r & 15) (16-row
+//     ds_read_b128 fragments conflict-free), V chunk c at c ^ 2 (r & 7) (4-row transposed reads conflict-free);
+//   * key blocks wholly below the valid prefix (every key allowed for every row) in a wave without dead / past-
+//     the-end rows skip the mask and the dead-row selects;
+//   * Q fragments and the V^T fragments by inline-asm loads (hipcc would drain the in-flight DMA before the first
+//     use of an ordinary global load or a transposed-read builtin).
+// Keys past nk read the last key row (finite) and are masked; the schedule always runs 5 + 5 stages (nk <= 320).
+constexpr int JD_SLOT = 64 * 512, JD_SMEM = 4 * JD_SLOT;
+
+struct JdDma {  // this lane's part of the wave's 4 LDS-DMA instructions of a 64-key block image
+  int row[4], coff[4];
+  __device__ __forceinline__ JdDma(int wave, int lane, bool trs) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int r = 2 * (wave * 4 + s) + (lane >> 5), pch = lane & 31;
+      row[s] = r;
+      coff[s] = 8 * (pch ^ (trs ? 2 * (r & 7) : (r & 15)));
+    }
+  }
+  __device__ __forceinline__ void issue(const bf16_t* X, int64_t ld, int kb, int nk, char* slot, int wave) const {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      int key = kb * 64 + row[s];
+      key = key < nk ? key : nk - 1;
+      fs_glds16(X + (int64_t)key * ld + coff[s], slot + (wave * 4 + s) * 1024);
+    }
+  }
+};
+
+// O^T += V^T P^T for head-dim blocks 4 DG .. 4 DG + 3 over the 32 keys of k-step K2: 8 transposed reads, one
+// wait naming them, 4 MFMAs
+template <int K2, int DG>
+__device__ __forceinline__ void jd_pv_group(f32x4 (&o)[16], const unsigned (&vs)[8], const bf16x8& pk) {
+  s16x4 tv[4][2];
+#define JD_TR(u, hf) tv[u][hf] = fs_tr<(K2 * 32 + 16 * (hf)) * 512 + ((DG * 4 + (u)) & 8) * 32>(vs[(DG * 4 + (u)) & 7])
+  JD_TR(0, 0); JD_TR(0, 1); JD_TR(1, 0); JD_TR(1, 1); JD_TR(2, 0); JD_TR(2, 1); JD_TR(3, 0); JD_TR(3, 1);
+#undef JD_TR
+  asm volatile("s_waitcnt lgkmcnt(0)"
+               : "+v"(tv[0][0]), "+v"(tv[0][1]), "+v"(tv[1][0]), "+v"(tv[1][1]), "+v"(tv[2][0]), "+v"(tv[2][1]),
+                 "+v"(tv[3][0]), "+v"(tv[3][1]));
+#pragma unroll
+  for (int u = 0; u < 4; ++u) o[DG * 4 + u] = mfma(fs_cat(tv[u][0], tv[u][1]), pk, o[DG * 4 + u]);
+}
+
+template <bool CAP>
+__global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_flash_args a, bf16_t* P, bf16_t* TC,
+                                                                         int64_t ldp) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  constexpr int RPW = JP_NW * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l15 = lane & 15;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)qblk * RPW + wave * 16 + l15;  // this lane's query row
+  const bool live = r < a.nq;
+  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
+  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const FaMask mk(a, b);
+  const FaFast ff(a);
+  const int nk = (int)a.nk;
+  const JdDma dmk(wave, lane, false), dmv(wave, lane, true);
+  bf16x8 qf[8];
+  {
+    const bf16_t* qrow = Q + (live ? r : 0) * a.ldq + 8 * g;
+#define JD_QLD(ks) asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(qf[ks]) : "v"(qrow), "i"((ks) * 64) : "memory")
+    JD_QLD(0); JD_QLD(1); JD_QLD(2); JD_QLD(3); JD_QLD(4); JD_QLD(5); JD_QLD(6); JD_QLD(7);
+#undef JD_QLD
+  }
+  auto issue = [&](int s) {  // stage s: K block s (s < 5) or V block s - 5, into slot s % 4
+    char* slot = fa_smem + (s % 4) * JD_SLOT;
+    if (s < 5) dmk.issue(K, a.ldk, s, nk, slot, wave);
+    else dmv.issue(V, a.ldv, s - 5, nk, slot, wave);
+  };
+  issue(0);
+  issue(1);
+  issue(2);
+  const int t = mk.token((int)r);
+  const bool dead = mk.dead(t);
+  const int rb = fa_row_bits(mk, t), full_keys = fa_full_keys(mk);
+  const bool clean = __ballot(dead || !live) == 0ull;  // wave-uniform
+  // pass 1: S^T[key][q] for every key of the row block (stage kb = K block kb)
+  f32x4 sc[JP_MAXKB][4];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    FS_WAIT_VM(8);  // stage kb landed (stages kb + 1, kb + 2 in flight; the Q loads precede stage 0)
+    FS_BARRIER();
+    if (kb == 0)
+      asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4]), "+v"(qf[5]), "+v"(qf[6]),
+                   "+v"(qf[7]));
+    issue(kb + 3);
+    const char* slot = fa_smem + (kb % 4) * JD_SLOT + l15 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const char* kp = slot + 16 * ((4 * ks + g) ^ l15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[kb][i] = mfma(*reinterpret_cast<const bf16x8*>(kp + i * 8192), qf[ks], sc[kb][i]);
+    }
+  }
+  FS_WAIT_VM(4);  // V blocks 0, 1 (stages 5, 6) landed by this wave; stage 7 in flight
+  // logits (log2 domain) + the tanh(cap) export; keys past nk / masked -> -inf
+  bf16_t* prow = P + (b * a.nq + (live ? r : 0)) * ldp;
+  bf16_t* trow = TC ? TC + (b * a.nq + (live ? r : 0)) * ldp : nullptr;
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    // uniform per block: every key allowed and every row live (no mask, no dead-row selects, no store guards)
+    auto logits = [&](auto FAST) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float tv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float sv = sc[kb][i][e];
+          float th = 0.f, x2;
+          if constexpr (CAP) {
+            th = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(sv * ff.k2) + 1.f), 1.f);
+            x2 = th * ff.crow_live;
+          } else {
+            x2 = sv * ff.crow_live;
+          }
+          if constexpr (!decltype(FAST)::value) {
+            const int j = kb * FA_KB + i * 16 + 4 * g + e;
+            const bool ok = j < nk && (j < full_keys || ((rb >> fa_key_class(mk, j)) & 1));
+            x2 = ok ? x2 : -INFINITY;
+            th = (dead || j >= nk) ? 0.f : th;
+          }
+          sc[kb][i][e] = x2;
+          mx = fmaxf(mx, x2);
+          tv[e] = th;
+        }
+        const int j0 = kb * FA_KB + i * 16 + 4 * g;
+        if (trow && (decltype(FAST)::value || (live && j0 < ldp)))
+          *reinterpret_cast<u32x2*>(trow + j0) = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
+      }
+    };
+    if (clean && (kb + 1) * 64 <= full_keys) logits(std::true_type{});
+    else logits(std::false_type{});
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pv = __builtin_amdgcn_exp2f(sc[kb][i][e] - mx);  // exp2(-inf) = 0
+        sc[kb][i][e] = pv;
+        sum += pv;
+      }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  // fully masked (dead) rows: uniform over the N keys (the finfo.min mask absorbs the logits)
+  const float inv = 1.f / sum, uni = 1.f / (float)nk;
+  bf16x8 pf[JP_MAXKB][2];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    unsigned pk[4][2];
+    auto probs = [&](auto FAST) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (decltype(FAST)::value) {
+          pk[i][0] = pack2bf(sc[kb][i][0] * inv, sc[kb][i][1] * inv);
+          pk[i][1] = pack2bf(sc[kb][i][2] * inv, sc[kb][i][3] * inv);
+        } else {
+          float pv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = kb * FA_KB + i * 16 + 4 * g + e;
+            pv[e] = dead ? (j < nk ? uni : 0.f) : sc[kb][i][e] * inv;
+          }
+          pk[i][0] = pack2bf(pv[0], pv[1]);
+          pk[i][1] = pack2bf(pv[2], pv[3]);
+        }
+        const int j0 = kb * FA_KB + i * 16 + 4 * g;
+        if (decltype(FAST)::value || (live && j0 < ldp)) *reinterpret_cast<u32x2*>(prow + j0) = u32x2{pk[i][0], pk[i][1]};
+      }
+    };
+    if (clean && (kb + 1) * 64 <= full_keys) probs(std::true_type{});
+    else probs(std::false_type{});
+    pf[kb][0] = __builtin_bit_cast(bf16x8, u32x4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+    pf[kb][1] = __builtin_bit_cast(bf16x8, u32x4{pk[2][0], pk[2][1], pk[3][0], pk[3][1]});
+  }
+  // pass 2: O^T[d][q] = V^T[d][key] P^T[key][q] with the bf16 P (stage 5 + kb = V block kb)
+  f32x4 o[16];
+#pragma unroll
+  for (int db = 0; db < 16; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // V^T fragment of (k2, db): rows k2*32 + 16 hf + 4g + q, 8-B piece p of head dims 16 db .. : swizzled chunk
+  // (2 db + (p >> 1)) ^ 2 (r & 7) = 2 (db ^ w) + (p >> 1) with w = 4 (g & 1) + q
+  const int q4 = l15 >> 2, p4 = lane & 3, w = 4 * (g & 1) + q4;
+  unsigned va[8];
+#pragma unroll
+  for (int d7 = 0; d7 < 8; ++d7) va[d7] = fs_lds_addr(fa_smem + (4 * g + q4) * 512 + 32 * (d7 ^ w) + 8 * p4);
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    const int s = 5 + kb;
+    if (s == 7) FS_WAIT_VM(8);  // (this wave's stages 5, 6 were waited before the softmax)
+    if (s == 8) FS_WAIT_VM(4);
+    if (s == 9) FS_WAIT_VM(0);
+    FS_BARRIER();
+    if (s + 3 <= 9) issue(s + 3);
+    const unsigned sb = (unsigned)((s % 4) * JD_SLOT);
+    unsigned vs[8];
+#pragma unroll
+    for (int d7 = 0; d7 < 8; ++d7) vs[d7] = va[d7] + sb;
+    jd_pv_group<0, 0>(o, vs, pf[kb][0]);
+    jd_pv_group<0, 1>(o, vs, pf[kb][0]);
+    jd_pv_group<0, 2>(o, vs, pf[kb][0]);
+    jd_pv_group<0, 3>(o, vs, pf[kb][0]);
+    jd_pv_group<1, 0>(o, vs, pf[kb][1]);
+    jd_pv_group<1, 1>(o, vs, pf[kb][1]);
+    jd_pv_group<1, 2>(o, vs, pf[kb][1]);
+    jd_pv_group<1, 3>(o, vs, pf[kb][1]);
+  }
+  if (!live) return;
+  const FaRow fr{&a};
+  const int gi = fr.grp(r);
+  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
+#pragma unroll
+  for (int db = 0; db < 16; ++db) {
+    const int d = db * 16 + 4 * g;
+    *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(o[db][0], o[db][1]), pack2bf(o[db][2], o[db][3])};
+  }
+}
+
 }  // namespace
 
 // head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
@@ -2762,6 +3000,21 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
                "flash_fwd_probs: operands need 16-byte aligned rows");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z * a->H < 65536, "flash_fwd_probs: nq / units too large");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
+  const char* e = getenv("PZ_PROBS_DMA");  // "0": the register-staged kernel (A/B runs)
+  if (!(e && e[0] == '0')) {
+    static bool attr0 = false, attr1 = false;
+    if (a->cap > 0.f) {
+      fa_smem_attr(flash_fwd_probs_dma_kernel<true>, JD_SMEM, attr1);
+      hipLaunchKernelGGL(flash_fwd_probs_dma_kernel<true>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
+                         (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
+    } else {
+      fa_smem_attr(flash_fwd_probs_dma_kernel<false>, JD_SMEM, attr0);
+      hipLaunchKernelGGL(flash_fwd_probs_dma_kernel<false>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
+                         (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
+    }
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
                      (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
   PZ_CHECK_LAUNCH();

@@ -2615,22 +2615,21 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
 // Keys past nk read the last key row (finite) and are masked; the schedule always runs 5 + 5 stages (nk <= 320).
 constexpr int JD_SLOT = 64 * 512, JD_SMEM = 4 * JD_SLOT;
 
-struct JdDma {  // this lane's part of the wave's 4 LDS-DMA instructions of a 64-key block image
-  int row[4], coff[4];
-  __device__ __forceinline__ JdDma(int wave, int lane, bool trs) {
+struct JdDma {  // this lane's part of the wave's 4 LDS-DMA instructions of a 64-key block image (recomputed per
+               // issue: a few vector instructions instead of 8 live registers)
+  int wave, lane;
+  bool trs;
+  __device__ __forceinline__ JdDma(int wave_, int lane_, bool trs_) : wave(wave_), lane(lane_), trs(trs_) {}
+  __device__ __forceinline__ void issue(const bf16_t* X, int64_t ld, int kb, int nk, char* slot, int) const {
+    int ln = lane;
+    asm volatile("" : "+v"(ln));  // keeps hipcc from hoisting every stage's 64-bit addresses (80 live VGPRs)
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const int r = 2 * (wave * 4 + s) + (lane >> 5), pch = lane & 31;
-      row[s] = r;
-      coff[s] = 8 * (pch ^ (trs ? 2 * (r & 7) : (r & 15)));
-    }
-  }
-  __device__ __forceinline__ void issue(const bf16_t* X, int64_t ld, int kb, int nk, char* slot, int wave) const {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      int key = kb * 64 + row[s];
+      const int r = 2 * (wave * 4 + s) + (ln >> 5), pch = ln & 31;
+      const int coff = 8 * (pch ^ (trs ? 2 * (r & 7) : (r & 15)));
+      int key = kb * 64 + r;
       key = key < nk ? key : nk - 1;
-      fs_glds16(X + (int64_t)key * ld + coff[s], slot + (wave * 4 + s) * 1024);
+      fs_glds16(X + (int64_t)key * ld + coff, slot + (wave * 4 + s) * 1024);
     }
   }
 };
@@ -2833,6 +2832,185 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_f
   for (int db = 0; db < 16; ++db) {
     const int d = db * 16 + 4 * g;
     *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(o[db][0], o[db][1]), pack2bf(o[db][2], o[db][3])};
+  }
+}
+
+// ---- joint backward dS (+ dQ) from the exported softmax: LDS-DMA value / key ring -----------------------------
+// flash_bwd_ds_kernel's math and contract with flash_fwd_probs_dma_kernel's staging: stages 0..4 = V blocks
+// (16-row fragments: K-style swizzle), 5..9 = K blocks (transposed fragments) in the 4-slot ring, three ahead;
+// the P / tanh(cap) rows (inline-asm loads) are issued with the last V block so they land under its MFMAs.
+// Without dQ the K stages still stream (from V: every wave's DMA count stays what the counted waits assume).
+__global__ void __launch_bounds__(JP_NW * 64, 1) flash_bwd_ds_dma_kernel(pz_flash_args a, const bf16_t* P,
+                                                                      const bf16_t* TC, bf16_t* dS, int64_t ldp) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  constexpr int RPW = JP_NW * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, l15 = lane & 15;
+  int64_t zh;
+  int qblk;
+  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
+  const int64_t b = zh / a.H, h = zh % a.H;
+  const int64_t r = (int64_t)qblk * RPW + wave * 16 + l15;
+  const bool live = r < a.nq;
+  const bool want_dq = a.dq != nullptr;
+  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
+  const bf16_t* K = want_dq ? (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride : V;
+  const int64_t ldk = want_dq ? a.ldk : a.ldv;
+  const int nk = (int)a.nk;
+  const JdDma dmv(wave, lane, false), dmk(wave, lane, true);
+  auto issue = [&](int s) {  // stage s: V block s (s < 5) or K block s - 5, into slot s % 4
+    char* slot = fa_smem + (s % 4) * JD_SLOT;
+    if (s < 5) dmv.issue(V, a.ldv, s, nk, slot, wave);
+    else dmk.issue(K, ldk, s - 5, nk, slot, wave);
+  };
+  // dO fragments (a mixture without dO contributes dP = 0)
+  bf16x8 df[8];
+  bool has_do;
+  {
+    const FaRow fr{&a};
+    const int gi = live ? fr.grp(r) : 0;
+    has_do = live && a.g_do[gi];
+    const bf16_t* dOr = has_do ? (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi) + 8 * g : V;
+#define JD_DLD(ks) asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(df[ks]) : "v"(dOr), "i"((ks) * 64) : "memory")
+    JD_DLD(0); JD_DLD(1); JD_DLD(2); JD_DLD(3); JD_DLD(4); JD_DLD(5); JD_DLD(6); JD_DLD(7);
+#undef JD_DLD
+  }
+  issue(0);
+  issue(1);
+  issue(2);
+  const bf16_t* prow = P + (b * a.nq + (live ? r : 0)) * ldp;
+  const bf16_t* trow = TC ? TC + (b * a.nq + (live ? r : 0)) * ldp : prow;
+  const bool clean = __ballot(!live) == 0ull;
+  // pass 1 (stage kb = V block kb): dP^T[key][q] = V dO^T
+  f32x4 dp[JP_MAXKB][4];
+  u32x2 pw[JP_MAXKB][4], tw[JP_MAXKB][4];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    FS_WAIT_VM(8);
+    FS_BARRIER();
+    if (kb == 0) {
+      asm volatile("" : "+v"(df[0]), "+v"(df[1]), "+v"(df[2]), "+v"(df[3]), "+v"(df[4]), "+v"(df[5]), "+v"(df[6]),
+                   "+v"(df[7]));
+      if (!has_do) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) df[ks] = bf16x8{};
+      }
+    }
+    issue(kb + 3);
+    const char* slot = fa_smem + (kb % 4) * JD_SLOT + l15 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dp[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const char* vp = slot + 16 * ((4 * ks + g) ^ l15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dp[kb][i] = mfma(*reinterpret_cast<const bf16x8*>(vp + i * 8192), df[ks], dp[kb][i]);
+    }
+  }
+  // this row's P and tanh(cap) (issued once dO's fragments are dead; the tanh(cap) latency runs under the P . dP
+  // row sum; columns past ldp are never read).  The opaque lane index keeps hipcc from computing the 40 addresses
+  // up front.
+  int gl = g;
+  asm volatile("" : "+v"(gl));
+#pragma unroll
+  for (int k2 = 0; k2 < JP_MAXKB; ++k2)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = k2 * FA_KB + i * 16 + 4 * gl;
+      const int jc = j0 < ldp ? j0 : 0;
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(pw[k2][i]) : "v"(prow + jc) : "memory");
+    }
+#pragma unroll
+  for (int k2 = 0; k2 < JP_MAXKB; ++k2)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = k2 * FA_KB + i * 16 + 4 * gl;
+      const int jc = j0 < ldp ? j0 : 0;
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(tw[k2][i]) : "v"(trow + jc) : "memory");
+    }
+  FS_WAIT_VM(20);  // P rows and K blocks 0..2 (stages 5..7) landed; the 20 tanh(cap) loads in flight
+  // dS = P (dP - delta) scale (1 - tc^2) for the row (kept in dp as fp32; stored in bf16)
+  bf16_t* orow = dS + (b * a.nq + (live ? r : 0)) * ldp;
+  const bool cap = a.cap > 0.f;
+  float dot = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      asm volatile("" : "+v"(pw[kb][i]));
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      if (!(live && j0 < nk)) pw[kb][i] = u32x2{0u, 0u};  // P = 0 past N (and for rows past nq)
+      const float p0 = __uint_as_float(pw[kb][i][0] << 16), p1 = __uint_as_float(pw[kb][i][0] & 0xffff0000u);
+      const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
+      dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
+    }
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  FS_WAIT_VM(0);
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(tw[kb][i]));
+  bf16x8 dsf[JP_MAXKB][2];
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    unsigned pk[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j0 = kb * FA_KB + i * 16 + 4 * g;
+      const u32x2 tv2 = (cap && live && j0 < nk) ? tw[kb][i] : u32x2{0u, 0u};
+      const float pv[4] = {__uint_as_float(pw[kb][i][0] << 16), __uint_as_float(pw[kb][i][0] & 0xffff0000u),
+                           __uint_as_float(pw[kb][i][1] << 16), __uint_as_float(pw[kb][i][1] & 0xffff0000u)};
+      const float tv[4] = {__uint_as_float(tv2[0] << 16), __uint_as_float(tv2[0] & 0xffff0000u),
+                           __uint_as_float(tv2[1] << 16), __uint_as_float(tv2[1] & 0xffff0000u)};
+      float x[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // pv = 0 past N: x = 0 there
+        x[e] = pv[e] * (dp[kb][i][e] - dot) * a.scale;
+        if (cap) x[e] *= fmaf(-tv[e], tv[e], 1.f);
+      }
+      pk[i][0] = pack2bf(x[0], x[1]);
+      pk[i][1] = pack2bf(x[2], x[3]);
+      if (clean ? j0 < ldp : (live && j0 < ldp)) *reinterpret_cast<u32x2*>(orow + j0) = u32x2{pk[i][0], pk[i][1]};
+    }
+    dsf[kb][0] = __builtin_bit_cast(bf16x8, u32x4{pk[0][0], pk[0][1], pk[1][0], pk[1][1]});
+    dsf[kb][1] = __builtin_bit_cast(bf16x8, u32x4{pk[2][0], pk[2][1], pk[3][0], pk[3][1]});
+  }
+  // pass 2 (stage 5 + kb = K block kb): dQ^T[d][q] = K^T[d][key] dS^T[key][q] with the bf16 dS
+  f32x4 dq[16];
+#pragma unroll
+  for (int db = 0; db < 16; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int q4 = l15 >> 2, p4 = lane & 3, w = 4 * (g & 1) + q4;
+  unsigned ka[8];
+#pragma unroll
+  for (int d7 = 0; d7 < 8; ++d7) ka[d7] = fs_lds_addr(fa_smem + (4 * g + q4) * 512 + 32 * (d7 ^ w) + 8 * p4);
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    const int s = 5 + kb;
+    if (s == 8) FS_WAIT_VM(4);  // (stages 5..7 were waited before the dS phase; its stores precede stage 8)
+    if (s == 9) FS_WAIT_VM(0);
+    FS_BARRIER();
+    if (s + 3 <= 9) issue(s + 3);
+    if (want_dq) {  // uniform
+      const unsigned sb = (unsigned)((s % 4) * JD_SLOT);
+      unsigned ks_[8];
+#pragma unroll
+      for (int d7 = 0; d7 < 8; ++d7) ks_[d7] = ka[d7] + sb;
+      jd_pv_group<0, 0>(dq, ks_, dsf[kb][0]);
+      jd_pv_group<0, 1>(dq, ks_, dsf[kb][0]);
+      jd_pv_group<0, 2>(dq, ks_, dsf[kb][0]);
+      jd_pv_group<0, 3>(dq, ks_, dsf[kb][0]);
+      jd_pv_group<1, 0>(dq, ks_, dsf[kb][1]);
+      jd_pv_group<1, 1>(dq, ks_, dsf[kb][1]);
+      jd_pv_group<1, 2>(dq, ks_, dsf[kb][1]);
+      jd_pv_group<1, 3>(dq, ks_, dsf[kb][1]);
+    }
+  }
+  if (!live || !want_dq) return;
+  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
+#pragma unroll
+  for (int db = 0; db < 16; ++db) {
+    const int d = db * 16 + 4 * g;
+    *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
   }
 }
 
@@ -3039,6 +3217,15 @@ extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void
                  "flash_bwd_ds: dQ needs K (16-byte rows) and an 8-byte aligned dQ");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_bwd_ds: too many units");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
+  const char* e = getenv("PZ_PROBS_DMA");  // "0": the register-staged kernel (A/B runs)
+  if (!(e && e[0] == '0')) {
+    static bool attr = false;
+    fa_smem_attr(flash_bwd_ds_dma_kernel, JD_SMEM, attr);
+    hipLaunchKernelGGL(flash_bwd_ds_dma_kernel, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
+                       (hipStream_t)stream, *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
   hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0, (hipStream_t)stream,
                      *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
   PZ_CHECK_LAUNCH();

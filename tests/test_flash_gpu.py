@@ -115,12 +115,15 @@ def test_flash_fwd_joint_block_mask(cnt, key_split):
     close(lse.view(B, L, nh), rlse.permute(0, 2, 1), rtol=1e-3, atol=2e-3)
 
 
+@pytest.mark.parametrize("dma", ["1", "0"])
 @pytest.mark.parametrize("cnt", [[276, 276, 276], [276, 250, 9]])
-def test_flash_fwd_probs_joint_block_mask(cnt):
+def test_flash_fwd_probs_joint_block_mask(cnt, dma, monkeypatch):
     """pz_flash_fwd_probs (training-default joint forward): O, and the exported bf16 softmax P and
     tanh(cap) with pz_attn_softmax's conventions (dead rows uniform over L keys with tcap 0, zeros in
-    the L..Lp pad columns), against torch fp32"""
+    the L..Lp pad columns), against torch fp32; both the LDS-DMA ring kernel (default) and the register-staged one"""
     from pizero_native import ops
+
+    monkeypatch.setenv("PZ_PROBS_DMA", dma)
 
     B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
     L = P + C + Hc

@@ -57,8 +57,12 @@ def main():
     fl = 4.0 * B * L * nh * L * hd
     Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
     tcm = torch.empty_like(Pm)
-    tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
-    print(f"joint  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)", flush=True)
+    for dma in ("1",) if a.default_only else ("1", "0"):  # PZ_PROBS_DMA: LDS-DMA ring (default) vs register staging
+        os.environ["PZ_PROBS_DMA"] = dma
+        tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
+        print(f"joint  fwd+probs(dma={dma}) {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)",
+              flush=True)
+    os.environ.pop("PZ_PROBS_DMA")
     dSm = torch.empty_like(Pm)
     td = timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters)
     print(f"joint  bwd dS {td:.3f} ms (dP = dO V^T in registers + softmax backward from P / tanh(cap))", flush=True)

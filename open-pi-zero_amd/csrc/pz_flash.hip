@@ -2301,6 +2301,32 @@ __device__ __forceinline__ void fs_load_rows(bf16x8 (&f)[3], const bf16_t* row, 
   }
 }
 
+// delta[zh][r] = sum_d dO[r][d] O[r][d] for the SigLIP shape (head 72, one output group): one thread per (token,
+// head), the 16 heads of a token row on 16 adjacent lanes (their 144-B segments tile the row), 9 + 9 16-B loads
+__global__ void __launch_bounds__(256) flash_delta72_kernel(pz_flash_args a) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= a.Z * a.nq * a.H) return;
+  const int64_t h = t % a.H, br = t / a.H, r = br % a.nq, b = br / a.nq;
+  const int64_t off = b * a.g_bstride[0] + r * a.g_ld[0] + h * a.o_hstride;
+  const u32x4* O = reinterpret_cast<const u32x4*>((const bf16_t*)a.g_o[0] + off);
+  const u32x4* dO = reinterpret_cast<const u32x4*>((const bf16_t*)a.g_do[0] + off);
+  u32x4 x[9], y[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    x[i] = O[i];
+    y[i] = dO[i];
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      acc = fmaf(__uint_as_float(x[i][e] << 16), __uint_as_float(y[i][e] << 16), acc);
+      acc = fmaf(__uint_as_float(x[i][e] & 0xffff0000u), __uint_as_float(y[i][e] & 0xffff0000u), acc);
+    }
+  a.delta[(b * a.H + h) * a.nq + r] = acc;
+}
+
 // dQ with K / V resident (delta = rowsum(dO O) from flash_bwd_prep_kernel): wave w owns query rows 32w ..
 // 32w + 31; the next unit's Q / dO rows, lse and delta (inline-asm loads) and K / V images (LDS-DMA) are issued
 // before this unit's compute
@@ -3078,6 +3104,7 @@ static bool fa_sig(const pz_flash_args* a) {
   const char* e = getenv("PZ_FLASH_SIG");
   if (e && e[0] == '0') return false;
   return fa_plain(a) && a->head_dim == 72 && a->nq == FS_N && a->nk == FS_N && a->n_groups == 1 &&
+         a->o_hstride % 8 == 0 && a->g_ld[0] % 8 == 0 && a->g_bstride[0] % 8 == 0 &&
          a->ldq * FS_N < (1 << 30) && a->ldk * FS_N < (1 << 30) && a->ldv * FS_N < (1 << 30) &&
          a->g_ld[0] * FS_N < (1 << 30);
 }
@@ -3265,7 +3292,7 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
       const int64_t rows = a->Z * a->H * a->nq;
-      hipLaunchKernelGGL(flash_bwd_prep_kernel<72>, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, *a);
+      hipLaunchKernelGGL(flash_delta72_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, *a);
       PZ_CHECK_LAUNCH();
       const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
       fa_smem_attr(flash_bwd_q_sig_kernel, FS_SMEM, aq3);

@@ -95,6 +95,10 @@ PY
     pmcdgeglu)  # the same counter passes on the DGEGLU dgrad (down-proj dgrad + GeGLU derivative, micro-batch 256)
       PMC_CMD="python3 tools/gemm_one.py --layout DGEGLU --M 70656 --N 2048 --K 16384 --iters 3" \
         bash tools/pmc_dominant.sh "$OUT/pmcd" ;;
+    flashprof)  # per-kernel times of the attention microbenchmark (every variant)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/flashprof" -o flash \
+        -- python3 tools/flash_bench.py --iters 5 > "$OUT/flashprof.log" 2>&1
+      rm -f "$OUT"/flashprof/*kernel_trace.csv "$OUT"/flashprof/*/*kernel_trace.csv ;;
     pmcattn)  # counter passes of the training-default attention kernels at micro-batch 256
       bash tools/pmc_flash.sh "$OUT/pmca" && python3 tools/pmc_attn.py "$OUT/pmca" "$OUT/pmc_attn.json" \
         > "$OUT/pmc_attn.txt" 2>&1

@@ -26,7 +26,7 @@ def load(root):
         for r in csv.DictReader(open(path)):
             k = (r["Dispatch_Id"], r["Counter_Name"])
             per[k] += float(r["Counter_Value"])
-            names[r["Dispatch_Id"]] = r["Kernel_Name"].replace("void (anonymous namespace)::", "").split("(")[0]
+            names[r["Dispatch_Id"]] = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
             if "Start_Timestamp" in r and r["Start_Timestamp"]:
                 d[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
         for (disp, c), v in per.items():

@@ -2198,11 +2198,10 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
 #pragma unroll
     for (int db = 0; db < 5; ++db) o[db][0] = o[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};  // m: running max of the RAW scores
-#pragma unroll 1
-    for (int kb = 0; kb < FS_N / FA_KB; ++kb) {
+    // software pipeline over the four 64-key blocks: block kb + 1's S MFMAs are issued before block kb's softmax
+    // (independent vector work the SIMD issues while they run), then block kb's P V
+    auto scores = [&](int kb, f32x4 (&sc)[4][2]) {
       const bf16_t* Ks = Kall + kb * FA_KB * FS_ROW;
-      const bf16_t* Vs = Vall + kb * FA_KB * FS_ROW;
-      f32x4 sc[4][2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) sc[i][0] = sc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2213,6 +2212,9 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
           sc[i][0] = mfma(kf, qf[0][ks], sc[i][0]);
           sc[i][1] = mfma(kf, qf[1][ks], sc[i][1]);
         }
+    };
+    auto soft_pv = [&](int kb, f32x4 (&sc)[4][2]) {
+      const bf16_t* Vs = Vall + kb * FA_KB * FS_ROW;
       bf16x8 pf[2][2];  // [k-step of 32 keys][query block]
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
@@ -2244,33 +2246,41 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
       }
       // V^T fragments by inline-asm transposed reads (with the builtin hipcc drains the in-flight LDS-DMA
       // before each); the waits name the fragments so the consuming MFMAs stay behind them
-      s16x4 tv[2][5][2];
       const unsigned va = fs_lds_addr(Vs + (4 * g + ((lane & 15) >> 2)) * FS_ROW + 4 * (lane & 3));
-#define FS_TR(k2, db, hf) tv[k2][db][hf] = fs_tr<((k2) * 32 + 16 * (hf)) * FS_ROW * 2 + (db) * 32>(va)
-#define FS_TR_DB(k2, db) FS_TR(k2, db, 0); FS_TR(k2, db, 1)
-      FS_TR_DB(0, 0); FS_TR_DB(0, 1); FS_TR_DB(0, 2); FS_TR_DB(0, 3); FS_TR_DB(0, 4);
-      FS_TR_DB(1, 0); FS_TR_DB(1, 1); FS_TR_DB(1, 2); FS_TR_DB(1, 3); FS_TR_DB(1, 4);
-#undef FS_TR_DB
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        s16x4 tv[5][2];
+        if (k2 == 0) {
+#define FS_TR(db, hf) tv[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(va)
+          FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1); FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
+          FS_TR(4, 0); FS_TR(4, 1);
 #undef FS_TR
-      asm volatile("s_waitcnt lgkmcnt(10)"
-                   : "+v"(tv[0][0][0]), "+v"(tv[0][0][1]), "+v"(tv[0][1][0]), "+v"(tv[0][1][1]), "+v"(tv[0][2][0]),
-                     "+v"(tv[0][2][1]), "+v"(tv[0][3][0]), "+v"(tv[0][3][1]), "+v"(tv[0][4][0]), "+v"(tv[0][4][1]));
+        } else {
+#define FS_TR(db, hf) tv[db][hf] = fs_tr<(32 + 16 * (hf)) * FS_ROW * 2 + (db) * 32>(va)
+          FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1); FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
+          FS_TR(4, 0); FS_TR(4, 1);
+#undef FS_TR
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(tv[0][0]), "+v"(tv[0][1]), "+v"(tv[1][0]), "+v"(tv[1][1]), "+v"(tv[2][0]), "+v"(tv[2][1]),
+                       "+v"(tv[3][0]), "+v"(tv[3][1]), "+v"(tv[4][0]), "+v"(tv[4][1]));
 #pragma unroll
-      for (int db = 0; db < 5; ++db) {
-        const bf16x8 vf = fs_cat(tv[0][db][0], tv[0][db][1]);
-        o[db][0] = mfma(vf, pf[0][0], o[db][0]);
-        o[db][1] = mfma(vf, pf[0][1], o[db][1]);
+        for (int db = 0; db < 5; ++db) {
+          const bf16x8 vf = fs_cat(tv[db][0], tv[db][1]);
+          o[db][0] = mfma(vf, pf[k2][0], o[db][0]);
+          o[db][1] = mfma(vf, pf[k2][1], o[db][1]);
+        }
       }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(tv[1][0][0]), "+v"(tv[1][0][1]), "+v"(tv[1][1][0]), "+v"(tv[1][1][1]), "+v"(tv[1][2][0]),
-                     "+v"(tv[1][2][1]), "+v"(tv[1][3][0]), "+v"(tv[1][3][1]), "+v"(tv[1][4][0]), "+v"(tv[1][4][1]));
-#pragma unroll
-      for (int db = 0; db < 5; ++db) {
-        const bf16x8 vf = fs_cat(tv[1][db][0], tv[1][db][1]);
-        o[db][0] = mfma(vf, pf[1][0], o[db][0]);
-        o[db][1] = mfma(vf, pf[1][1], o[db][1]);
-      }
-    }
+    };
+    f32x4 scA[4][2], scB[4][2];
+    scores(0, scA);
+    scores(1, scB);
+    soft_pv(0, scA);
+    scores(2, scA);
+    soft_pv(1, scB);
+    scores(3, scB);
+    soft_pv(2, scA);
+    soft_pv(3, scB);
     FS_WAIT_VM(0);  // the next unit's Q fragments and images (issued before this unit's compute)
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {  // one output group (host-checked)
@@ -2713,34 +2723,14 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_f
   const bool dead = mk.dead(t);
   const int rb = fa_row_bits(mk, t), full_keys = fa_full_keys(mk);
   const bool clean = __ballot(dead || !live) == 0ull;  // wave-uniform
-  // pass 1: S^T[key][q] for every key of the row block (stage kb = K block kb)
+  // pass 1: S^T[key][q] for every key of the row block (stage kb = K block kb); the element-wise logits of block
+  // kb - 1 (soft-cap tanh, mask) are computed in stage kb beside its MFMAs (independent work the SIMD issues while
+  // the MFMAs run), tanh(cap) kept packed in registers and exported after the pass
   f32x4 sc[JP_MAXKB][4];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    FS_WAIT_VM(8);  // stage kb landed (stages kb + 1, kb + 2 in flight; the Q loads precede stage 0)
-    FS_BARRIER();
-    if (kb == 0)
-      asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4]), "+v"(qf[5]), "+v"(qf[6]),
-                   "+v"(qf[7]));
-    issue(kb + 3);
-    const char* slot = fa_smem + (kb % 4) * JD_SLOT + l15 * 512;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const char* kp = slot + 16 * ((4 * ks + g) ^ l15);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sc[kb][i] = mfma(*reinterpret_cast<const bf16x8*>(kp + i * 8192), qf[ks], sc[kb][i]);
-    }
-  }
-  FS_WAIT_VM(4);  // V blocks 0, 1 (stages 5, 6) landed by this wave; stage 7 in flight
-  // logits (log2 domain) + the tanh(cap) export; keys past nk / masked -> -inf
-  bf16_t* prow = P + (b * a.nq + (live ? r : 0)) * ldp;
-  bf16_t* trow = TC ? TC + (b * a.nq + (live ? r : 0)) * ldp : nullptr;
+  u32x2 tcv[JP_MAXKB][4];
   float mx = -INFINITY;
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    // uniform per block: every key allowed and every row live (no mask, no dead-row selects, no store guards)
+  auto logits_blk = [&](int kb) {
+    // uniform per block: every key allowed and every row live (no mask, no dead-row selects)
     auto logits = [&](auto FAST) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -2765,13 +2755,44 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_f
           mx = fmaxf(mx, x2);
           tv[e] = th;
         }
-        const int j0 = kb * FA_KB + i * 16 + 4 * g;
-        if (trow && (decltype(FAST)::value || (live && j0 < ldp)))
-          *reinterpret_cast<u32x2*>(trow + j0) = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
+        tcv[kb][i] = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
       }
     };
     if (clean && (kb + 1) * 64 <= full_keys) logits(std::true_type{});
     else logits(std::false_type{});
+  };
+#pragma unroll
+  for (int kb = 0; kb < JP_MAXKB; ++kb) {
+    FS_WAIT_VM(8);  // stage kb landed (stages kb + 1, kb + 2 in flight; the Q loads precede stage 0)
+    FS_BARRIER();
+    if (kb == 0)
+      asm volatile("" : "+v"(qf[0]), "+v"(qf[1]), "+v"(qf[2]), "+v"(qf[3]), "+v"(qf[4]), "+v"(qf[5]), "+v"(qf[6]),
+                   "+v"(qf[7]));
+    issue(kb + 3);
+    const char* slot = fa_smem + (kb % 4) * JD_SLOT + l15 * 512;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const char* kp = slot + 16 * ((4 * ks + g) ^ l15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sc[kb][i] = mfma(*reinterpret_cast<const bf16x8*>(kp + i * 8192), qf[ks], sc[kb][i]);
+    }
+    if (kb >= 1) logits_blk(kb - 1);
+  }
+  logits_blk(JP_MAXKB - 1);
+  FS_WAIT_VM(4);  // V blocks 0, 1 (stages 5, 6) landed by this wave; stage 7 in flight
+  bf16_t* prow = P + (b * a.nq + (live ? r : 0)) * ldp;
+  if (TC) {  // uniform: the tanh(cap) export (zeros past nk and for dead rows)
+    bf16_t* trow = TC + (b * a.nq + (live ? r : 0)) * ldp;
+#pragma unroll
+    for (int kb = 0; kb < JP_MAXKB; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j0 = kb * FA_KB + i * 16 + 4 * g;
+        if (clean && (kb + 1) * 64 <= full_keys) *reinterpret_cast<u32x2*>(trow + j0) = tcv[kb][i];
+        else if (live && j0 < ldp) *reinterpret_cast<u32x2*>(trow + j0) = tcv[kb][i];
+      }
   }
   mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));

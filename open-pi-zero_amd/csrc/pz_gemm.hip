@@ -1799,6 +1799,22 @@ void plan_tail(Plan& pl, const pz_gemm_args* a) {
   if (r == 0 || (q > 0 && 2 * r >= G) || q > 8) return;
   int64_t s = G / r;
   s = s < 16 ? s : 16;
+  if (q == 0) {
+    // the whole GEMM is the tail (weight gradients of the 1152-wide SigLIP layers: 70 / 85 / 25 tiles): the pieces
+    // may take several rounds when that fills the CUs better.  Cost (us) = rounds(s) / s x nk x 1.8 (a 256 x 256 x 64
+    // step at ~4.6 TF/s per CU) + r s x 0.1 (each piece's 256 KiB fp32 partial written and re-read, chip-wide):
+    // 70 tiles x 1024 K-tiles -> 3 pieces in one 82 %-full round 635 us, 7 pieces in two 96 %-full rounds 576 us
+    const int64_t smax = (int64_t)(a->ws_bytes / (32 * NT2 * 16)) / r;
+    auto cost = [&](int64_t s2) { return (double)((r * s2 + G - 1) / G) / (double)s2 * (double)nk * 1.8 + r * s2 * 0.1; };
+    double best = cost(s);
+    for (int64_t s2 = s + 1; s2 <= 16 && s2 <= nk / 2 && s2 <= smax; ++s2) {
+      const double c = cost(s2);
+      if (c < best * 0.97) {
+        best = c;
+        s = s2;
+      }
+    }
+  }
   // no split below 8 K-tiles: a piece writes (and the merge re-reads) a 256 KiB fp32 partial, which a short
   // reduction cannot amortise -- the K = 320 action-expert wgrad (8192 x 1024, 5 K-tiles) took 42.0 us with
   // 2 pieces per leftover tile vs 20.0 us whole (tools/shape_ab.py, profiles/r03/shape_ab.log)

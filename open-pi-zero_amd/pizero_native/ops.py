@@ -73,7 +73,7 @@ def gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, *, epi=PZ_EPI_NONE, alpha
           geglu_inter, batch, batch_inner, sA, sB, sC, sR, norm)
 
 
-_WS_BYTES = 64 << 20
+_WS_BYTES = 160 << 20  # split-K / split-tail fp32 partials (multi-round tails: up to 640 x 256 KiB)
 _WS = {}
 
 

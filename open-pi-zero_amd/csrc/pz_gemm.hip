@@ -804,12 +804,15 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
   }
   const bool act = FM == FM_BF16 && (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU);
   const bool gelu = p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_DGELU;
+  // side inputs in 4 batches of 4 chunks (8 x 16 B per thread in flight); batches of 8 chunks (128 KiB per CU in
+  // flight) make hipcc spill 136-172 B in every non-GeGLU 8-phase kernel, so they were not measured
+  constexpr int CPB = 4;
 #pragma unroll
-  for (int half = 0; half < 4; ++half) {  // 4 batches of 4 chunks: a batch's loads issued together
-    u32x4 a0[4], a1[4], iv[4];
+  for (int half = 0; half < 16 / CPB; ++half) {  // a batch's loads issued together
+    u32x4 a0[CPB], a1[CPB], iv[CPB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = threadIdx.x + (half * 4 + i) * NT2;  // 0 .. 8191 over the two images
+    for (int i = 0; i < CPB; ++i) {
+      const int c = threadIdx.x + (half * CPB + i) * NT2;  // 0 .. 8191 over the two images
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
       const int col = im * 128 + ch * 8;
       iv[i] = *reinterpret_cast<const u32x4*>(smem + im * 65536 + row * 256 + ((ch ^ (row & 15)) << 4));
@@ -817,8 +820,8 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
       a1[i] = X1 ? *reinterpret_cast<const u32x4*>(X1 + row * ld1 + col) : u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int c = threadIdx.x + (half * 4 + i) * NT2;
+    for (int i = 0; i < CPB; ++i) {
+      const int c = threadIdx.x + (half * CPB + i) * NT2;
       const int im = c >> 12, row = (c >> 4) & 255, ch = c & 15;
       const int col = im * 128 + ch * 8;
       float v[8], x0[8], x1[8];

@@ -2340,6 +2340,8 @@ __global__ void __launch_bounds__(256) flash_delta72_kernel(pz_flash_args a) {
 // dQ with K / V resident (delta = rowsum(dO O) from flash_bwd_prep_kernel): wave w owns query rows 32w ..
 // 32w + 31; the next unit's Q / dO rows, lse and delta (inline-asm loads) and K / V images (LDS-DMA) are issued
 // before this unit's compute
+template <bool DELTA>  // DELTA: delta = rowsum(dO O) computed here from O rows loaded at the unit's start (and written
+                       // for the dK / dV pass) instead of read from flash_delta72_kernel's output
 __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash_args a, int G) {
   extern __shared__ __attribute__((aligned(16))) char fa_smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
@@ -2360,7 +2362,7 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
       fs_load_rows(qn[qb], Q + r * a.ldq, g);
       fs_load_rows(dn[qb], (const bf16_t*)a.g_do[0] + bn * a.g_bstride[0] + r * a.g_ld[0] + hn * a.o_hstride, g);
       asm volatile("global_load_dword %0, %1, off" : "=v"(ln[qb]) : "v"(a.lse + un * FS_N + r) : "memory");
-      asm volatile("global_load_dword %0, %1, off" : "=v"(dln[qb]) : "v"(a.delta + un * FS_N + r) : "memory");
+      if (!DELTA) asm volatile("global_load_dword %0, %1, off" : "=v"(dln[qb]) : "v"(a.delta + un * FS_N + r) : "memory");
     }
     char* nxt = fa_smem + (t1 & 1) * 2 * FS_IMG;
     fs_dma((const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride, offk, nxt, wave);
@@ -2385,6 +2387,26 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
       asm volatile("" : "+v"(ln[qb]), "+v"(dln[qb]));
       lse2[qb] = ln[qb] * FA_LOG2E;
       del[qb] = dln[qb];
+    }
+    if constexpr (DELTA) {  // O rows by ordinary loads, before the next unit's DMA is issued (nothing else in flight)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        const int64_t r = wave * 32 + qb * 16 + (lane & 15);
+        const bf16_t* Or = (const bf16_t*)a.g_o[0] + b * a.g_bstride[0] + r * a.g_ld[0] + h * a.o_hstride;
+        float dl = 0.f;
+        bf16x8 ov[3];
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks)  // dims 72..95 re-read 64..71 against the zeroed dO fragment (no branch)
+          ov[ks] = *reinterpret_cast<const bf16x8*>(Or + (ks < 2 || g == 0 ? ks * 32 + 8 * g : 64));
+#pragma unroll
+        for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dl = fmaf((float)df[qb][ks][e], (float)ov[ks][e], dl);
+        dl += __shfl_xor(dl, 16, 64);
+        dl += __shfl_xor(dl, 32, 64);
+        del[qb] = dl;
+        if (g == 0) a.delta[u * FS_N + r] = dl;
+      }
     }
     const int64_t un = fs_unit(a, G, t + 1);
     if (un < units) issue(un, t + 1);  // uniform
@@ -3312,13 +3334,20 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     static bool aq = false, akv = false, aq2 = false, akv2 = false, aq3 = false, akv3 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
-      const int64_t rows = a->Z * a->H * a->nq;
-      hipLaunchKernelGGL(flash_delta72_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, *a);
-      PZ_CHECK_LAUNCH();
       const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
-      fa_smem_attr(flash_bwd_q_sig_kernel, FS_SMEM, aq3);
+      const char* ed = getenv("PZ_SIG_DELTA");  // "pass": the separate delta pass (A/B runs)
       fa_smem_attr(flash_bwd_kv_sig_kernel, FS_SMEM, akv3);
-      hipLaunchKernelGGL(flash_bwd_q_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+      if (ed && ed[0] == 'p') {
+        const int64_t rows = a->Z * a->H * a->nq;
+        hipLaunchKernelGGL(flash_delta72_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, *a);
+        PZ_CHECK_LAUNCH();
+        fa_smem_attr(flash_bwd_q_sig_kernel<false>, FS_SMEM, aq3);
+        hipLaunchKernelGGL(flash_bwd_q_sig_kernel<false>, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+      } else {
+        static bool aq4 = false;
+        fa_smem_attr(flash_bwd_q_sig_kernel<true>, FS_SMEM, aq4);
+        hipLaunchKernelGGL(flash_bwd_q_sig_kernel<true>, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+      }
       PZ_CHECK_LAUNCH();
       hipLaunchKernelGGL(flash_bwd_kv_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
     } else if (fa_plain(a)) {

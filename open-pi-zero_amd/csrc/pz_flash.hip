@@ -2143,45 +2143,56 @@ __device__ __forceinline__ bf16x8 fs_cat(const s16x4& a, const s16x4& b) {
     asm volatile("" ::: "memory");                     \
   } while (0)
 
-// forward: wave w owns query rows 32w .. 32w + 31 of the unit (two 16-row blocks share each K / V
-// fragment read); log2-domain online softmax over four 64-key blocks with the scale folded into the
-// exponent's FMA (max over raw scores: scale > 0)
-__global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_args a, int G) {
+// forward: QB 16-row query blocks per wave (QB = 2: 8 waves, two blocks share each K / V fragment read, 2 waves per
+// SIMD; QB = 1: 16 waves of 16 rows, 4 waves per SIMD at <= 128 VGPRs -- twice the LDS fragment reads per MFMA but
+// twice the waves to hide the softmax chains and LDS latencies); log2-domain online softmax over four 64-key blocks
+// with the scale folded into the exponent's FMA (max over raw scores: scale > 0)
+template <int QB>
+__global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash_args a, int G) {
+  constexpr int NW = 16 / QB;
   extern __shared__ __attribute__((aligned(16))) char fa_smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const int64_t units = a.Z * a.H;
+  // DMA pieces: QB = 2 -- each wave 5 pieces of K and 5 of V; QB = 1 -- waves 0..7 the K image, 8..15 the V image
   int offk[FS_PER], offv[FS_PER];
-  fs_dma_offsets(a.ldk, wave, lane, offk);
-  fs_dma_offsets(a.ldv, wave, lane, offv);
+  fs_dma_offsets(QB == 1 && wave >= 8 ? a.ldv : a.ldk, wave & 7, lane, offk);
+  fs_dma_offsets(a.ldv, wave & 7, lane, offv);
   const float sl2 = a.scale * FA_LOG2E;
   // Pipeline (per workgroup, unit t in buffer t & 1): the Q fragments of unit t + 1 (inline-asm loads into
   // qn: hipcc would drain every in-flight LDS-DMA with vmcnt(0) at the first use of an ordinary load) and its
   // K / V images are issued before unit t's compute; one vmcnt(0) after the compute (long landed by then),
   // before unit t's O stores, and the barrier that ends unit t publish them, so no wait stalls in steady state.
   int64_t u = fs_unit(a, G, 0);
-  bf16x8 qn[2][3];
+  bf16x8 qn[QB][3];
   auto issue = [&](int64_t un, int t1) {  // Q fragments + K / V images of unit un into buffer t1 & 1
     const int64_t bn = un / a.H, hn = un % a.H;
     const bf16_t* Q = (const bf16_t*)a.q + bn * a.q_bstride + hn * a.q_hstride;
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
+    for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) {  // head dims 72..95 (g >= 1 at ks 2) re-read dims 64..71, zeroed below
-        const bf16_t* src = Q + (wave * 32 + qb * 16 + (lane & 15)) * a.ldq + (ks < 2 || g == 0 ? ks * 32 + 8 * g : 64);
+        const bf16_t* src =
+            Q + (wave * 16 * QB + qb * 16 + (lane & 15)) * a.ldq + (ks < 2 || g == 0 ? ks * 32 + 8 * g : 64);
         asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qn[qb][ks]) : "v"(src) : "memory");
       }
     char* nxt = fa_smem + (t1 & 1) * 2 * FS_IMG;
-    fs_dma((const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride, offk, nxt, wave);
-    fs_dma((const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride, offv, nxt + FS_IMG, wave);
+    const bf16_t* Kn = (const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride;
+    const bf16_t* Vn = (const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride;
+    if constexpr (QB == 2) {
+      fs_dma(Kn, offk, nxt, wave);
+      fs_dma(Vn, offv, nxt + FS_IMG, wave);
+    } else {
+      fs_dma(wave < 8 ? Kn : Vn, offk, nxt + (wave < 8 ? 0 : FS_IMG), wave & 7);
+    }
   };
   if (u < units) issue(u, 0);
   FS_WAIT_VM(0);
   FS_BARRIER();
   for (int t = 0; u < units; ++t) {
     const int64_t b = u / a.H, h = u % a.H;
-    bf16x8 qf[2][3];
+    bf16x8 qf[QB][3];
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks) {
         asm volatile("" : "+v"(qn[qb][ks]));  // landed (the vmcnt(0) before the previous barrier)
@@ -2194,30 +2205,39 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
     const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
     const bf16_t* Kall = reinterpret_cast<const bf16_t*>(cur);
     const bf16_t* Vall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
-    f32x4 o[5][2];
+    f32x4 o[5][QB];
 #pragma unroll
-    for (int db = 0; db < 5; ++db) o[db][0] = o[db][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m[2] = {-INFINITY, -INFINITY}, l[2] = {0.f, 0.f};  // m: running max of the RAW scores
+    for (int db = 0; db < 5; ++db)
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m[QB], l[QB];  // m: running max of the RAW scores
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+      m[qb] = -INFINITY;
+      l[qb] = 0.f;
+    }
     // software pipeline over the four 64-key blocks: block kb + 1's S MFMAs are issued before block kb's softmax
     // (independent vector work the SIMD issues while they run), then block kb's P V
-    auto scores = [&](int kb, f32x4 (&sc)[4][2]) {
+    auto scores = [&](int kb, f32x4 (&sc)[4][QB]) {
       const bf16_t* Ks = Kall + kb * FA_KB * FS_ROW;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sc[i][0] = sc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) sc[i][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 3; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bf16x8 kf = frag_row<FS_ROW>(Ks, i * 16, ks * 32, lane);
-          sc[i][0] = mfma(kf, qf[0][ks], sc[i][0]);
-          sc[i][1] = mfma(kf, qf[1][ks], sc[i][1]);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) sc[i][qb] = mfma(kf, qf[qb][ks], sc[i][qb]);
         }
     };
-    auto soft_pv = [&](int kb, f32x4 (&sc)[4][2]) {
+    auto soft_pv = [&](int kb, f32x4 (&sc)[4][QB]) {
       const bf16_t* Vs = Vall + kb * FA_KB * FS_ROW;
-      bf16x8 pf[2][2];  // [k-step of 32 keys][query block]
+      bf16x8 pf[2][QB];  // [k-step of 32 keys][query block]
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
+      for (int qb = 0; qb < QB; ++qb) {
         float mx = fmaxf(fmaxf(sc[0][qb][0], sc[0][qb][1]), fmaxf(sc[0][qb][2], sc[0][qb][3]));
 #pragma unroll
         for (int i = 1; i < 4; ++i)
@@ -2267,12 +2287,12 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
 #pragma unroll
         for (int db = 0; db < 5; ++db) {
           const bf16x8 vf = fs_cat(tv[db][0], tv[db][1]);
-          o[db][0] = mfma(vf, pf[k2][0], o[db][0]);
-          o[db][1] = mfma(vf, pf[k2][1], o[db][1]);
+#pragma unroll
+          for (int qb = 0; qb < QB; ++qb) o[db][qb] = mfma(vf, pf[k2][qb], o[db][qb]);
         }
       }
     };
-    f32x4 scA[4][2], scB[4][2];
+    f32x4 scA[4][QB], scB[4][QB];
     scores(0, scA);
     scores(1, scB);
     soft_pv(0, scA);
@@ -2283,8 +2303,8 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_fwd_sig_kernel(pz_flash_a
     soft_pv(3, scB);
     FS_WAIT_VM(0);  // the next unit's Q fragments and images (issued before this unit's compute)
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {  // one output group (host-checked)
-      const int64_t rq = wave * 32 + qb * 16 + (lane & 15);
+    for (int qb = 0; qb < QB; ++qb) {  // one output group (host-checked)
+      const int64_t rq = wave * 16 * QB + qb * 16 + (lane & 15);
       const float inv = 1.f / l[qb];
       bf16_t* O = (bf16_t*)a.g_o[0] + b * a.g_bstride[0] + rq * a.g_ld[0] + h * a.o_hstride;
 #pragma unroll
@@ -3200,8 +3220,15 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {
       const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
-      fa_smem_attr(flash_fwd_sig_kernel, FS_SMEM, attr3);
-      hipLaunchKernelGGL(flash_fwd_sig_kernel, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
+      const char* eq = getenv("PZ_SIG_QB");  // "2": 8 waves of 32 rows (A/B runs); default 16 waves of 16 rows
+      if (eq && eq[0] == '2') {
+        fa_smem_attr(flash_fwd_sig_kernel<2>, FS_SMEM, attr3);
+        hipLaunchKernelGGL(flash_fwd_sig_kernel<2>, dim3((unsigned)G), dim3(8 * 64), FS_SMEM, st, *a, G);
+      } else {
+        static bool attr4 = false;
+        fa_smem_attr(flash_fwd_sig_kernel<1>, FS_SMEM, attr4);
+        hipLaunchKernelGGL(flash_fwd_sig_kernel<1>, dim3((unsigned)G), dim3(16 * 64), FS_SMEM, st, *a, G);
+      }
     } else if (fa_plain(a)) {
       fa_smem_attr(flash_fwd_unit_kernel<72, true>, FR_SMEM_KQ, attr);
       hipLaunchKernelGGL((flash_fwd_unit_kernel<72, true>), gu, dim3(FU_NW * 64), FR_SMEM_KQ, st, *a);

@@ -62,8 +62,9 @@ def ref_attention(q, k, v, scale, cap=0.0, allowed=None, dead=None):
     return p @ v, lse
 
 
-@pytest.mark.parametrize("unit,sig,B", [("0", "0", 3), ("1", "0", 3), ("1", "1", 3), ("1", "1", 40)])
-def test_flash_fwd_siglip(unit, sig, B, monkeypatch):
+@pytest.mark.parametrize("unit,sig,B,qb", [("0", "0", 3, "1"), ("1", "0", 3, "1"), ("1", "1", 3, "1"), ("1", "1", 40, "1"),
+                                           ("1", "1", 40, "2")])
+def test_flash_fwd_siglip(unit, sig, B, qb, monkeypatch):
     """the SigLIP forward kernel families: 2 workgroups per unit (few units), one workgroup per unit, and the
     persistent pipelined kernel (B = 40: 640 units over the CUs, several units per workgroup with a ragged
     last round, XCD-grouped unit order)"""
@@ -71,6 +72,7 @@ def test_flash_fwd_siglip(unit, sig, B, monkeypatch):
 
     monkeypatch.setenv("PZ_FLASH_UNIT", unit)
     monkeypatch.setenv("PZ_FLASH_SIG", sig)
+    monkeypatch.setenv("PZ_SIG_QB", qb)  # persistent forward: 16 waves x 16 rows (1) or 8 x 32 (2)
 
     nh, hd, N = 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)

@@ -84,10 +84,12 @@ def main():
     fl = 4.0 * B * nh * N * N * hd
     # PZ_FLASH_SIG / PZ_FLASH_UNIT: the persistent pipelined kernels (default), one workgroup per (image, head)
     # unit, the 2-/4-workgroup resident kernels
-    for sig, unit in (("1", "1"),) if a.default_only else (("1", "1"), ("1p", "1"), ("0", "1"), ("0", "0")):
-        # "1p": the persistent kernels with the separate delta pass (PZ_SIG_DELTA=pass)
+    for sig, unit in (("1", "1"),) if a.default_only else (("1", "1"), ("1q", "1"), ("1p", "1"), ("0", "1"), ("0", "0")):
+        # "1p": the persistent kernels with the separate delta pass (PZ_SIG_DELTA=pass); "1q": the forward with 8 waves
+        # of 32 rows (PZ_SIG_QB=2)
         os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig[0]
         os.environ["PZ_SIG_DELTA"] = "pass" if sig == "1p" else "fused"
+        os.environ["PZ_SIG_QB"] = "2" if sig == "1q" else "1"
         tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
         tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
         print(f"siglip(sig={sig},unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
@@ -95,6 +97,7 @@ def main():
     os.environ.pop("PZ_FLASH_UNIT")
     os.environ.pop("PZ_FLASH_SIG")
     os.environ.pop("PZ_SIG_DELTA")
+    os.environ.pop("PZ_SIG_QB")
 
 
 if __name__ == "__main__":

@@ -32,7 +32,7 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--default-only", action="store_true", help="only the training-default kernels (PMC passes)")
     a = ap.parse_args()

@@ -2085,6 +2085,22 @@ constexpr int FU_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
 // the 64 banks).  Each row's tenth 16-B chunk (head dims 72..79) repeats the ninth: the products that read it
 // meet zero Q / dO columns or land in discarded output columns; the 32-wide k step past column 79 reads the
 // next row's (finite) data against zero Q columns the same way.
+// reductions over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (the 4 lane groups of a 16 x 16 MFMA column) with gfx950's
+// v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip as __shfl_xor's ds_bpermute); every lane gets the
+// same value, combined in the same order
+__device__ __forceinline__ float fs_max4(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+}
+__device__ __forceinline__ float fs_sum4(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+}
+
 constexpr int FS_N = 256, FS_ROW = 80, FS_IMG = FS_N * FS_ROW * 2, FS_SMEM = 4 * FS_IMG;
 constexpr int FS_NW = 8, FS_PER = FS_N * 10 / 64 / FS_NW;  // DMA instructions per wave per image (5)
 
@@ -2242,8 +2258,7 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
 #pragma unroll
         for (int i = 1; i < 4; ++i)
           mx = fmaxf(fmaxf(mx, fmaxf(sc[i][qb][0], sc[i][qb][1])), fmaxf(sc[i][qb][2], sc[i][qb][3]));
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mx = fs_max4(mx);
         const float mn = fmaxf(m[qb], mx), nb = -mn * sl2;
         const float alpha = __builtin_amdgcn_exp2f((m[qb] - mn) * sl2);  // exp2(-inf) = 0 on the first block
         float sum = 0.f;
@@ -2255,8 +2270,7 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
             sc[i][qb][e] = pv;
             sum += pv;
           }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
+        sum = fs_sum4(sum);
         l[qb] = fmaf(l[qb], alpha, sum);
         m[qb] = mn;
 #pragma unroll
@@ -2422,8 +2436,7 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
         for (int ks = 0; ks < 3; ++ks)
 #pragma unroll
           for (int e = 0; e < 8; ++e) dl = fmaf((float)df[qb][ks][e], (float)ov[ks][e], dl);
-        dl += __shfl_xor(dl, 16, 64);
-        dl += __shfl_xor(dl, 32, 64);
+        dl = fs_sum4(dl);
         del[qb] = dl;
         if (g == 0) a.delta[u * FS_N + r] = dl;
       }
@@ -2836,8 +2849,7 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_f
         else if (live && j0 < ldp) *reinterpret_cast<u32x2*>(trow + j0) = tcv[kb][i];
       }
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = fs_max4(mx);
   float sum = 0.f;
 #pragma unroll
   for (int kb = 0; kb < JP_MAXKB; ++kb)
@@ -2849,8 +2861,7 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_fwd_probs_dma_kernel(pz_f
         sc[kb][i][e] = pv;
         sum += pv;
       }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
+  sum = fs_sum4(sum);
   // fully masked (dead) rows: uniform over the N keys (the finfo.min mask absorbs the logits)
   const float inv = 1.f / sum, uni = 1.f / (float)nk;
   bf16x8 pf[JP_MAXKB][2];
@@ -3032,8 +3043,7 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_bwd_ds_dma_kernel(pz_flas
       const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
       dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
     }
-  dot += __shfl_xor(dot, 16, 64);
-  dot += __shfl_xor(dot, 32, 64);
+  dot = fs_sum4(dot);
   FS_WAIT_VM(0);
 #pragma unroll
   for (int kb = 0; kb < JP_MAXKB; ++kb)

@@ -3043,7 +3043,8 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_bwd_ds_dma_kernel(pz_flas
       const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
       dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
     }
-  dot = fs_sum4(dot);
+  dot += __shfl_xor(dot, 16, 64);  // (fs_sum4's two extra registers make this kernel spill)
+  dot += __shfl_xor(dot, 32, 64);
   FS_WAIT_VM(0);
 #pragma unroll
   for (int kb = 0; kb < JP_MAXKB; ++kb)

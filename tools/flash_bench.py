@@ -32,9 +32,10 @@ def timeit(fn, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--default-only", action="store_true", help="only the training-default kernels (PMC passes)")
+    ap.add_argument("--rounds", type=int, default=5, help="interleaved timing rounds per variant (median)")
     a = ap.parse_args()
     dev = "cuda"
     B, P, C, H, nh, hd = a.batch, 276, 1, 4, 8, 256
@@ -57,15 +58,18 @@ def main():
     fl = 4.0 * B * L * nh * L * hd
     Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
     tcm = torch.empty_like(Pm)
-    for dma in ("1",) if a.default_only else ("1", "0"):  # PZ_PROBS_DMA: LDS-DMA ring (default) vs register staging
-        os.environ["PZ_PROBS_DMA"] = dma
-        tp = timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters)
-        print(f"joint  fwd+probs(dma={dma}) {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)",
-              flush=True)
-    os.environ.pop("PZ_PROBS_DMA")
     dSm = torch.empty_like(Pm)
-    td = timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters)
-    print(f"joint  bwd dS {td:.3f} ms (dP = dO V^T in registers + softmax backward from P / tanh(cap))", flush=True)
+    jt = {dma: ([], []) for dma in (("1",) if a.default_only else ("1", "0"))}  # PZ_PROBS_DMA: LDS-DMA ring / registers
+    for _ in range(1 if a.default_only else a.rounds):
+        for dma in jt:
+            os.environ["PZ_PROBS_DMA"] = dma
+            jt[dma][0].append(timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters))
+            jt[dma][1].append(timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters))
+    os.environ.pop("PZ_PROBS_DMA")
+    for dma, (tps, tds) in jt.items():
+        tp, td = sorted(tps)[len(tps) // 2], sorted(tds)[len(tds) // 2]
+        print(f"joint(dma={dma})  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)   "
+              f"bwd dS {td:.3f} ms (+ dQ)  (median of {len(tps)} rounds)", flush=True)
     for fast in () if a.default_only else ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
         os.environ["PZ_FLASH_FAST"] = fast
         tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
@@ -83,22 +87,26 @@ def main():
     sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
     fl = 4.0 * B * nh * N * N * hd
     # PZ_FLASH_SIG / PZ_FLASH_UNIT: the persistent pipelined kernels (default), one workgroup per (image, head)
-    # unit, the 2-/4-workgroup resident kernels
-    for sig, unit in (("1", "1"),) if a.default_only else (("1", "1"), ("1q", "1"), ("1p", "1"), ("0", "1"), ("0", "0")):
-        # "1p": the persistent kernels with the separate delta pass (PZ_SIG_DELTA=pass); "1q": the forward with 8 waves
-        # of 32 rows (PZ_SIG_QB=2)
-        os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig[0]
-        os.environ["PZ_SIG_DELTA"] = "pass" if sig == "1p" else "fused"
-        os.environ["PZ_SIG_QB"] = "2" if sig == "1q" else "1"
-        tf = timeit(lambda: ops.flash_fwd(sa), a.iters)
-        tb = timeit(lambda: ops.flash_bwd(sa), a.iters)
+    # unit, the 2-/4-workgroup resident kernels; "1p": the persistent kernels with the separate delta pass
+    # (PZ_SIG_DELTA=pass); "1q": the forward with 8 waves of 32 rows (PZ_SIG_QB=2).  The variants are timed in
+    # interleaved rounds (clock drift between back-to-back runs of the same kernel reaches ~10 %) and the median
+    # of the rounds is printed.
+    variants = [("1", "1")] if a.default_only else [("1", "1"), ("1q", "1"), ("1p", "1"), ("0", "1"), ("0", "0")]
+    times = {v: ([], []) for v in variants}
+    for _ in range(1 if a.default_only else a.rounds):
+        for v in variants:
+            sig, unit = v
+            os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig[0]
+            os.environ["PZ_SIG_DELTA"] = "pass" if sig == "1p" else "fused"
+            os.environ["PZ_SIG_QB"] = "2" if sig == "1q" else "1"
+            times[v][0].append(timeit(lambda: ops.flash_fwd(sa), a.iters))
+            times[v][1].append(timeit(lambda: ops.flash_bwd(sa), a.iters))
+    for (sig, unit), (tfs, tbs) in times.items():
+        tf, tb = sorted(tfs)[len(tfs) // 2], sorted(tbs)[len(tbs) // 2]
         print(f"siglip(sig={sig},unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
-              f"{2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
-    os.environ.pop("PZ_FLASH_UNIT")
-    os.environ.pop("PZ_FLASH_SIG")
-    os.environ.pop("PZ_SIG_DELTA")
-    os.environ.pop("PZ_SIG_QB")
-
+              f"{2.5 * fl / tb / 1e9:.0f} TF/s  (median of {len(tfs)} rounds)", flush=True)
+    for k in ("PZ_FLASH_UNIT", "PZ_FLASH_SIG", "PZ_SIG_DELTA", "PZ_SIG_QB"):
+        os.environ.pop(k)
 
 if __name__ == "__main__":
     main()

@@ -484,7 +484,10 @@ extern "C" int64_t pz_norm_rows_per_part(void) { return ROWS_PER_PART; }
 // loads are issued before the current row's reductions (two rows in flight per workgroup); the two
 // row sums go through a double-buffered LDS slot (one barrier per row).  The wave-per-row kernels
 // above hold MAXC x 8 accumulators per thread (2 waves / SIMD at D >= 1152): PZ_NORM_BWD=wave (A/B).
-template <bool LN>
+// PF = rows loaded ahead (1: the next row; 2: the next two -- three rows of x / dy / residual gradient in
+// flight per workgroup, so a partly filled last round of workgroups is not latency-bound: 70656 Gemma rows
+// are 4416 parts of 16 rows = 2.16 rounds of 2048 resident workgroups).  PZ_NORM_PF=1 (A/B).
+template <bool LN, int PF>
 __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
     const bf16_t* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -506,19 +509,24 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
   const int64_t r0 = (int64_t)blockIdx.x * ROWS_PER_PART;
   const int nrows = (int)(R - r0 < ROWS_PER_PART ? R - r0 : ROWS_PER_PART);
   const u32x4 z4 = {0u, 0u, 0u, 0u};
-  u32x4 xr = z4, dyr = z4, drr = z4;
+  u32x4 xr = z4, dyr = z4, drr = z4, x1 = z4, dy1 = z4, dr1 = z4;
   if (act) {
     xr = *reinterpret_cast<const u32x4*>(x + r0 * ldx + t * 8);
     dyr = *reinterpret_cast<const u32x4*>(dy + r0 * lddy + t * 8);
     if (dres) drr = *reinterpret_cast<const u32x4*>(dres + r0 * lddx + t * 8);
+    if (PF == 2 && nrows > 1) {
+      x1 = *reinterpret_cast<const u32x4*>(x + (r0 + 1) * ldx + t * 8);
+      dy1 = *reinterpret_cast<const u32x4*>(dy + (r0 + 1) * lddy + t * 8);
+      if (dres) dr1 = *reinterpret_cast<const u32x4*>(dres + (r0 + 1) * lddx + t * 8);
+    }
   }
   for (int i = 0; i < nrows; ++i) {
     const int64_t row = r0 + i;
     u32x4 xn = z4, dyn = z4, drn = z4;
-    if (act && i + 1 < nrows) {  // next row in flight during this row's reductions
-      xn = *reinterpret_cast<const u32x4*>(x + (row + 1) * ldx + t * 8);
-      dyn = *reinterpret_cast<const u32x4*>(dy + (row + 1) * lddy + t * 8);
-      if (dres) drn = *reinterpret_cast<const u32x4*>(dres + (row + 1) * lddx + t * 8);
+    if (act && i + PF < nrows) {  // the row PF ahead in flight during this row's reductions
+      xn = *reinterpret_cast<const u32x4*>(x + (row + PF) * ldx + t * 8);
+      dyn = *reinterpret_cast<const u32x4*>(dy + (row + PF) * lddy + t * 8);
+      if (dres) drn = *reinterpret_cast<const u32x4*>(dres + (row + PF) * lddx + t * 8);
     }
     const float r = rstd[row], mu = LN ? mean[row] : 0.f;
     float xv[8], dv[8], g[8];
@@ -567,9 +575,12 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
         for (int e = 0; e < 8; ++e) dxa[e] += bf2f(f2bf(o[e]));
       }
     }
-    xr = xn;
-    dyr = dyn;
-    drr = drn;
+    if (PF == 2) {
+      xr = x1, dyr = dy1, drr = dr1;
+      x1 = xn, dy1 = dyn, dr1 = drn;
+    } else {
+      xr = xn, dyr = dyn, drr = drn;
+    }
   }
   if (!act) return;
   if (dx_part) {
@@ -592,6 +603,11 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
 static bool norm_bwd_rows() {
   const char* e = getenv("PZ_NORM_BWD");
   return !(e && e[0] == 'w');
+}
+
+static bool norm_bwd_pf1() {
+  const char* e = getenv("PZ_NORM_PF");
+  return e && e[0] == '1';
 }
 
 #define NORM_DISPATCH(KERNEL, GRID, ...)                                                   \
@@ -633,9 +649,9 @@ extern "C" int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16))
-    hipLaunchKernelGGL(norm_bwd_row_kernel<false>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
-                       ldx, (const bf16_t*)w, nullptr, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, nullptr,
-                       R, (int)D, nullptr);
+    hipLaunchKernelGGL((norm_bwd_pf1() ? norm_bwd_row_kernel<false, 1> : norm_bwd_row_kernel<false, 2>), grid,
+                       dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w, nullptr,
+                       rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, nullptr, R, (int)D, nullptr);
   else
     NORM_DISPATCH(rmsnorm_bwd_kernel, grid, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w,
                   rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, R, (int)D);
@@ -667,9 +683,9 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16) &&
       PZ_ALIGNED(db_part, 16) && (!dx_part || PZ_ALIGNED(dx_part, 16)))
-    hipLaunchKernelGGL(norm_bwd_row_kernel<true>, grid, dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x,
-                       ldx, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R,
-                       (int)D, dx_part);
+    hipLaunchKernelGGL((norm_bwd_pf1() ? norm_bwd_row_kernel<true, 1> : norm_bwd_row_kernel<true, 2>), grid,
+                       dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w, mean, rstd,
+                       (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D, dx_part);
   else if (dx_part)
     PZ_CHECK_ARG(false, "layernorm_bwd: dx_part (fused column sums of dx) needs the row kernel (16-byte aligned "
                         "dy / dres / partials / dx_part, PZ_NORM_BWD != wave)");

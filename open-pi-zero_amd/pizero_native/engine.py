@@ -970,7 +970,9 @@ class Engine:
                 ops.gemm(Lp, hd, L * nh, dS, Lp, False, Qj, hd, False, dK, hd, batch=B, sA=(L * nh * Lp, 0),
                          sB=(L * nh * hd, 0), sC=(Lp * hd, 0))
                 first = True
-                for g in groups:
+                # the shortest mixture first (the action expert's 5 rows x heads: its launch then writes dV
+                # instead of reading + writing it, and the long vlm launch accumulates in its epilogue)
+                for g in sorted(groups, key=lambda g: g.T):
                     if g.name not in dO:
                         continue
                     ops.gemm(Lp, hd, g.T * nh, Pm[:, g.off * nh:], Lp, False, dO[g.name], hd, False, dV, hd, batch=B,

@@ -69,3 +69,7 @@ def test_gemm_planner_routes_without_gpu():
     assert not ops.gemm_kernel_name(17664, 2560, 2048).startswith("gemm_rows")  # training rows: 8-phase
     assert not ops.gemm_kernel_name(320, 1024, 2048, a_kc=False).startswith("gemm_rows")  # k-strided A
     assert ops.gemm_kernel_name(16384, 1152, 1152).startswith("gemm8p_kernel")
+    # fewer 256-tiles than CUs at K <= 4096 and >= 1024 rows (the action expert at micro-batch 256): 128-tile kernel
+    assert ops.gemm_kernel_name(1280, 2560, 1024).startswith("gemm_kernel<")
+    assert ops.gemm_kernel_name(8192, 1024, 1280, a_kc=False, b_kc=False).startswith("gemm_kernel<")
+    assert ops.gemm_kernel_name(1280, 1024, 8192, b_kc=False).startswith("gemm8k_kernel")  # K 8192: 256 + tail

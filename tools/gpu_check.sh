@@ -106,6 +106,19 @@ PY
     launcher)  # bench.py --gpus 2 rehearsal: 2 gloo ranks on this card
       timeout -k 10 900 python -u -m pytest tests/test_bench_launcher.py -m gpu -x -v --timeout 880 \
         --timeout-method thread > "$OUT/launcher.log" 2>&1 ;;
+    normbench)  # memory-bound backward kernels (norms, GELU backward + column sums) under their A/B knobs
+      timeout -k 10 300 python -u tools/norm_bench.py > "$OUT/norm_bench.log" 2>&1 ;;
+    attngemm)  # planner A/B on the joint attention's batched dK / dV and the action expert's 1280-row GEMMs
+      timeout -k 10 300 python -u tools/attn_gemm_ab.py > "$OUT/attn_gemm_ab.log" 2>&1 ;;
+    ntab)  # non-temporal weight-stream loads (default) vs PZ_W_NT=0 on the C4 / C5 inference graphs, interleaved
+      for kv in base PZ_W_NT=0 base PZ_W_NT=0; do
+        if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
+        env "${envs[@]}" timeout -k 10 300 python -u tools/infer_bench.py --iters 50 > "$OUT/ab.tmp" 2>&1
+        echo "$kv C4 $(grep -o 'graph [0-9.]* ms' "$OUT/ab.tmp")" >> "$OUT/ntab.log"
+        env "${envs[@]}" timeout -k 10 300 python -u tools/c5_bench.py --iters 20 > "$OUT/ab.tmp" 2>&1
+        echo "$kv C5 $(grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' "$OUT/ab.tmp" | tr '\n' ' ')" >> "$OUT/ntab.log"
+      done
+      rm -f "$OUT/ab.tmp" ;;
     census)
       timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-256} > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -938,7 +938,8 @@ __device__ __forceinline__ void epilogue8p(const GemmP& p, int64_t cofs, int64_t
           const int row = wr * 128 + rb * 16 + rl, col = wc * 32 + j * 16 + g4;
           img_put(smem, row, col, u32x2{pack2bf(hh[0], hh[1]), pack2bf(hh[2], hh[3])});
           img_put(smem + 65536, row, col, u32x2{pack2bf(gg[0], gg[1]), pack2bf(gg[2], gg[3])});
-          *reinterpret_cast<u32x2*>(Ur + j * 16) = pk4(uu);
+          if (p.nt_aux) __builtin_nontemporal_store(pk4(uu), reinterpret_cast<u32x2*>(Ur + j * 16));
+          else *reinterpret_cast<u32x2*>(Ur + j * 16) = pk4(uu);
         }
       }
       lds_sync();
@@ -2017,12 +2018,12 @@ Plan make_plan(const pz_gemm_args* a) {
   // are faster on 128-row tiles); PZ_GEMM_256_MINM overrides (A/B runs)
   const char* mm = getenv("PZ_GEMM_256_MINM");
   const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192) ? 256 : 512);
-  // fewer 256-tiles than CUs at short K (the action expert's 1024- and 1280-row GEMMs at micro-batch 256): the 128-tile
+  // at most half a round of 256-tiles at short K (the action expert's 1024- and 1280-row GEMMs at micro-batch 256): the 128-tile
   // kernel (+ split-K) beats the 256-tile split tail, 22-37 vs 29-45 us per launch, except at K 8192
   // (tools/attn_gemm_ab.py, profiles/r05/attn_gemm_ab.log); PZ_GEMM_SMALL256=1 keeps the 256 path (A/B)
   const char* es2 = getenv("PZ_GEMM_SMALL256");
   const bool small_short = !pl.geglu && a->batch == 1 && a->M >= 1024 && a->K <= 4096 &&
-                           ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) < device_cus() && !(es2 && es2[0] == '1');
+                           ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) <= 128 && !(es2 && es2[0] == '1');
   if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= (pl.geglu ? 256 : 512) &&
       !small_short) {
     const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;

@@ -48,9 +48,6 @@ struct GemmP {
   // ... and for the saved activations only (aux: GeGLU g|u, GELU / SiLU pre-activation -- read again only by the
   // backward, long after; PZ_GEMM_NT_AUX, read per call)
   int nt_aux;
-  // few-row weight-streaming kernels (gemm_skinny64_kernel): non-temporal weight loads (PZ_W_NT, read per call;
-  // default on) -- a denoise step's weights are read once and exceed the MALL
-  int w_nt;
 };
 
 namespace {

@@ -221,17 +221,14 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   const int64_t kchunks = split ? min(kchunks_all - kz0, p.ksplit / 64) : kchunks_all;
   const int64_t per = (kchunks + W - 1) / W;
   const int64_t kb = kz0 + wave * per, ke = kz0 + min(kchunks, (int64_t)(wave + 1) * per);
-  // weights: streamed once, non-temporal loads unless PZ_W_NT=0 (p.w_nt; one copy of the loop per policy)
-  auto body = [&](auto NT_) {
-  constexpr bool NT = decltype(NT_)::value;
   auto load_b = [&](const char* row, int64_t c, bf16x8& lo, bf16x8& hi) {
     if (!nok) {
       lo = hi = bf16x8{};
     } else if (F8W) {
-      fp8x16_to_bf16(ld16_stream<NT>(row + c * 64), lo, hi);
+      fp8x16_to_bf16(*reinterpret_cast<const u32x4*>(row + c * 64), lo, hi);
     } else {
-      lo = __builtin_bit_cast(bf16x8, ld16_stream<NT>(row + c * 128));
-      hi = __builtin_bit_cast(bf16x8, ld16_stream<NT>(row + c * 128 + 16));
+      lo = *reinterpret_cast<const bf16x8*>(row + c * 128);
+      hi = *reinterpret_cast<const bf16x8*>(row + c * 128 + 16);
     }
   };
   int64_t kc = kb;
@@ -243,8 +240,8 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
 #pragma unroll
       for (int u = 0; u < UU; ++u) {
         if (F8W) {  // raw codes first (all loads in flight), expanded after the A loads are issued
-          braw[u] = nok ? ld16_stream<NT>(Brow + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
-          if (geglu) braw2[u] = nok ? ld16_stream<NT>(Brow2 + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+          braw[u] = nok ? *reinterpret_cast<const u32x4*>(Brow + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
+          if (geglu) braw2[u] = nok ? *reinterpret_cast<const u32x4*>(Brow2 + (kc + u) * 64) : u32x4{0u, 0u, 0u, 0u};
         } else {
           load_b(Brow, kc + u, b[u][0], b[u][1]);
           if (geglu) load_b(Brow2, kc + u, b2[u][0], b2[u][1]);
@@ -289,9 +286,6 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   };
   run(std::integral_constant<int, U>{});
   run(std::integral_constant<int, 1>{});
-  };
-  if (p.w_nt) body(std::true_type{});
-  else body(std::false_type{});
   // D[n_local = 4g + r][m = mb*16 + (lane & 15)]; wave w < MB finishes row block w
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
@@ -471,8 +465,6 @@ static int launch_sk64_any(const GemmP& p, int w, int nc, int mb, int64_t tn, hi
   return launch_sk64_nc<4, 4, F8W>(p, nc, tn, st);
 }
 
-int pz_sk64_launch(const GemmP& p0, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st) {
-  GemmP p = p0;
-  p.w_nt = pz_weight_nt();
+int pz_sk64_launch(const GemmP& p, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st) {
   return f8w ? launch_sk64_any<true>(p, w, nc, mb, tiles_n, st) : launch_sk64_any<false>(p, w, nc, mb, tiles_n, st);
 }

@@ -8,7 +8,8 @@ gradient-arena slice on the communication stream while the backward continues; `
 the rest and makes the compute stream wait.  Asserts: the RCCL (async) branch ran, buckets were
 enqueued during the backward (before the flush), every slice of the trainable arena was reduced once,
 and the gradient arena is BITWISE equal to the same backward without the wrapper.  ``no_sync`` leaves
-the reducer idle.
+the reducer idle.  A third step delays the engine's expert side stream and snapshots every bucket on the
+communication stream after its collective: each snapshot equals the final gradients.
 """
 
 import os
@@ -99,6 +100,41 @@ def _worker(port, q):
                                      for r in ("action", "vlm") if r in ar.region_range)
         res["bitwise_equal"] = torch.equal(ar.grad, gref)
         res["max_abs_diff"] = float((ar.grad.float() - gref.float()).abs().max())
+        # the communication stream must wait for the expert side stream before each bucket.  Delay the
+        # side stream (a ~20 ms spin before every layer's expert q|k|v backward) and snapshot each bucket's slice
+        # on the communication stream right after its all_reduce: every snapshot must equal the final gradients
+        # (a bucket that read its slice before the side stream's wgrads landed would differ)
+        snaps = []
+        red.finish = orig_finish
+        eng.post_backward = None
+
+        def launch_snap(region, lo, hi, streams=()):
+            orig_launch(region, lo, hi, streams)
+            with torch.cuda.stream(red.stream):
+                snaps.append((lo, hi, m._arena.grad[lo:hi].clone()))
+
+        red._launch = launch_snap
+        orig_qkv = eng._qkv_backward
+        main_stream = torch.cuda.current_stream()
+        delayed = {"n": 0}
+
+        def qkv_delayed(*a, **k):
+            if torch.cuda.current_stream() != main_stream:
+                torch.cuda._sleep(40_000_000)
+                delayed["n"] += 1
+            return orig_qkv(*a, **k)
+
+        eng._qkv_backward = qkv_delayed
+        m.zero_grad(set_to_none=True)
+        loss = w(**kw)
+        eng.post_backward = red.finish
+        loss.backward()
+        torch.cuda.synchronize()
+        eng._qkv_backward = orig_qkv
+        res["side_delays"] = delayed["n"]
+        res["snapshots"] = len(snaps)
+        res["snapshots_final"] = all(torch.equal(sn, m._arena.grad[lo:hi]) for lo, hi, sn in snaps)
+        res["delayed_bitwise_equal"] = torch.equal(m._arena.grad, gref)
         dist.destroy_process_group()
         q.put(res)
     except Exception as e:  # pragma: no cover
@@ -125,3 +161,6 @@ def test_rccl_reducer_branch_world1_bitwise():
     assert res["during_backward"] >= 2, res  # enqueued while the backward was still running
     assert res["reduced_elems"] == res["trainable_elems"], res  # each final slice reduced exactly once
     assert res["bitwise_equal"], res
+    assert res["side_delays"] >= 1 and res["snapshots"] >= 3, res  # the side stream ran (and was delayed)
+    assert res["snapshots_final"], res  # every collective read the finished slice, side-stream wgrads included
+    assert res["delayed_bitwise_equal"], res

@@ -804,13 +804,14 @@ def test_time_embed_modes_match_reference():
 
 @pytest.mark.parametrize("mode", ["mfma", "mfma_wg64"])
 @pytest.mark.parametrize("B,T,cnts,P", [(1, 4, [270], 276), (2, 4, [276, 259], 276), (1, 2, [100], 276),
-                                          (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276)])
+                                          (2, 1, [5, 276], 276), (1, 50, [788], 788), (2, 13, [276, 200], 276),
+                                          (3, 4, [300, 20, 311], 311), (1, 4, [7], 7)])
 def test_decode_attn_matches_reference(B, T, cnts, P, mode, monkeypatch):
     """pz_decode_attn (denoise attention: T action tokens x 8 heads vs the cached keys, MQA) vs fp32 torch
     with the Gemma soft-cap and the Pi0 block mask (joint_model.py:259-292, pizero.py:271-306); T = 50 at
-    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile.  mode "mfma": the
-    key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default); "mfma_wg64": several chunks
-    per workgroup (online softmax across chunks) + merge"""
+    P = 788 is C5's chunk (400 query rows = 13 row tiles), T = 13 a ragged last tile, 3 samples with 316 keys, 12 keys =
+    one partial chunk.  mode "mfma": the key-split MFMA kernel (P.V on the matrix cores) + fixed-order merge (default);
+    "mfma_wg64": several chunks per workgroup (online softmax across chunks) + merge"""
     from pizero_native import ops
 
     if mode == "mfma_wg64":

@@ -110,13 +110,13 @@ PY
       timeout -k 10 300 python -u tools/norm_bench.py > "$OUT/norm_bench.log" 2>&1 ;;
     attngemm)  # planner A/B on the joint attention's batched dK / dV and the action expert's 1280-row GEMMs
       timeout -k 10 300 python -u tools/attn_gemm_ab.py > "$OUT/attn_gemm_ab.log" 2>&1 ;;
-    ntab)  # non-temporal weight-stream loads (default) vs PZ_W_NT=0 on the C4 / C5 inference graphs, interleaved
-      for kv in base PZ_W_NT=0 base PZ_W_NT=0; do
+    infab)  # inference knobs on the C4 / C5 graphs, interleaved (KNOBS: "base" = defaults, or VAR=value each)
+      for kv in ${KNOBS:-base PZ_W_NT=0 base PZ_W_NT=0}; do
         if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
         env "${envs[@]}" timeout -k 10 300 python -u tools/infer_bench.py --iters 50 > "$OUT/ab.tmp" 2>&1
-        echo "$kv C4 $(grep -o 'graph [0-9.]* ms' "$OUT/ab.tmp")" >> "$OUT/ntab.log"
+        echo "$kv C4 $(grep -o 'graph [0-9.]* ms' "$OUT/ab.tmp")" >> "$OUT/infab.log"
         env "${envs[@]}" timeout -k 10 300 python -u tools/c5_bench.py --iters 20 > "$OUT/ab.tmp" 2>&1
-        echo "$kv C5 $(grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' "$OUT/ab.tmp" | tr '\n' ' ')" >> "$OUT/ntab.log"
+        echo "$kv C5 $(grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' "$OUT/ab.tmp" | tr '\n' ' ')" >> "$OUT/infab.log"
       done
       rm -f "$OUT/ab.tmp" ;;
     census)

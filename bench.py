@@ -67,12 +67,13 @@ def synthetic_batch(model, B, device, gen):
 
 def pmc_traffic(kname, shape):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (profiles/r04/pmc_dominant.json, else the round-3 file; tools/pmc_dominant.sh + tools/pmc_summary.py):
+    (the newest of profiles/r05, r04, r03 pmc_dominant.json; tools/pmc_dominant.sh + tools/pmc_summary.py):
     FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another
     kernel/shape."""
-    path = os.path.join(ROOT, "profiles", "r04", "pmc_dominant.json")
-    if not os.path.exists(path):
-        path = os.path.join(ROOT, "profiles", "r03", "pmc_dominant.json")
+    for rnd in ("r05", "r04", "r03"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_dominant.json")
+        if os.path.exists(path):
+            break
     try:
         with open(path) as f:
             pm = json.load(f)

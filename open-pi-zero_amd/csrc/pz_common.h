@@ -72,19 +72,6 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));  // e^{-2u}
   return x * fast_rcp(1.f + e);
 }
-// 16-byte load of a streamed-once operand (decode weights): NT = non-temporal (no L2 / MALL allocation)
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16_stream(const void* ptr) {
-  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(ptr));
-  else return *reinterpret_cast<const u32x4*>(ptr);
-}
-
-// weight-stream load policy knob (host): PZ_W_NT=0 -> default policy; read per call
-static inline bool pz_weight_nt() {
-  const char* e = getenv("PZ_W_NT");
-  return !(e && e[0] == '0');
-}
-
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   float x2 = x * x;

@@ -37,7 +37,6 @@ struct GemvP {
   const float* cs;
   bf16_t *q, *k, *v;
   int64_t T, nh, hd, Lq, qoff, Lk, koff;
-  int wnt;  // non-temporal weight loads (pz_weight_nt)
 };
 
 __device__ __forceinline__ void unpack8(const u32x4& r, float (&f)[8]) {
@@ -49,9 +48,9 @@ __device__ __forceinline__ void unpack8(const u32x4& r, float (&f)[8]) {
 }
 
 // Main body: accumulate acc[r][c] over this thread's k chunks (rows r < M of x, CW weight rows)
-template <int MR, int CW, int TPG, bool NT>
-__device__ __forceinline__ void gemv_body_p(const GemvP& p, const int64_t* wrow, const bool* wok, int j,
-                                            float (&acc)[MR][CW], float (&ss)[MR]) {
+template <int MR, int CW, int TPG>
+__device__ __forceinline__ void gemv_body(const GemvP& p, const int64_t* wrow, const bool* wok, int j,
+                                          float (&acc)[MR][CW], float (&ss)[MR]) {
   const int64_t KC = p.K / 8;
 #pragma unroll
   for (int r = 0; r < MR; ++r) {
@@ -64,7 +63,7 @@ __device__ __forceinline__ void gemv_body_p(const GemvP& p, const int64_t* wrow,
     u32x4 wr[CW];
 #pragma unroll
     for (int c = 0; c < CW; ++c)
-      wr[c] = wok[c] ? ld16_stream<NT>(p.W + wrow[c] * p.ldw + kc * 8) : u32x4{0u, 0u, 0u, 0u};
+      wr[c] = wok[c] ? *reinterpret_cast<const u32x4*>(p.W + wrow[c] * p.ldw + kc * 8) : u32x4{0u, 0u, 0u, 0u};
     u32x4 xr[MR];
 #pragma unroll
     for (int r = 0; r < MR; ++r)
@@ -91,13 +90,6 @@ __device__ __forceinline__ void gemv_body_p(const GemvP& p, const int64_t* wrow,
       }
     }
   }
-}
-
-template <int MR, int CW, int TPG>
-__device__ __forceinline__ void gemv_body(const GemvP& p, const int64_t* wrow, const bool* wok, int j,
-                                          float (&acc)[MR][CW], float (&ss)[MR]) {
-  if (p.wnt) gemv_body_p<MR, CW, TPG, true>(p, wrow, wok, j, acc, ss);
-  else gemv_body_p<MR, CW, TPG, false>(p, wrow, wok, j, acc, ss);
 }
 
 // Reduce acc / ss over the TPG threads of each group through LDS (a shuffle tree per accumulator
@@ -302,7 +294,6 @@ int pz_gemv_launch(const pz_gemm_args* a, hipStream_t st) {
   p.ldaux = a->ld_aux;
   p.nw = (const bf16_t*)a->norm_w;
   p.neps = a->norm_eps;
-  p.wnt = pz_weight_nt();
   // columns per group: >= 256 workgroups for the Pi0 widths (N = 1024: 4 -> 256; GeGLU I = 4096: 4 -> 512)
   if (a->M <= 4) {
     if (geglu) return launch_gemv<4, 4, true>(p, st);
@@ -346,7 +337,6 @@ extern "C" int pz_gemv_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
   p.qoff = a->qoff;
   p.Lk = a->Lk;
   p.koff = a->koff;
-  p.wnt = pz_weight_nt();
   hipStream_t st = (hipStream_t)stream;
   const int64_t pairs = a->N / 2, KC = a->K / 8;
   // 2 pairs per group: N = 2560 -> 1280 pairs -> 320 workgroups at K = 1024 (2 groups of 128 threads)

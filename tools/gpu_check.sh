@@ -111,7 +111,7 @@ PY
     attngemm)  # planner A/B on the joint attention's batched dK / dV and the action expert's 1280-row GEMMs
       timeout -k 10 300 python -u tools/attn_gemm_ab.py > "$OUT/attn_gemm_ab.log" 2>&1 ;;
     infab)  # inference knobs on the C4 / C5 graphs, interleaved (KNOBS: "base" = defaults, or VAR=value each)
-      for kv in ${KNOBS:-base PZ_W_NT=0 base PZ_W_NT=0}; do
+      for kv in ${KNOBS:-base base}; do
         if [ "$kv" = base ]; then envs=(); else envs=("$kv"); fi
         env "${envs[@]}" timeout -k 10 300 python -u tools/infer_bench.py --iters 50 > "$OUT/ab.tmp" 2>&1
         echo "$kv C4 $(grep -o 'graph [0-9.]* ms' "$OUT/ab.tmp")" >> "$OUT/infab.log"

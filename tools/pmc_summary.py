@@ -38,14 +38,21 @@ def mean(x):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    M, N, K = int(os.environ.get("PMC_M", "70656")), 32768, 2048
-    kern = sys.argv[3] if len(sys.argv) > 3 else "gemm8p_kernel<true, true, true"
+    dgeglu = os.environ.get("PMC_LAYOUT") == "DGEGLU"  # the down-proj dgrad + GeGLU derivative (pmcdgeglu passes)
+    if dgeglu:  # d(g|u)[M, 2I] from dy[M, H] W_down[H, I]: reads dy, W, g|u; writes d(g|u)
+        M, N, K = int(os.environ.get("PMC_M", "70656")), 16384, 2048
+    else:
+        M, N, K = int(os.environ.get("PMC_M", "70656")), 32768, 2048
+    kern = sys.argv[3] if len(sys.argv) > 3 else ("gemm8k_kernel<true, false" if dgeglu else "gemm8p_kernel<true, true, true")
     name, fetch, d1 = per_dispatch(os.path.join(src, "fetch", "fetch_counter_collection.csv"), kern)
     _, write, d2 = per_dispatch(os.path.join(src, "write", "write_counter_collection.csv"), kern)
     _, sq, d3 = per_dispatch(os.path.join(src, "sq", "sq_counter_collection.csv"), kern)
     fetch_raw = mean(fetch["FETCH_SIZE"]) * 1024
     write_b = mean(write["WRITE_SIZE"]) * 1024
-    algo = 2 * (M * K + N * K) + 2 * M * (N // 2) + 2 * M * N  # A + B read, h + saved g|u written
+    if dgeglu:
+        algo = 2 * (M * K + N * K) + 2 * (2 * M * 2 * N)  # dy + W read, g|u read and d(g|u) written
+    else:
+        algo = 2 * (M * K + N * K) + 2 * M * (N // 2) + 2 * M * N  # A + B read, h + saved g|u written
     mfma_cyc = mean(sq["SQ_VALU_MFMA_BUSY_CYCLES"])
     gui = mean(fetch["GRBM_GUI_ACTIVE"])
     ms = mean(d1)

@@ -2017,15 +2017,20 @@ Plan make_plan(const pz_gemm_args* a) {
   // at B=1, 276 rows: 64 vs 78 us and 51 vs 56 us measured), 512 otherwise (narrow prefill GEMMs
   // are faster on 128-row tiles); PZ_GEMM_256_MINM overrides (A/B runs)
   const char* mm = getenv("PZ_GEMM_256_MINM");
-  const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192) ? 256 : 512);
+  const int64_t min_m = mm ? atoll(mm) : ((pl.geglu || a->K >= 8192 || (a->batch > 1 && !pl.akc && !pl.bkc)) ? 256 : 512);
   // at most half a round of 256-tiles at short K (the action expert's 1024- and 1280-row GEMMs at micro-batch 256): the 128-tile
   // kernel (+ split-K) beats the 256-tile split tail, 22-37 vs 29-45 us per launch, except at K 8192
   // (tools/attn_gemm_ab.py, profiles/r05/attn_gemm_ab.log); PZ_GEMM_SMALL256=1 keeps the 256 path (A/B)
   const char* es2 = getenv("PZ_GEMM_SMALL256");
   const bool small_short = !pl.geglu && a->batch == 1 && a->M >= 1024 && a->K <= 4096 &&
                            ((a->M + BT - 1) / BT) * ((ncols + cw - 1) / cw) <= 128 && !(es2 && es2[0] == '1');
-  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= (pl.geglu ? 256 : 512) &&
-      !small_short) {
+  // batched TN GEMMs with >= 256 x 256 outputs per batch entry (the joint attention's dK = dS^T Q and dV = P^T dO,
+  // 288 x 256 per sample): the 256-tile kernel, two row tiles per sample, 173 vs 190-203 us (dV of the 5-row action
+  // mixture 28.7 vs 40.6 us) against the 128-tile kernel (tools/attn_gemm_ab.py, profiles/r05/attn_gemm_ab_r5s.log)
+  const bool batched_tn = a->batch > 1 && !pl.akc && !pl.bkc && a->M >= 256 && ncols >= 256;
+  const char* mn = getenv("PZ_GEMM_256_MINN");  // A/B: output columns from which the 256-tile path is tried
+  const int64_t min_n = mn ? atoll(mn) : (pl.geglu || batched_tn ? 256 : 512);
+  if ((use_8phase() ? a->K % 8 == 0 : a->K % BK256 == 0) && a->M >= min_m && ncols >= min_n && !small_short) {
     const int64_t tm = (a->M + BT - 1) / BT, tn = (ncols + cw - 1) / cw;
     Plan cand = pl;
     cand.kind = PATH_256;

@@ -83,11 +83,32 @@ def test_all_four_layouts_batched_fp32_out():
             close(C, ref, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("K", [2208, 40, 200])
+def test_batched_tn_256_tile(K):
+    """Batched TN GEMMs with >= 256 x 256 outputs per entry (the joint attention's dK = dS^T Q, dV = P^T dO: 288 x 256
+    per sample, K = vlm rows x heads 2208 or the action mixture's 40 with beta accumulation) take the 256-tile kernel:
+    two row tiles per sample, the second with 32 rows; bf16 out, then accumulated (beta) -- vs fp32 torch"""
+    from pizero_native import ops
+
+    Bt, M, N = 96, 288, 256  # >= 160 workgroups (2 row tiles x 96): the 256-tile path's fill threshold
+    assert ops.gemm_kernel_name(M, N, K, a_kc=False, b_kc=False, batch=Bt).startswith("gemm8k_kernel<false, false")
+    At = bf(Bt, K, M, scale=0.5)  # k-strided A (dS / P as stored: [rows x heads][keys])
+    Bk = bf(Bt, K, N, scale=0.5)  # k-strided B (Q / dO)
+    ref = At.float().transpose(1, 2) @ Bk.float()
+    C = torch.empty(Bt, M, N, device=dev, dtype=torch.bfloat16)
+    kw = dict(batch=Bt, sA=(M * K, 0), sB=(N * K, 0), sC=(M * N, 0))
+    ops.gemm(M, N, K, At, M, False, Bk, N, False, C, N, **kw)
+    close(C, ref, atol=3e-2 * math.sqrt(K) / 8)
+    ops.gemm(M, N, K, At, M, False, Bk, N, False, C, N, beta=True, **kw)
+    close(C, 2 * ref, atol=6e-2 * math.sqrt(K) / 8)
+
+
 @pytest.mark.parametrize("xcd", ["1", "0"])
 def test_batched_xcd_grouped_layouts(xcd):
     """batch % 8 == 0 launches of the 128-tile kernel take the XCD-grouped 1-D grid (a batch entry's tiles
-    on one XCD; PZ_GEMM_BATCH_XCD=0 = the 2-D grid): every layout, the joint-attention dK shape, fp32 and
-    bf16 outputs, beta accumulation -- run in a subprocess because the switch is read once per process"""
+    on one XCD; PZ_GEMM_BATCH_XCD=0 = the 2-D grid): every layout (the TN one of the 288 x 256 shape = the joint
+    attention's dK takes the 256-tile kernel), fp32 and bf16 outputs, beta accumulation -- run in a subprocess
+    because the switch is read once per process"""
     import subprocess
     import sys
 

@@ -37,7 +37,8 @@ SHAPES = [
 ]
 VARIANTS = [("default", {}), ("no tail", {"PZ_GEMM_TAIL": "0"}), ("128-tile", {"PZ_GEMM_256_MINM": "1000000"}),
             ("256 any", {"PZ_GEMM_256_MINM": "1", "PZ_GEMM_256_MINUNITS": "1"}),
-            ("256 any, no tail", {"PZ_GEMM_256_MINM": "1", "PZ_GEMM_256_MINUNITS": "1", "PZ_GEMM_TAIL": "0"})]
+            ("256 any, no tail", {"PZ_GEMM_256_MINM": "1", "PZ_GEMM_256_MINUNITS": "1", "PZ_GEMM_TAIL": "0"}),
+            ("256 N>=256", {"PZ_GEMM_256_MINM": "1", "PZ_GEMM_256_MINN": "256"})]
 
 
 def main():

@@ -119,6 +119,16 @@ PY
         echo "$kv C5 $(grep -o '"graph_ms": [0-9.]*\|"fp8_graph_ms": [0-9.]*' "$OUT/ab.tmp" | tr '\n' ' ')" >> "$OUT/infab.log"
       done
       rm -f "$OUT/ab.tmp" ;;
+    optbench)  # the 8-bit AdamW step over a Pi0-sized arena
+      timeout -k 10 300 python -u tools/optim_bench.py > "$OUT/optim_bench.log" 2>&1 ;;
+    optprof)  # kernel times of the 8-bit AdamW step (this build, and the build in ab_old/ when present)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/optprof" -o opt \
+        -- python3 tools/optim_bench.py > "$OUT/optprof.log" 2>&1
+      if [ -f ab_old/libpizero_hip.so ]; then
+        PZ_LIB_PATH=$PWD/ab_old/libpizero_hip.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$OUT/optprof_old" -o opt -- python3 tools/optim_bench.py > "$OUT/optprof_old.log" 2>&1
+      fi
+      rm -f "$OUT"/optprof*/*kernel_trace.csv "$OUT"/optprof*/*/*kernel_trace.csv ;;
     census)
       timeout -k 10 300 python -u tools/gemm_census.py --micro-batch ${CENSUS_MB:-256} > "$OUT/gemm_census.log" 2>&1 ;;
     *) echo "unknown step $s"; exit 2 ;;

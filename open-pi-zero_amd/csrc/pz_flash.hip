@@ -2345,6 +2345,8 @@ __device__ __forceinline__ void fs_load_rows(bf16x8 (&f)[3], const bf16_t* row, 
   }
 }
 
+#ifdef PZ_FLASH_AB
+// (A/B builds only, -DPZ_FLASH_AB: the default dQ kernel computes delta itself)
 // delta[zh][r] = sum_d dO[r][d] O[r][d] for the SigLIP shape (head 72, one output group): one thread per (token,
 // head), the 16 heads of a token row on 16 adjacent lanes (their 144-B segments tile the row), 9 + 9 16-B loads
 __global__ void __launch_bounds__(256) flash_delta72_kernel(pz_flash_args a) {
@@ -2370,6 +2372,7 @@ __global__ void __launch_bounds__(256) flash_delta72_kernel(pz_flash_args a) {
     }
   a.delta[(b * a.H + h) * a.nq + r] = acc;
 }
+#endif  // PZ_FLASH_AB
 
 // dQ with K / V resident (delta = rowsum(dO O) from flash_bwd_prep_kernel): wave w owns query rows 32w ..
 // 32w + 31; the next unit's Q / dO rows, lse and delta (inline-asm loads) and K / V images (LDS-DMA) are issued
@@ -3231,11 +3234,16 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {
       const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
-      const char* eq = getenv("PZ_SIG_QB");  // "2": 8 waves of 32 rows (A/B runs); default 16 waves of 16 rows
+#ifdef PZ_FLASH_AB
+      const char* eq = getenv("PZ_SIG_QB");  // "2": 8 waves of 32 rows (A/B builds); default 16 waves of 16 rows
       if (eq && eq[0] == '2') {
         fa_smem_attr(flash_fwd_sig_kernel<2>, FS_SMEM, attr3);
         hipLaunchKernelGGL(flash_fwd_sig_kernel<2>, dim3((unsigned)G), dim3(8 * 64), FS_SMEM, st, *a, G);
-      } else {
+      } else
+#else
+      (void)attr3;
+#endif
+      {
         static bool attr4 = false;
         fa_smem_attr(flash_fwd_sig_kernel<1>, FS_SMEM, attr4);
         hipLaunchKernelGGL(flash_fwd_sig_kernel<1>, dim3((unsigned)G), dim3(16 * 64), FS_SMEM, st, *a, G);
@@ -3286,8 +3294,16 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
                "flash_fwd_probs: operands need 16-byte aligned rows");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z * a->H < 65536, "flash_fwd_probs: nq / units too large");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
-  const char* e = getenv("PZ_PROBS_DMA");  // "0": the register-staged kernel (A/B runs)
-  if (!(e && e[0] == '0')) {
+#ifdef PZ_FLASH_AB
+  const char* e = getenv("PZ_PROBS_DMA");  // "0": the round-4 register-staged kernel (A/B builds)
+  if (e && e[0] == '0') {
+    hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
+                       (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
+    PZ_CHECK_LAUNCH();
+    return PZ_OK;
+  }
+#endif
+  {
     static bool attr0 = false, attr1 = false;
     if (a->cap > 0.f) {
       fa_smem_attr(flash_fwd_probs_dma_kernel<true>, JD_SMEM, attr1);
@@ -3301,10 +3317,6 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
     PZ_CHECK_LAUNCH();
     return PZ_OK;
   }
-  hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
-                     (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
-  PZ_CHECK_LAUNCH();
-  return PZ_OK;
 }
 
 extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void* tcap, void* dS, int64_t ldp,
@@ -3325,17 +3337,19 @@ extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void
                  "flash_bwd_ds: dQ needs K (16-byte rows) and an 8-byte aligned dQ");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_bwd_ds: too many units");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
-  const char* e = getenv("PZ_PROBS_DMA");  // "0": the register-staged kernel (A/B runs)
-  if (!(e && e[0] == '0')) {
-    static bool attr = false;
-    fa_smem_attr(flash_bwd_ds_dma_kernel, JD_SMEM, attr);
-    hipLaunchKernelGGL(flash_bwd_ds_dma_kernel, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
+#ifdef PZ_FLASH_AB
+  const char* e = getenv("PZ_PROBS_DMA");  // "0": the round-4 register-staged kernel (A/B builds)
+  if (e && e[0] == '0') {
+    hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
                        (hipStream_t)stream, *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
     PZ_CHECK_LAUNCH();
     return PZ_OK;
   }
-  hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0, (hipStream_t)stream,
-                     *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
+#endif
+  static bool attr = false;
+  fa_smem_attr(flash_bwd_ds_dma_kernel, JD_SMEM, attr);
+  hipLaunchKernelGGL(flash_bwd_ds_dma_kernel, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
+                     (hipStream_t)stream, *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
@@ -3373,15 +3387,20 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
       const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
-      const char* ed = getenv("PZ_SIG_DELTA");  // "pass": the separate delta pass (A/B runs)
       fa_smem_attr(flash_bwd_kv_sig_kernel, FS_SMEM, akv3);
+#ifdef PZ_FLASH_AB
+      const char* ed = getenv("PZ_SIG_DELTA");  // "pass": the separate delta pass (A/B builds)
       if (ed && ed[0] == 'p') {
         const int64_t rows = a->Z * a->H * a->nq;
         hipLaunchKernelGGL(flash_delta72_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, *a);
         PZ_CHECK_LAUNCH();
         fa_smem_attr(flash_bwd_q_sig_kernel<false>, FS_SMEM, aq3);
         hipLaunchKernelGGL(flash_bwd_q_sig_kernel<false>, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
-      } else {
+      } else
+#else
+      (void)aq3;
+#endif
+      {
         static bool aq4 = false;
         fa_smem_attr(flash_bwd_q_sig_kernel<true>, FS_SMEM, aq4);
         hipLaunchKernelGGL(flash_bwd_q_sig_kernel<true>, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);

@@ -484,9 +484,9 @@ extern "C" int64_t pz_norm_rows_per_part(void) { return ROWS_PER_PART; }
 // loads are issued before the current row's reductions (two rows in flight per workgroup); the two
 // row sums go through a double-buffered LDS slot (one barrier per row).  The wave-per-row kernels
 // above hold MAXC x 8 accumulators per thread (2 waves / SIMD at D >= 1152): PZ_NORM_BWD=wave (A/B).
-// PF = rows loaded ahead (1: the next row; 2: the next two -- three rows of x / dy / residual gradient in
-// flight per workgroup, so a partly filled last round of workgroups is not latency-bound: 70656 Gemma rows
-// are 4416 parts of 16 rows = 2.16 rounds of 2048 resident workgroups).  PZ_NORM_PF=1 (A/B).
+// PF = rows loaded ahead (2: three rows of x / dy / residual gradient in flight per workgroup, so a partly filled
+// last round of workgroups is not latency-bound; PF = 1 measured 138 vs 131.5 us at 65536 x 1152,
+// profiles/r05/norm_bench.log).
 template <bool LN, int PF>
 __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
     const bf16_t* __restrict__ dy, int64_t lddy, const bf16_t* __restrict__ x, int64_t ldx,
@@ -605,10 +605,7 @@ static bool norm_bwd_rows() {
   return !(e && e[0] == 'w');
 }
 
-static bool norm_bwd_pf1() {
-  const char* e = getenv("PZ_NORM_PF");
-  return e && e[0] == '1';
-}
+
 
 #define NORM_DISPATCH(KERNEL, GRID, ...)                                                   \
   do {                                                                                    \
@@ -649,7 +646,7 @@ extern "C" int pz_rmsnorm_bwd(const void* dy, int64_t lddy, const void* x, int64
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16))
-    hipLaunchKernelGGL((norm_bwd_pf1() ? norm_bwd_row_kernel<false, 1> : norm_bwd_row_kernel<false, 2>), grid,
+    hipLaunchKernelGGL((norm_bwd_row_kernel<false, 2>), grid,
                        dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w, nullptr,
                        rstd, (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, nullptr, R, (int)D, nullptr);
   else
@@ -683,7 +680,7 @@ extern "C" int pz_layernorm_bwd(const void* dy, int64_t lddy, const void* x, int
   dim3 grid((unsigned)((R + ROWS_PER_PART - 1) / ROWS_PER_PART));
   if (norm_bwd_rows() && PZ_ALIGNED(dy, 16) && (!dres || PZ_ALIGNED(dres, 16)) && PZ_ALIGNED(dw_part, 16) &&
       PZ_ALIGNED(db_part, 16) && (!dx_part || PZ_ALIGNED(dx_part, 16)))
-    hipLaunchKernelGGL((norm_bwd_pf1() ? norm_bwd_row_kernel<true, 1> : norm_bwd_row_kernel<true, 2>), grid,
+    hipLaunchKernelGGL((norm_bwd_row_kernel<true, 2>), grid,
                        dim3(256), 0, st, (const bf16_t*)dy, lddy, (const bf16_t*)x, ldx, (const bf16_t*)w, mean, rstd,
                        (const bf16_t*)dres, (bf16_t*)dx, lddx, dw_part, db_part, R, (int)D, dx_part);
   else if (dx_part)

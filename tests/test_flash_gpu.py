@@ -62,9 +62,8 @@ def ref_attention(q, k, v, scale, cap=0.0, allowed=None, dead=None):
     return p @ v, lse
 
 
-@pytest.mark.parametrize("unit,sig,B,qb", [("0", "0", 3, "1"), ("1", "0", 3, "1"), ("1", "1", 3, "1"), ("1", "1", 40, "1"),
-                                           ("1", "1", 40, "2")])
-def test_flash_fwd_siglip(unit, sig, B, qb, monkeypatch):
+@pytest.mark.parametrize("unit,sig,B", [("0", "0", 3), ("1", "0", 3), ("1", "1", 3), ("1", "1", 40)])
+def test_flash_fwd_siglip(unit, sig, B, monkeypatch):
     """the SigLIP forward kernel families: 2 workgroups per unit (few units), one workgroup per unit, and the
     persistent pipelined kernel (B = 40: 640 units over the CUs, several units per workgroup with a ragged
     last round, XCD-grouped unit order)"""
@@ -72,7 +71,6 @@ def test_flash_fwd_siglip(unit, sig, B, qb, monkeypatch):
 
     monkeypatch.setenv("PZ_FLASH_UNIT", unit)
     monkeypatch.setenv("PZ_FLASH_SIG", sig)
-    monkeypatch.setenv("PZ_SIG_QB", qb)  # persistent forward: 16 waves x 16 rows (1) or 8 x 32 (2)
 
     nh, hd, N = 16, 72, 256
     qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
@@ -117,15 +115,13 @@ def test_flash_fwd_joint_block_mask(cnt, key_split):
     close(lse.view(B, L, nh), rlse.permute(0, 2, 1), rtol=1e-3, atol=2e-3)
 
 
-@pytest.mark.parametrize("dma", ["1", "0"])
 @pytest.mark.parametrize("cnt", [[276, 276, 276], [276, 250, 9]])
-def test_flash_fwd_probs_joint_block_mask(cnt, dma, monkeypatch):
+def test_flash_fwd_probs_joint_block_mask(cnt):
     """pz_flash_fwd_probs (training-default joint forward): O, and the exported bf16 softmax P and
     tanh(cap) with pz_attn_softmax's conventions (dead rows uniform over L keys with tcap 0, zeros in
-    the L..Lp pad columns), against torch fp32; both the LDS-DMA ring kernel (default) and the register-staged one"""
+    the L..Lp pad columns), against torch fp32 (the LDS-DMA ring kernel; the round-4 register-staged one is built
+    only with -DPZ_FLASH_AB)"""
     from pizero_native import ops
-
-    monkeypatch.setenv("PZ_PROBS_DMA", dma)
 
     B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256
     L = P + C + Hc

@@ -4,6 +4,9 @@
 joint: B samples x (281 tokens x 8 heads) queries, 281 keys, head 256, soft-cap + block mask;
 siglip: B x 16 heads x 256 x 256, head 72.  Prints fwd / bwd ms and TF/s (algorithmic
 FLOP: fwd 4*nq*nk*hd per unit, bwd 2.5x fwd).
+
+The non-default variants (PZ_PROBS_DMA=0, PZ_SIG_DELTA=pass, PZ_SIG_QB=2) exist only in a -DPZ_FLASH_AB build of the
+library; in the product build those settings run the default kernels (use --default-only there).
 """
 import argparse
 import math

@@ -1,7 +1,8 @@
 """Memory-bound kernels of the training backward at micro-batch 256, hipGraph-timed per launch, with the
 algorithmic HBM bytes and the rate: Gemma RMSNorm backward (70656 x 2048, residual gradient), SigLIP LayerNorm
 backward (65536 x 1152, residual gradient, dw / db / dx column-sum partials), SigLIP fc1 GELU backward + bias
-column sums (65536 x 4304).  Each under its A/B knobs (PZ_NORM_PF=1: one row ahead instead of two).
+column sums (65536 x 4304), timed twice (round 5 measured the norm backward with one row ahead instead of two:
+LayerNorm 138.1 vs 131.5 us, profiles/r05/norm_bench.log; that variant is no longer built).
 
     python tools/norm_bench.py [--n 20]
 """
@@ -60,7 +61,7 @@ def main():
 
     for name, fn, nbytes in cases:
         res = []
-        for label, env in (("default", {}), ("PZ_NORM_PF=1", {"PZ_NORM_PF": "1"}), ("default", {})):
+        for label, env in (("run 1", {}), ("run 2", {})):
             os.environ.update(env)
             try:
                 t = graph_us(fn, a.n)

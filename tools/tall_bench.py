@@ -49,16 +49,23 @@ def main():
         fl = 2 * M * N * K
         wb = N * K * 2
         res, outs = [], []
-        for label, env in [("default", {"PZ_GEMM_TALL": "0"}), ("tall", {"PZ_GEMM_TALL": "1"})]:
+        variants = [("default", {"PZ_GEMM_TALL": "0"}), ("tall", {"PZ_GEMM_TALL": "1"})]
+        for label, env in variants:
             os.environ.update(env)
-            kn = ops.gemm_kernel_name(M, N, K, epi=epi, **gi)
-            run()
-            torch.cuda.synchronize()
-            outs.append(out.float().clone())
-            t = graph_us(run, a.n)
-            res.append(f"{label} {t:7.2f} us ({fl / t / 1e6:5.0f} TF/s, {wb / t / 1e3:5.0f} GB/s wts) [{kn}]")
-            os.environ.pop("PZ_GEMM_TALL")
-        d = (outs[0] - outs[1]).abs().max().item()
+            try:
+                kn = ops.gemm_kernel_name(M, N, K, epi=epi, **gi)
+                if label.startswith("tall") and not kn.startswith("gemm_tall"):
+                    res.append(f"{label} n/a [{kn}]")
+                    continue
+                run()
+                torch.cuda.synchronize()
+                outs.append(out.float().clone())
+                t = graph_us(run, a.n)
+                res.append(f"{label} {t:7.2f} us ({fl / t / 1e6:5.0f} TF/s, {wb / t / 1e3:5.0f} GB/s wts) [{kn}]")
+            finally:
+                for k in env:
+                    os.environ.pop(k)
+        d = max((o - outs[0]).abs().max().item() for o in outs[1:]) if len(outs) > 1 else 0.0
         print(f"{name:12s} {M}x{N}x{K}: " + " | ".join(res) + f" | max|d| {d:.3g}", flush=True)
     main_nn(a.n)
 

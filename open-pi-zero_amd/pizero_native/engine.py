@@ -868,16 +868,29 @@ class Engine:
                                B, g.T, nh, 1, hd, L, g.off, Lp, g.off)
         names = [p + f"self_attn.{k}_proj.weight" for k in "qkv"]
         rgs = [self.rg(n) for n in names]
-        if all(rgs):
-            ops.linear_wgrad(dqkv, gs["h"], self.ar.grad_span(names[0], names[2]), beta=beta)
-        elif rgs[0] and rgs[1]:  # e.g. last-layer vlm v_proj frozen (pizero.py:231)
-            ops.linear_wgrad(dqkv[:, : (nh + 1) * hd], gs["h"], self.ar.grad_span(names[0], names[1]), beta=beta)
-        else:
-            for n, rgk, c0, c1 in zip(names, rgs, (0, nh * hd, (nh + 1) * hd), (nh * hd, (nh + 1) * hd, W)):
+        if gs.get("skip"):
+            # last vlm layer: its query rows feed nothing (the post-attention block is skipped), so dQ = 0 exactly --
+            # the q_proj gradient is zero (written as such, not computed: pizero.py:231's frozen v_proj and the zero
+            # q_proj grad) and only the k|v columns enter the weight / input gradients
+            if rgs[0] and not beta:
+                self.gw(names[0]).zero_()
+            for n, rgk, c0, c1 in zip(names[1:], rgs[1:], (nh * hd, (nh + 1) * hd), ((nh + 1) * hd, W)):
                 if rgk:
                     ops.linear_wgrad(dqkv[:, c0:c1], gs["h"], self.gw(n), beta=beta)
-        dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
-        ops.linear_dgrad(dqkv, self.qkv_w(p), dh)
+            dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
+            ops.linear_dgrad(dqkv[:, nh * hd:], self.ar.span(names[1], names[2]), dh)
+        else:
+            if all(rgs):
+                ops.linear_wgrad(dqkv, gs["h"], self.ar.grad_span(names[0], names[2]), beta=beta)
+            elif rgs[0] and rgs[1]:  # e.g. last-layer vlm v_proj frozen (pizero.py:231)
+                ops.linear_wgrad(dqkv[:, : (nh + 1) * hd], gs["h"], self.ar.grad_span(names[0], names[1]),
+                                 beta=beta)
+            else:
+                for n, rgk, c0, c1 in zip(names, rgs, (0, nh * hd, (nh + 1) * hd), (nh * hd, (nh + 1) * hd, W)):
+                    if rgk:
+                        ops.linear_wgrad(dqkv[:, c0:c1], gs["h"], self.gw(n), beta=beta)
+            dh = torch.empty(M, g.hid, device=dev, dtype=BF16)
+            ops.linear_dgrad(dqkv, self.qkv_w(p), dh)
         part = torch.empty((M + rpp - 1) // rpp, g.hid, device=dev, dtype=F32)
         dxn = torch.empty(M, g.hid, device=dev, dtype=BF16)
         ops.rmsnorm_bwd(dh, x, self.w(p + "input_layernorm.weight"), gs["r"], dxn, dres=dXm.get(g.name),

@@ -1149,6 +1149,66 @@ __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   // after the one a wait retires) are the same for all four combinations: 5 / 4 at phase 1
   // (A split only), 4 at phase 3; tails retire everything.
   constexpr bool AS = AKC, BS = BKC;
+#ifndef PZ_GEMM_QUAD4
+  if constexpr (AS && BS) {
+    // Two sections per K-tile (both operands k-contiguous, the product's only gemm8p case): section 0 reads
+    // A region 0 and all of B (16 fragment loads) and runs quadrants (0,0), (0,1); section 1 reads A region 1
+    // (8) and runs (1,1), (1,0).  32 MFMAs per section against the other row group's reads; the four-phase
+    // schedule below front-loads 12 of its 24 loads into one 16-MFMA phase, and its loads, not its DMA, set
+    // that phase's length (profiles/r05/feed_ab_*.log).  DMA: A1(kt+1) in section 0 (its region was last read
+    // in section 1 of kt-1), A0 | B0 | B1 (kt+2) in section 1 (last read in section 0 of kt).  Waits (2 DMA
+    // instructions per piece): section 0 retires A1(kt) (4 newer pieces), section 1 retires tile kt+1's
+    // section-0 pieces (4 newer, or only A1(kt+1) on the next-to-last tile); each is followed by the
+    // barrier the next reader of those regions passes.
+    issue(0, 0);
+    issue(1, 0);
+    issue(2, 0);
+    issue(3, 0);
+    if (nk > 1) {
+      issue(0, 1);
+      issue(1, 1);
+      issue(2, 1);
+      PZ_WAIT_VM(8);
+    } else {
+      PZ_WAIT_VM(2);
+    }
+    PZ_RAW_BARRIER();
+    if (wr == 1) PZ_RAW_BARRIER();  // stagger: row-1 waves run one barrier behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const char* buf = smem + (kt & 1) * P8_BUF;
+      const bool n1 = kt + 1 < nk, n2 = kt + 2 < nk;
+      // section 0: quadrants (0,0), (0,1)
+      if (n1) issue(3, kt + 1);
+      read_a(buf, 0);
+      read_b(buf, 0);
+      read_b(buf, 1);
+      if (n1) PZ_WAIT_VM(8);
+      else PZ_WAIT_VM(0);
+      PZ_WAIT_LGKM0();
+      PZ_RAW_BARRIER();
+      mask_tail_a(kt);
+      mfma_quad(0, 0);
+      mfma_quad(0, 1);
+      PZ_RAW_BARRIER();
+      // section 1: quadrants (1,1), (1,0)
+      if (n2) {
+        issue(0, kt + 2);
+        issue(1, kt + 2);
+        issue(2, kt + 2);
+      }
+      read_a(buf, 1);
+      if (n2) PZ_WAIT_VM(8);
+      else if (n1) PZ_WAIT_VM(2);
+      PZ_WAIT_LGKM0();
+      PZ_RAW_BARRIER();
+      mask_tail_a(kt);
+      mfma_quad(1, 1);
+      mfma_quad(1, 0);
+      PZ_RAW_BARRIER();
+    }
+  } else
+#endif
+  {
   if (AS) {
     issue(0, 0);
     issue(1, 0);
@@ -1231,6 +1291,7 @@ __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
     PZ_RAW_BARRIER();
     mfma_quad(1, 0);
     PZ_RAW_BARRIER();
+  }
   }
   if (wr == 0) PZ_RAW_BARRIER();
   if (F8 && p.rs) {  // per-row activation scale: lane rows m0 + wr*128 + 16 rb + (lane & 15)

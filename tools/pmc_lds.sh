@@ -12,7 +12,7 @@ import csv, glob, sys, collections
 tot, n = collections.defaultdict(float), collections.Counter()
 for f in glob.glob(sys.argv[1] + "/lds/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "gemm8p" in r.get("Kernel_Name", ""):
+        if "gemm8" in r.get("Kernel_Name", ""):
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
             n[r["Counter_Name"]] += 1
 for k in sorted(tot):

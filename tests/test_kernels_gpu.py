@@ -172,6 +172,29 @@ def test_gemm256_layouts_with_tails(akc, bkc, K):
     close(Cf, 2 * ref, rtol=1e-3, atol=1e-2)
 
 
+@pytest.mark.parametrize("K", [64, 128, 192, 136, 320])
+def test_gemm8p_two_section_short_k(K):
+    """The two-section main loop (both operands k-contiguous) at 1, 2 and 3 K-tiles, where its prologue issues fewer
+    pieces and its counted waits drop to vmcnt(2) / (0); 136 = two full K-tiles + an 8-deep tail, 320 = 5 tiles;
+    plain + bias and the GeGLU epilogue (saved g|u) vs fp32 torch."""
+    from pizero_native import ops
+
+    M, N = 2600, 4104
+    assert ops.gemm_kernel_name(M, N, K, a_kc=True, b_kc=True).startswith("gemm8p_kernel")
+    A, Bm, bias = bf(M, K, scale=0.5), bf(N, K, scale=0.5), bf(N)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, A, K, True, Bm, K, True, C, N, bias=bias)
+    close(C, A.float() @ Bm.float().t() + bias.float(), atol=3e-2)
+    I = 2052
+    W = bf(2 * I, K, scale=K ** -0.5)
+    h = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+    gu = torch.empty(M, 2 * I, device=dev, dtype=torch.bfloat16)
+    ops.linear(A, W, h, epi=ops.PZ_EPI_GEGLU, aux=gu)
+    ref = A.float() @ W.float().t()
+    close(gu, ref)
+    close(h, torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:])
+
+
 def test_gemm256_geglu_with_tail():
     from pizero_native import ops
 

@@ -1150,10 +1150,10 @@ __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
   // (A split only), 4 at phase 3; tails retire everything.
   constexpr bool AS = AKC, BS = BKC;
 #ifndef PZ_GEMM_QUAD4
-  if constexpr (AS && BS) {
-    // Two sections per K-tile (both operands k-contiguous, the product's only gemm8p case): section 0 reads
-    // A region 0 and all of B (16 fragment loads) and runs quadrants (0,0), (0,1); section 1 reads A region 1
-    // (8) and runs (1,1), (1,0).  32 MFMAs per section against the other row group's reads; the four-phase
+  if constexpr (AS) {
+    // Two sections per K-tile (A k-contiguous; B either way -- a k-strided B is read whole in section 0 through
+    // transposed loads): section 0 reads A region 0 and all of B (16 fragment loads) and runs quadrants
+    // (0,0), (0,1); section 1 reads A region 1 (8) and runs (1,1), (1,0).  32 MFMAs per section against the other row group's reads; the four-phase
     // schedule below front-loads 12 of its 24 loads into one 16-MFMA phase, and its loads, not its DMA, set
     // that phase's length (profiles/r05/feed_ab_*.log).  DMA: A1(kt+1) in section 0 (its region was last read
     // in section 1 of kt-1), A0 | B0 | B1 (kt+2) in section 1 (last read in section 0 of kt).  Waits (2 DMA
@@ -1816,7 +1816,7 @@ static int launch256(const GemmP& p, int64_t batch, hipStream_t st) {
 }
 
 static bool use_8phase();
-static bool use_khalf(bool akc, bool bkc);
+static bool use_khalf(bool akc, bool bkc, int64_t m, int64_t n, int64_t k);
 
 namespace {
 enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS, PATH_TALL };
@@ -2153,10 +2153,10 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
     case PATH_256:
       if (use_8phase() && pl.tail_s)
         snprintf(buf, sizeof(buf), "%s<%s, %s, %s, %s>+gemm8p_tail_epilogue(tail %lld x %d)",
-                 use_khalf(pl.akc, pl.bkc) ? "gemm8k_kernel" : "gemm8p_kernel", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0),
+                 use_khalf(pl.akc, pl.bkc, a->M, a->N, a->K) ? "gemm8k_kernel" : "gemm8p_kernel", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0),
                  (long long)(pl.tiles_m * pl.tiles_n - pl.dp_tiles), pl.tail_s);
       else if (use_8phase())
-        snprintf(buf, sizeof(buf), "%s<%s, %s, %s, %s>", use_khalf(pl.akc, pl.bkc) ? "gemm8k_kernel" : "gemm8p_kernel",
+        snprintf(buf, sizeof(buf), "%s<%s, %s, %s, %s>", use_khalf(pl.akc, pl.bkc, a->M, a->N, a->K) ? "gemm8k_kernel" : "gemm8p_kernel",
                  bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu), bstr(a->K % 64 != 0));
       else
         snprintf(buf, sizeof(buf), "gemm256_kernel<%s, %s, %s, %d>", bstr(pl.akc), bstr(pl.bkc), bstr(pl.geglu),
@@ -2238,13 +2238,21 @@ static int launch_tile_any(GemmP& p, const Plan& pl, int64_t batch, hipStream_t 
 }
 
 // main loop of the 256-tile kernels: k-half segments (gemm8k_kernel) when an operand is k-strided,
-// quadrant segments (gemm8p_kernel) when both are k-contiguous -- there the k-half images' 64-B row
-// pieces cost more than the halved barrier count saves (measured on every Pi0 NT shape).
+// region sections (gemm8p_kernel) when both are k-contiguous -- there the k-half images' 64-B row
+// pieces cost more than the halved barrier count saves (measured on every Pi0 NT shape) -- and, since the
+// two-section loop (round 5), for the micro-batch's NN dgrads (A k-contiguous, B k-strided; >= 16384 rows) with
+// >= 4096 output columns or a reduction >= 4096: 2-4 % faster there, 2.5 % slower at 2048 x 2048
+// (profiles/r05/nn_main_ab.log; smaller row counts not measured, left on the k-half kernel).  Micro-batch census:
+// gate|up dgrad 128.5 vs 136.2 ms, down-proj DGEGLU dgrad 90.5 vs 94.1 ms, all GEMMs 854.6 vs 865.5 ms
+// (profiles/r05/census_nn_routing_ab.log; -DPZ_NN_KHALF builds the old routing for that A/B).
 // PZ_GEMM_MAIN=quad|khalf forces one (A/B runs; read per call).
-static bool use_khalf(bool akc, bool bkc) {
+static bool use_khalf(bool akc, bool bkc, int64_t m, int64_t n, int64_t k) {
   const char* e = getenv("PZ_GEMM_MAIN");
   if (e && strcmp(e, "quad") == 0) return false;
   if (e && strcmp(e, "khalf") == 0) return true;
+#ifndef PZ_NN_KHALF
+  if (akc && !bkc && m >= 16384 && (n >= 4096 || k >= 4096)) return false;
+#endif
   return !(akc && bkc);
 }
 
@@ -2261,7 +2269,7 @@ static void launch_tail(const GemmP& p, int T, hipStream_t st) {
 template <bool AKC, bool BKC, bool GEGLU, bool KTAIL>
 static int launch8p_k(const GemmP& p, int64_t batch, hipStream_t st) {
   const int smem = 2 * P8_BUF;  // 128 KiB
-  const bool kh = use_khalf(AKC, BKC);
+  const bool kh = use_khalf(AKC, BKC, p.M, p.N, p.K);
   auto kern = kh ? gemm8k_kernel<AKC, BKC, GEGLU, KTAIL> : gemm8p_kernel<AKC, BKC, GEGLU, KTAIL>;
   static bool attr_set[2] = {false, false};
   if (!attr_set[kh]) {

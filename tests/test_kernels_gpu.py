@@ -195,6 +195,27 @@ def test_gemm8p_two_section_short_k(K):
     close(h, torch.nn.functional.gelu(ref[:, :I], approximate="tanh") * ref[:, I:])
 
 
+@pytest.mark.parametrize("K", [64, 136, 2056])
+def test_gemm8p_two_section_kstrided_b(K):
+    """Micro-batch-sized NN dgrads (A k-contiguous, B k-strided, >= 16384 rows, >= 4096 output columns) take the
+    two-section loop with B read through transposed loads: 1 K-tile, 2 + tail, 32 + tail; bias, then fp32 beta
+    accumulation, vs fp32 torch."""
+    from pizero_native import ops
+
+    M, N = 16400, 4104
+    assert ops.gemm_kernel_name(M, N, K, a_kc=True, b_kc=False).startswith("gemm8p_kernel<true, false")
+    A, Bm, bias = bf(M, K, scale=0.5), bf(N, K, scale=0.5), bf(N)
+    Bop = Bm.t().contiguous()
+    ref = A.float() @ Bm.float().t()
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    ops.gemm(M, N, K, A, K, True, Bop, N, False, C, N, bias=bias)
+    close(C, ref + bias.float(), atol=3e-2)
+    Cf = torch.zeros(M, N, device=dev, dtype=torch.float32)
+    ops.gemm(M, N, K, A, K, True, Bop, N, False, Cf, N, beta=True)
+    ops.gemm(M, N, K, A, K, True, Bop, N, False, Cf, N, beta=True)
+    close(Cf, 2 * ref, rtol=1e-3, atol=1e-2)
+
+
 def test_gemm256_geglu_with_tail():
     from pizero_native import ops
 

@@ -43,7 +43,7 @@ def main():
         M, N, K = int(os.environ.get("PMC_M", "70656")), 16384, 2048
     else:
         M, N, K = int(os.environ.get("PMC_M", "70656")), 32768, 2048
-    kern = sys.argv[3] if len(sys.argv) > 3 else ("gemm8k_kernel<true, false" if dgeglu else "gemm8p_kernel<true, true, true")
+    kern = sys.argv[3] if len(sys.argv) > 3 else ("gemm8p_kernel<true, false" if dgeglu else "gemm8p_kernel<true, true, true")
     name, fetch, d1 = per_dispatch(os.path.join(src, "fetch", "fetch_counter_collection.csv"), kern)
     _, write, d2 = per_dispatch(os.path.join(src, "write", "write_counter_collection.csv"), kern)
     _, sq, d3 = per_dispatch(os.path.join(src, "sq", "sq_counter_collection.csv"), kern)

@@ -476,25 +476,27 @@ constexpr int BK256 = 64;  // dispatched K-tile of the 256 kernel (see above)
 // 256x256x64 "8-phase" ping-pong GEMM (the dispatched large-GEMM kernel).
 //
 // 8 waves as 2 (M) x 4 (N), 128 x 64 outputs per wave (acc[8][4], 128 AGPR/VGPR).
-// Each 64-deep K-tile is consumed in 4 phases of 16 MFMAs, one output quadrant
-// (64 rows x 32 cols) per phase, order (0,0) (0,1) (1,1) (1,0) so fragments are
-// read once per K-tile: phase 0 reads A-lo + B-lo, 1 reads B-hi, 2 reads A-hi,
-// 3 reads nothing.  Every phase = [issue one LDS-DMA piece, ds_reads, counted
-// vmcnt, lgkmcnt(0)] barrier [16 MFMA at setprio 1] barrier.  The M-row-1 wave
-// group runs one barrier behind the row-0 group, so on every SIMD (waves w and
-// w+4) one wave's MFMAs overlap the other's LDS reads / DMA issue.
+// With A k-contiguous (every forward GEMM and the large NN dgrads) each 64-deep K-tile
+// is consumed in 2 sections of 32 MFMAs: section 0 reads A-lo + all of B and runs
+// output quadrants (0,0) (0,1), section 1 reads A-hi and runs (1,1) (1,0).  Every
+// section = [issue LDS-DMA pieces, ds_reads, counted vmcnt, lgkmcnt(0)] barrier
+// [32 MFMA at setprio 1] barrier.  (A k-strided, PZ_GEMM_MAIN=quad only: the older
+// 4 phases of 16 MFMAs, order (0,0) (0,1) (1,1) (1,0), reads A-lo + B-lo / B-hi /
+// A-hi / nothing.)  The M-row-1 wave group runs one barrier behind the row-0 group,
+// so on every SIMD (waves w and w+4) one wave's MFMAs overlap the other's LDS reads
+// / DMA issue.
 //
 // LDS: two K-tile buffers of 64 KiB, each = 4 regions of 16 KiB:
 //   A region 0 (rows with (r % 128) < 64), A region 1 (the other 128 rows),
 //   B region 0 (virtual cols 0..127), B region 1 (cols 128..255).
-// A region is free as soon as the phase that last reads it has ended, so the
-// next-but-one K-tile streams in piece by piece: tile kt issues A1(kt+1) in
-// phase 0 and A0/B0/B1(kt+2) in phases 1-3; 4-5 pieces (64-80 KiB) stay in
-// flight and the counted waits (vmcnt 8 / 10) never drain the DMA queue in
-// steady state.  Hazards (one barrier per phase boundary, stagger included):
-// a piece is waited for (vmcnt, issuing waves) in a phase strictly before the
-// phase that reads it; a region is restaged >= 1 phase after its last read,
-// whose lgkmcnt(0) precedes that phase's first barrier.
+// A region is free as soon as the section (phase) that last reads it has ended,
+// so the next-but-one K-tile streams in piece by piece (two sections: A1(kt+1) in
+// section 0, A0/B0/B1(kt+2) in section 1); 4 pieces (64 KiB) stay in flight and
+// the counted waits (vmcnt 8) never drain the DMA queue in steady state.  Hazards
+// (one barrier per section boundary, stagger included): a piece is waited for
+// (vmcnt, issuing waves) in a section strictly before the one that reads it; a
+// region is restaged >= 1 section after its last read, whose lgkmcnt(0) precedes
+// that section's first barrier.
 // -------------------------------------------------------------------------
 constexpr int P8_BUF = 65536, P8_REG = 16384;
 

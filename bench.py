@@ -423,9 +423,14 @@ def main():
     gen = torch.Generator().manual_seed(rank)
     batches = [synthetic_batch(model, mb, dev, gen) for _ in range(min(accum, 2))]
     log(f"[bench] model ready in {time.time() - t0:.1f}s; world={world} micro_batch={mb} accum={accum} global={gb}")
-    loss_acc = torch.zeros(1, device=dev)
+    # per optimizer step (warm-up steps first): the sum of its micro-batch losses and the pre-clip gradient norm, kept
+    # on the device (no host sync inside the timed region) and checked after it -- a non-finite loss or norm fails
+    # the run (the reference logs the all-reduced loss of every micro-batch, train.py:399-410)
+    n_all = args.warmup + args.steps
+    step_loss = torch.zeros(n_all, device=dev)
+    step_gnorm = torch.zeros(n_all, device=dev)
 
-    def step():
+    def step(k):
         for i in range(accum):
             b = batches[i % len(batches)]
             last = i == accum - 1
@@ -433,15 +438,15 @@ def main():
             with ctx:
                 loss = meta(**b)
                 (loss / accum).backward()
-            loss_acc.add_(loss.detach())
-        clip_grad_norm_([opt_a, opt_v], cfg.max_grad_norm)
+            step_loss[k:k + 1].add_(loss.detach())
+        step_gnorm[k:k + 1].copy_(clip_grad_norm_([opt_a, opt_v], cfg.max_grad_norm))
         opt_a.step()
         opt_v.step()
         opt_a.zero_grad(set_to_none=True)
         opt_v.zero_grad(set_to_none=True)
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize()
     if ddp:
         dist.barrier()
@@ -456,10 +461,8 @@ def main():
     if ddp:
         dist.barrier()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if ddp:
-        dist.all_reduce(loss_acc)
+    for k in range(args.steps):
+        step(args.warmup + k)
     torch.cuda.synchronize()
     if ddp:
         dist.barrier()
@@ -469,6 +472,16 @@ def main():
     if ddp:
         dist.all_reduce(elt, op=dist.ReduceOp.MAX)
     el = float(elt.item())
+    if ddp:  # every rank's micro-batch losses (outside the timed region)
+        dist.all_reduce(step_loss)
+    losses = [v / (accum * world) for v in step_loss.tolist()]  # mean micro-batch loss of each step
+    gnorms = step_gnorm.tolist()
+    if not all(math.isfinite(v) for v in losses + gnorms):  # no headline from a diverged run
+        log(f"[bench] NON-FINITE training: loss per step {losses}, grad norm per step {gnorms} "
+            f"({gb * args.steps / el:.1f} samples/s, not reported)")
+        if ddp:
+            dist.destroy_process_group()
+        sys.exit(3)
     comm = None
     if ddp:
         # data parallelism keeps every replica's weights identical: a checksum of each rank's parameter arena
@@ -574,7 +587,8 @@ def main():
             "inference": infer,
             "c5_inference": c5,
             "cpu_baseline": cpu,
-            "loss_mean": float(loss_acc.item()) / (accum * args.steps * max(1, world)),
+            "loss_mean": sum(losses[args.warmup:]) / args.steps,  # timed steps only
+            "loss_per_step": losses, "grad_norm_per_step": gnorms,
             "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else None,
             "optimizer": {"kind": f"AdamW, {args.optim_bits}-bit state" + (" (bnb AdamW8bit algorithm)" if
                                                                            args.optim_bits == 8 else ""),

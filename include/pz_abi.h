@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 16
+#define PZ_ABI_VERSION 17
 
 enum {
   PZ_OK = 0,
@@ -381,6 +381,11 @@ int pz_copy_rows(const void* src, int64_t sld, int64_t sbs, void* dst, int64_t d
 /* bf16 <-> fp32 copies / scaled adds */
 int pz_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
+
+/* test instrument: fill every CU's LDS with `word` (0xffffffff = NaN) on `stream`, so the next kernel's reads of
+ * LDS it did not write return NaN (tests/test_train_loop_gpu.py; _lib.call runs it before every launch under
+ * PZ_POISON_LDS=1).  Not on any product path. */
+int pz_debug_poison_lds(uint32_t word, void* stream);
 
 const char* pz_last_error(void);
 int pz_abi_version(void);

@@ -2082,9 +2082,9 @@ constexpr int FU_SMEM_KV = 2 * FR_MAX * FaDims<72>::ROW * 2 + 2 * FR_MAX * 4;
 // unit i+1's images while unit i computes.  The images use an 80-element (160-B) row pitch, so two units'
 // K and V (or Q and dO) fit the CU's 160 KiB, and both the 16-row ds_read_b128 fragments and the 4-row
 // ds_read_b64_tr_b16 fragments are bank-conflict free (row r starts at dword 40 r: 16 consecutive rows tile
-// the 64 banks).  Each row's tenth 16-B chunk (head dims 72..79) repeats the ninth: the products that read it
-// meet zero Q / dO columns or land in discarded output columns; the 32-wide k step past column 79 reads the
-// next row's (finite) data against zero Q columns the same way.
+// the 64 banks).  Each row's tenth 16-B chunk (head dims 72..79) repeats the ninth (or, in the dK / dV kernel's
+// Q / dO images, carries lse / delta): the transposed reads that meet it land in discarded output columns, and
+// the 32-wide k step's lanes past dim 71 re-read dims 64..71 of their own row (fs_frag) against zeroed fragments.
 // reductions over the 4 lanes l, l ^ 16, l ^ 32, l ^ 48 (the 4 lane groups of a 16 x 16 MFMA column) with gfx950's
 // v_permlane16_swap / v_permlane32_swap (VALU, no LDS round trip as __shfl_xor's ds_bpermute); every lane gets the
 // same value, combined in the same order
@@ -2132,6 +2132,15 @@ __device__ __forceinline__ void fs_dma(const bf16_t* base, const int (&off)[FS_P
 }
 
 #define FS_WAIT_VM(n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory")
+
+// 16-row fragment of a resident image (80-element rows), k step ks of the 72-dim contraction.  At ks 2 every lane
+// group reads head dims 64..71 of its OWN row: groups g >= 1 stand for dims 72..95, which the other operand zeroes, so
+// only finite, landed bytes may meet those zeros.  (Reading on past dim 79 runs into the NEXT row -- for row 255 of
+// the second image of a buffer that is the other buffer's first image, whose DMA may still be in flight or which may
+// hold stale LDS of an earlier kernel on this CU: 0 x NaN = NaN.  Round 5's dQ kernel did exactly that.)
+__device__ __forceinline__ bf16x8 fs_frag(const bf16_t* T, int r0, int ks, int lane) {
+  return *reinterpret_cast<const bf16x8*>(T + (r0 + (lane & 15)) * FS_ROW + (ks < 2 ? ks * 32 + 8 * (lane >> 4) : 64));
+}
 
 // ds_read_b64_tr_b16 by inline asm: NOT counted by hipcc's lgkmcnt tracking -- the caller waits with an asm
 // that names the result (see the forward's V^T fragments)
@@ -2244,7 +2253,7 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
       for (int ks = 0; ks < 3; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bf16x8 kf = frag_row<FS_ROW>(Ks, i * 16, ks * 32, lane);
+          const bf16x8 kf = fs_frag(Ks, i * 16, ks, lane);
 #pragma unroll
           for (int qb = 0; qb < QB; ++qb) sc[i][qb] = mfma(kf, qf[qb][ks], sc[i][qb]);
         }
@@ -2466,8 +2475,8 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
           bf16x8 kfr[3], vfr[3];
 #pragma unroll
           for (int ks = 0; ks < 3; ++ks) {
-            kfr[ks] = frag_row<FS_ROW>(Ks, i * 16, ks * 32, lane);
-            vfr[ks] = frag_row<FS_ROW>(Vs, i * 16, ks * 32, lane);
+            kfr[ks] = fs_frag(Ks, i * 16, ks, lane);
+            vfr[ks] = fs_frag(Vs, i * 16, ks, lane);
           }
 #pragma unroll
           for (int qb = 0; qb < 2; ++qb) {
@@ -2606,10 +2615,10 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
         bf16x8 qa[3], da[3];
 #pragma unroll
         for (int ks = 0; ks < 3; ++ks) {
-          qa[ks] = frag_row<FS_ROW>(Qs, i * 16, ks * 32, lane);
-          da[ks] = frag_row<FS_ROW>(Ds, i * 16, ks * 32, lane);
+          qa[ks] = fs_frag(Qs, i * 16, ks, lane);
+          da[ks] = fs_frag(Ds, i * 16, ks, lane);
         }
-        if (g != 0) qa[2] = da[2] = bf16x8{};  // dims 72..95: the lse / delta chunk and the next row
+        // (dims 72..95: these lanes re-read dims 64..71 of their own row -- finite -- against the zeroed kfr / vfr)
 #pragma unroll
         for (int kb2 = 0; kb2 < 2; ++kb2) {
           f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};

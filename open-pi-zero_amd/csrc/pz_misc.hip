@@ -556,3 +556,36 @@ extern "C" int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
+
+// ---- test instrument (tests/test_train_loop_gpu.py, PZ_POISON_LDS) ------------------------------------------------
+// Fill the LDS of every CU with one 32-bit word (0xffffffff is NaN as fp32 and as both bf16 halves), so a kernel that
+// reads LDS it never wrote meets NaN instead of an earlier kernel's mostly-finite leftovers.  One 160 KiB workgroup
+// per CU at a time, 8 x the CU count of them: every CU runs several.
+constexpr int PZ_LDS_BYTES = 160 * 1024;
+
+__global__ void __launch_bounds__(256) poison_lds_kernel(uint32_t word) {
+  extern __shared__ __attribute__((aligned(16))) char pz_poison_smem[];
+  volatile u32x4* p = reinterpret_cast<volatile u32x4*>(pz_poison_smem);
+  for (int i = threadIdx.x; i < PZ_LDS_BYTES / 16; i += 256) {
+    p[i].x = word;
+    p[i].y = word;
+    p[i].z = word;
+    p[i].w = word;
+  }
+}
+
+extern "C" int pz_debug_poison_lds(uint32_t word, void* stream) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    if (hipFuncSetAttribute((const void*)poison_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            PZ_LDS_BYTES) != hipSuccess)
+      (void)hipGetLastError();
+  }
+  hipLaunchKernelGGL(poison_lds_kernel, dim3((unsigned)(8 * cus)), dim3(256), PZ_LDS_BYTES, ST, word);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

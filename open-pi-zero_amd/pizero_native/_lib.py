@@ -19,7 +19,7 @@ if os.environ.get("PZ_LIB_PATH"):
     print(f"[pizero_native] PZ_LIB_PATH override: loading {LIB_PATH} instead of the default libpizero_hip.so",
           file=_sys.stderr, flush=True)
 
-ABI_VERSION = 16  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 17  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -171,6 +171,7 @@ SIGNATURES = {
     "pz_fill_uniform": [vp, i32, i64, C.c_uint64, f32, f32, vp],
     "pz_cast_f32_bf16": [vp, vp, i64, vp],
     "pz_cast_bf16_f32": [vp, vp, i64, vp],
+    "pz_debug_poison_lds": [C.c_uint32, vp],
     "pz_last_error": [],
     "pz_abi_version": [],
 }
@@ -203,7 +204,39 @@ def lib():
     return _lib
 
 
+# entry points that enqueue no kernel (everything else takes the stream as its last argument)
+_NO_LAUNCH = {"pz_last_error", "pz_abi_version", "pz_gemm_kernel_name", "pz_norm_rows_per_part",
+              "pz_decode_attn_ws_bytes", "pz_debug_poison_lds"}
+# test instrument (tests/test_train_loop_gpu.py): with a word set, every launch is preceded on its stream by
+# pz_debug_poison_lds(word), so a kernel reading LDS it did not write sees NaN.  PZ_POISON_LDS=1 turns it on
+# for a whole process (0xffffffff).
+_POISON_LDS = [0xFFFFFFFF if os.environ.get("PZ_POISON_LDS", "0") == "1" else None]
+
+
+# debug instrument (PZ_CHECK_FINITE=1, engine._chk): names of the launches since the last finiteness check
+_RECENT = [[] if os.environ.get("PZ_CHECK_FINITE", "0") == "1" else None]
+
+
+def recent_launches(clear=True):
+    """the entry points called since the last call of this (PZ_CHECK_FINITE=1 only; else [])"""
+    r = _RECENT[0] or []
+    if clear and _RECENT[0] is not None:
+        _RECENT[0] = []
+    return r
+
+
+def set_poison_lds(word):
+    """word (e.g. 0xffffffff) or None: poison every CU's LDS before each kernel launch (test instrument)"""
+    _POISON_LDS[0] = None if word is None else int(word) & 0xFFFFFFFF
+
+
 def call(name, *args):
+    if _POISON_LDS[0] is not None and name not in _NO_LAUNCH:
+        rc = lib().pz_debug_poison_lds(_POISON_LDS[0], args[-1])
+        if rc != 0:
+            raise NativeError(f"pz_debug_poison_lds failed (rc={rc}): {lib().pz_last_error().decode(errors='replace')}")
+    if _RECENT[0] is not None:
+        _RECENT[0].append(name)
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         msg = lib().pz_last_error().decode(errors="replace")

@@ -133,6 +133,28 @@ class Dims:
         return (3 * self.ps * self.ps + 31) // 32 * 32
 
 
+def check_finite(where, **tensors):
+    """Synchronise the device and raise FloatingPointError if a floating-point tensor holds NaN / Inf, naming the
+    stage, the tensor and the native launches since the previous check (PZ_CHECK_FINITE debug instrument)."""
+    from ._lib import recent_launches
+
+    torch.cuda.synchronize()
+    for k, t in tensors.items():
+        if isinstance(t, dict):
+            for k2, t2 in t.items():
+                check_finite(where, **{f"{k}[{k2}]": t2})
+            continue
+        if not isinstance(t, torch.Tensor) or not t.is_floating_point() or t.numel() == 0:
+            continue
+        if not bool(torch.isfinite(t).all()):
+            bad = int((~torch.isfinite(t)).sum())
+            launches = recent_launches()
+            raise FloatingPointError(f"PZ_CHECK_FINITE: {where}: {k} {tuple(t.shape)} {t.dtype} has {bad} non-finite "
+                                     f"values; native launches since the previous check ({len(launches)}): "
+                                     f"{launches[-40:]}")
+    recent_launches()
+
+
 class _Token:
     """Lifetime marker of the forward state that borrows the engine's joint K/V buffers."""
 
@@ -215,11 +237,21 @@ class Engine:
         vI = self.d.vI
         self.sig_pitch = vI if os.environ.get("PZ_SIG_PITCH", "1") == "0" else (vI + 63) // 64 * 64
         self._side = {}
+        # PZ_CHECK_FINITE=1 (debug): after every layer / stage of the training forward and backward (and in
+        # FusedAdamW.step) synchronise and check the stage's outputs; the first non-finite tensor raises
+        # FloatingPointError naming the stage, the tensor and the kernels launched since the previous check
+        self.check_finite = os.environ.get("PZ_CHECK_FINITE", "0") == "1"
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
         self.f8 = None
         self.f8_version = None
         if self.d.nkv != 1:
             raise NotImplementedError("joint attention kernel path assumes MQA (num_key_value_heads=1, bridge.yaml:176)")
+
+    def _chk(self, where, **tensors):
+        """PZ_CHECK_FINITE: raise on the first non-finite tensor of this stage (no-op otherwise)"""
+        if not self.check_finite:
+            return
+        check_finite(where, **tensors)
 
     # ------------------------------------------------------------- weights --
     @property
@@ -455,6 +487,7 @@ class Engine:
             if save is not None:
                 st.update(h1=h1, mu1=mu1, r1=r1, qkv=qkv, lse=lse, O=O, xm=xm, h2=h2, mu2=mu2, r2=r2, a1=a1, g1=g1)
                 layers.append(st)
+                self._chk(f"siglip fwd layer {i}", h1=h1, qkv=qkv, O=O, lse=lse, xm=xm, h2=h2, g1=g1, x=xn)
             x = xn
         y = torch.empty_like(x)
         mu = torch.empty(M, device=dev, dtype=F32)
@@ -464,6 +497,7 @@ class Engine:
         ops.linear(y, self.w("multi_modal_projector.linear.weight"), img, bias=self.w("multi_modal_projector.linear.bias"))
         if save is not None:
             save.update(layers=layers, x_last=x, y=y, mu=mu, r=r, B=B)
+            self._chk("siglip fwd post-LN + projector", y=y, img=img)
         return img
 
     def siglip_backward(self, sv, dimg, beta):
@@ -572,6 +606,7 @@ class Engine:
                 ops.reduce_parts_multi(red, beta=beta)
             pd, pdn = pdn, pd  # this layer's dxn partials: the next (lower) layer's fc2 bias gradient
             dx = dxn
+            self._chk(f"siglip bwd layer {i}", dg=dg, dO=dO, dqkv=dqkv, dxm=dxm, dx=dxn)
             self._notify("vision", i)
         # patch embedding + position embedding
         pe = vt + "embeddings."
@@ -805,6 +840,7 @@ class Engine:
                 with self._on(side, g):
                     self._post_attn_train(g, l, X, gs, Os, dev)
             layers.append(st)
+            self._chk(f"joint fwd layer {l}", Q=Qj, K=Kj, V=Vj, O=Os, P=st.get("P"), tc=st.get("tc"), X=X)
         if side is not None:  # the expert output and its saved activations are read on the main stream later
             main.wait_stream(side)
             for t in X.values():
@@ -1003,6 +1039,7 @@ class Engine:
                                        rpp, nh, hd, dev)
             # the layer's expert gradients were produced on the side stream: the reducer's communication stream waits
             # for both streams before it reads them (the compute streams keep running; no main <- side join per layer)
+            self._chk(f"joint bwd layer {l}", dO=dO, dS=dS, dQ=dQ, dK=dK, dV=dV, dX=dX)
             self._notify("joint", l, (side,) if side is not None else ())
         if side is not None:
             main.wait_stream(side)
@@ -1056,6 +1093,7 @@ class Engine:
         ops.flow_loss(v[aoff:], 8, Tg * 8, x0, actions, loss, None, None, B, d.H, d.A, d.sig_min)
         save.update(sv_v=sv_v, ids=ids, cnt=cnt, pos=pos, B=B, prop=prop, pe=pe, tied=tied, Xl=Xl, ya=ya, ra=ra,
                     x0=x0, x1=actions, v=v, ag=ag, aoff=aoff, Tg=Tg, groups=groups)
+        self._chk("train fwd head (action norm, decoder, flow loss)", embed=Xv, ya=ya, v=v, loss=loss)
         return loss
 
     def train_backward(self, sv, grad_loss, beta):
@@ -1081,6 +1119,7 @@ class Engine:
         part = torch.empty((R + rpp - 1) // rpp, d.aH, device=dev, dtype=F32)
         ops.rmsnorm_bwd(dya, sv["Xl"], self.w("joint_model.mixtures.action.norm.weight"), sv["ra"], dXl, dw_part=part)
         self._norm_grads("joint_model.mixtures.action.norm.", part, None, beta)
+        self._chk("train bwd head", dv=dv, dya=dya, dXl=dXl)
         groups = sv["groups"]
         dX = {g.name: None for g in groups}
         dX[sv["ag"]] = dXl
@@ -1127,7 +1166,9 @@ class Engine:
         if self.m._vlm_needs_grad():
             dimg = torch.empty(B * d.n_img, d.gH, device=dev, dtype=BF16)
             ops.embed_merge_bwd(sv["ids"], dX["vlm"], dimg, d.n_img, d.image_token, 1.0)
+            self._chk("train bwd embed-merge", dimg=dimg)
             self.siglip_backward(sv["sv_v"], dimg, beta)
+        self._chk("train bwd end (gradient arena)", grad=self.ar.grad)
         if self.post_backward is not None:
             self.post_backward()
 

@@ -648,3 +648,8 @@ def fill_uniform(x, seed, off, scale):
 
 def cast_to_bf16(x, y):
     call("pz_cast_f32_bf16", _p(x), _p(y), x.numel(), _st())
+
+
+def debug_poison_lds(word=0xFFFFFFFF):
+    """Test instrument: fill every CU's LDS with ``word`` (0xffffffff = NaN) on the current stream."""
+    call("pz_debug_poison_lds", C.c_uint32(int(word) & 0xFFFFFFFF), _st())

@@ -29,12 +29,15 @@ partial-sum order), so clipping -- and training -- is bitwise reproducible.
 
 from __future__ import annotations
 
+import os
+
 import torch
 from torch.autograd.graph import increment_version
 
 from . import ops
 from ._lib import PZ_SUMSQ_PARTS
 
+_CHECK_FINITE = os.environ.get("PZ_CHECK_FINITE", "0") == "1"  # debug: check the updated weights (engine._chk)
 BLOCK8 = 256  # elements per absmax block (bnb blockwise 2-state optimizers)
 MIN_8BIT_SIZE = 4096  # bnb Optimizer8bit min_8bit_size: smaller tensors keep fp32 state
 
@@ -199,9 +202,10 @@ class FusedAdamW(torch.optim.Optimizer):
         full = torch.empty(0, dtype=g0.dtype, device=g0.device).set_(st)
         off = (g0.data_ptr() - st.data_ptr()) // g0.element_size()
         flat = full[off : off + run["flat"].numel()]
-        # verify the layout assumption (pointer arithmetic over every parameter of the run: ~1 ms of host time per
-        # 1,000 tensors) once per gradient layout -- the grads are arena views, so their pointers repeat every step
-        key = tuple(p.grad.data_ptr() if p.grad is not None else None for p in (run["params"][0], run["params"][-1]))
+        # verify the layout assumption once per gradient layout: the key holds EVERY parameter's gradient pointer
+        # (None for a missing one), so a grad set to None or replaced by a non-arena tensor anywhere in the run
+        # changes it and is re-checked; comparing the pointer list costs ~0.2 us per tensor
+        key = [p.grad.data_ptr() if p.grad is not None else None for p in run["params"]]
         if run.get("gkey") != key:
             base_p, base_g = run["flat"].data_ptr(), flat.data_ptr()
             for p in run["params"]:
@@ -238,6 +242,10 @@ class FusedAdamW(torch.optim.Optimizer):
                 # the kernels write through raw pointers: bump the parameters' (shared arena) version
                 # counter so weight-derived caches (the fp8 inference codes) see the change
                 increment_version(r["params"][0])
+                if _CHECK_FINITE:
+                    from .engine import check_finite
+
+                    check_finite(f"FusedAdamW.step (group lr {group['lr']:g})", param=r["flat"])
         self._gscale = None
 
     def zero_grad(self, set_to_none: bool = True):

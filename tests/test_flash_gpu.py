@@ -316,3 +316,38 @@ def test_flash_bwd_joint_block_mask(cnt):
     close(dQ.float().view(B, L, nh, hd).permute(0, 2, 1, 3), dq, atol=3e-2 * dq.abs().max().item() / 4)
     close(dK.float()[:, :L], dk.sum(1), atol=3e-2 * dk.abs().max().item())
     close(dV.float()[:, :L], dv.sum(1), atol=3e-2 * dv.abs().max().item())
+
+
+@pytest.mark.parametrize("B", [2, 40])
+def test_flash_bwd_siglip_poisoned_lds(B, monkeypatch):
+    """The persistent SigLIP kernels with every CU's LDS filled with NaN before each launch (pz_debug_poison_lds):
+    B = 2 gives 32 units over 32 workgroups, so each workgroup's second LDS buffer is never written -- round 5's dQ
+    kernel read row 255 of buffer 0's V image on into it (0 x NaN = NaN).  Outputs must be finite and
+    bitwise equal to an unpoisoned run."""
+    from pizero_native import _lib, ops
+
+    monkeypatch.setenv("PZ_FLASH_UNIT", "1")
+    monkeypatch.setenv("PZ_FLASH_SIG", "1")
+    nh, hd, N = 16, 72, 256
+    qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
+    dO = torch.randn(B * N, nh * hd, device=dev).to(torch.bfloat16)
+
+    def run():
+        O = torch.full((B * N, nh * hd), float("nan"), device=dev, dtype=torch.bfloat16)
+        lse = torch.full((B * nh, N), float("nan"), device=dev)
+        delta = torch.full((B * nh, N), float("nan"), device=dev)
+        dqkv = torch.full_like(qkv, float("nan"))
+        ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N))
+        ops.flash_bwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv))
+        torch.cuda.synchronize()
+        return O, lse, dqkv
+
+    ref = run()
+    _lib.set_poison_lds(0xFFFFFFFF)
+    try:
+        got = run()
+    finally:
+        _lib.set_poison_lds(None)
+    for r, g in zip(ref, got):
+        assert bool(torch.isfinite(g.float()).all())
+        assert torch.equal(r, g)

@@ -298,6 +298,33 @@ def rank_envs(n, port, base=None):
     return envs
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without touching HIP (a parent that initialised the GPU could not safely
+    start its ranks): the GPU nodes of the KFD topology (simd_count > 0; CPU nodes have none), narrowed by
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.  PZ_VISIBLE_GPUS overrides the count
+    (CPU-host tests of the launcher only)."""
+    if os.environ.get("PZ_VISIBLE_GPUS"):
+        return int(os.environ["PZ_VISIBLE_GPUS"])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(base):
+            try:
+                with open(os.path.join(base, node, "properties")) as f:
+                    props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(n, argv):
     """``bench.py --gpus N`` started without a launcher: run N copies of this script, one per GPU, as children
     (before this process touches the GPU), inheriting stdout/stderr so rank 0's JSON line is the output.  A
@@ -305,11 +332,14 @@ def launch_ranks(n, argv):
     import signal
     import subprocess
 
-    if "PZ_DEVICE" not in os.environ:
-        have = torch.cuda.device_count()  # does not initialise HIP on this image
-        if have < n:
-            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
-            return 2
+    # PZ_RANKS_PER_GPU = k (one-card rehearsal, tests/test_bench_launcher.py): k ranks share each GPU, rank r on
+    # device r // k -- applied in the children only; the parent's count is the same sysfs count as a real run's
+    per = max(1, int(os.environ.get("PZ_RANKS_PER_GPU", "1")))
+    have = visible_gpus()
+    if have * per < n:
+        print(f"bench.py: --gpus {n} but only {have} GPU(s) visible" + (f" ({per} ranks per GPU)" if per > 1 else ""),
+              file=sys.stderr, flush=True)
+        return 2
 
     def pdeathsig():  # a child outlives neither a killed parent nor its timeout
         import ctypes
@@ -380,8 +410,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # PZ_DEVICE / PZ_DIST_BACKEND: single-GPU rehearsal of the N>1 path (gloo, all ranks on one card)
-    dev_idx = int(os.environ.get("PZ_DEVICE", local))
+    # PZ_RANKS_PER_GPU / PZ_DIST_BACKEND: single-GPU rehearsal of the N>1 path (gloo, k ranks per card);
+    # PZ_DEVICE: run a single process on another card
+    per = max(1, int(os.environ.get("PZ_RANKS_PER_GPU", "1")))
+    dev_idx = local // per if per > 1 else int(os.environ.get("PZ_DEVICE", local))
     backend = os.environ.get("PZ_DIST_BACKEND", "nccl")
     torch.cuda.set_device(dev_idx)
     dev = torch.device(f"cuda:{dev_idx}")

@@ -386,6 +386,9 @@ int pz_cast_bf16_f32(const void* x, float* y, int64_t n, void* stream);
  * LDS it did not write return NaN (tests/test_train_loop_gpu.py; _lib.call runs it before every launch under
  * PZ_POISON_LDS=1).  Not on any product path. */
 int pz_debug_poison_lds(uint32_t word, void* stream);
+/* test instrument: `wgs` workgroups that each occupy a CU (96 KiB LDS) for `ticks` of the constant-rate wall clock
+ * (hipDeviceAttributeWallClockRate kHz) -- stands in for RCCL kernels sharing the CUs (tools/contention_probe.py). */
+int pz_debug_spin(int64_t wgs, int64_t ticks, void* stream);
 
 const char* pz_last_error(void);
 int pz_abi_version(void);

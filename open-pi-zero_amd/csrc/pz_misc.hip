@@ -589,3 +589,27 @@ extern "C" int pz_debug_poison_lds(uint32_t word, void* stream) {
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }
+
+// test instrument (tools/contention_probe.py): `wgs` workgroups that each hold a CU (96 KiB of LDS: one per CU, and no
+// 160 KiB persistent / 8-phase workgroup fits beside it) for `ticks` of the constant-rate wall clock -- a stand-in
+// for the RCCL kernels that share the CUs with the backward under data parallelism
+__global__ void __launch_bounds__(64) spin_kernel(int64_t ticks) {
+  extern __shared__ __attribute__((aligned(16))) char pz_spin_smem[];
+  const uint64_t t0 = wall_clock64();
+  while ((int64_t)(wall_clock64() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0 && ticks < 0) pz_spin_smem[0] = 0;  // (never: keeps the LDS allocation)
+}
+
+extern "C" int pz_debug_spin(int64_t wgs, int64_t ticks, void* stream) {
+  PZ_CHECK_ARG(wgs > 0 && wgs <= 65536 && ticks >= 0, "debug_spin: bad args");
+  static bool attr = false;
+  if (!attr) {
+    if (hipFuncSetAttribute((const void*)spin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) !=
+        hipSuccess)
+      (void)hipGetLastError();
+    attr = true;
+  }
+  hipLaunchKernelGGL(spin_kernel, dim3((unsigned)wgs), dim3(64), 96 * 1024, ST, ticks);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}

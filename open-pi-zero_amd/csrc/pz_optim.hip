@@ -235,10 +235,13 @@ __global__ void __launch_bounds__(256) adamw8_kernel(pz_adamw8_args a, int64_t p
   for (int64_t bi = b0; bi < b1; ++lo) {
     const A8Seg sg = a8_seg(a, lo);
     const int64_t send = min(b1, lo + 1 < a.nseg ? rfl64(a.seg[4 * (lo + 1) + 2]) : a.nblocks);
+    A8Pre cur{};
+    if (bi < send) adamw8_fetch(a, bi, sg, lane, cur);
     for (; bi < send; ++bi) {
-      A8Pre cur{};
-      adamw8_fetch(a, bi, sg, lane, cur);
+      A8Pre nxt{};
+      if (bi + 1 < send) adamw8_fetch(a, bi + 1, sg, lane, nxt);  // in flight under block bi's update
       adamw8_block(a, q1, q2, e1, e2, bi, sg, lane, cur, gs);
+      cur = nxt;
     }
   }
 }

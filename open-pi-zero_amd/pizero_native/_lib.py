@@ -172,6 +172,7 @@ SIGNATURES = {
     "pz_cast_f32_bf16": [vp, vp, i64, vp],
     "pz_cast_bf16_f32": [vp, vp, i64, vp],
     "pz_debug_poison_lds": [C.c_uint32, vp],
+    "pz_debug_spin": [i64, i64, vp],
     "pz_last_error": [],
     "pz_abi_version": [],
 }

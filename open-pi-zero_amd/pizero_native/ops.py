@@ -653,3 +653,8 @@ def cast_to_bf16(x, y):
 def debug_poison_lds(word=0xFFFFFFFF):
     """Test instrument: fill every CU's LDS with ``word`` (0xffffffff = NaN) on the current stream."""
     call("pz_debug_poison_lds", C.c_uint32(int(word) & 0xFFFFFFFF), _st())
+
+
+def debug_spin(wgs, ticks):
+    """Test instrument: ``wgs`` workgroups each holding a CU for ``ticks`` wall-clock ticks, on the current stream."""
+    call("pz_debug_spin", int(wgs), int(ticks), _st())

@@ -18,7 +18,8 @@ BENCH = os.path.join(ROOT, "bench.py")
 
 
 def _env(**kw):
-    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PZ_DEVICE")}
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PZ_DEVICE", "PZ_RANKS_PER_GPU", "PZ_VISIBLE_GPUS")}
     e.update(kw)
     return e
 
@@ -52,11 +53,30 @@ def test_too_few_gpus_refused():
     assert "GPU(s) visible" in r.stderr
 
 
+def test_visible_gpus_sysfs_count(tmp_path, monkeypatch):
+    """the launcher's GPU count reads the KFD topology (no HIP call in the parent) and honours the visibility
+    variables"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for var in ("PZ_VISIBLE_GPUS", "ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    n = bench.visible_gpus()
+    assert n >= 0
+    if not os.path.exists("/dev/kfd"):
+        assert n == 0
+    monkeypatch.setenv("PZ_VISIBLE_GPUS", "8")
+    assert bench.visible_gpus() == 8
+    import torch
+
+    assert not torch.cuda.is_initialized()
+
+
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="GPU host: the ranks would run")
 def test_failing_rank_fails_launcher():
-    # PZ_DEVICE skips the device count; each rank then fails at torch.cuda.set_device on this CPU-only host
+    # PZ_VISIBLE_GPUS claims 2 GPUs on this CPU-only host: the ranks start and fail at torch.cuda.set_device
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--no-infer", "--no-cpu-baseline"],
-                       env=_env(PZ_DEVICE="0"), capture_output=True, text=True, timeout=180)
+                       env=_env(PZ_VISIBLE_GPUS="2"), capture_output=True, text=True, timeout=180)
     assert r.returncode != 0
     assert r.stdout.strip() == ""
 
@@ -64,11 +84,13 @@ def test_failing_rank_fails_launcher():
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
 def test_bench_two_ranks_one_gpu():
-    """Rehearsal of the driver's multi-GPU run on one card: bench.py --gpus 2 spawns 2 ranks (gloo, both on
-    cuda:0), DDP over the gradient arena, one JSON line with n_gpus 2 and equal replica weights."""
+    """Rehearsal of the driver's multi-GPU run on one card: bench.py --gpus 2 counts the GPUs from sysfs as the real
+    run does (1 here, with PZ_RANKS_PER_GPU=2 ranks per card), spawns 2 ranks (gloo, both on cuda:0), DDP over the
+    gradient arena, one JSON line with n_gpus 2 and equal replica weights."""
     r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--micro-batch", "4", "--global-batch", "16",
                         "--steps", "1", "--warmup", "1", "--no-infer", "--no-cpu-baseline"],
-                       env=_env(PZ_DIST_BACKEND="gloo", PZ_DEVICE="0"), capture_output=True, text=True, timeout=840)
+                       env=_env(PZ_DIST_BACKEND="gloo", PZ_RANKS_PER_GPU="2"), capture_output=True, text=True,
+                       timeout=840)
     assert r.returncode == 0, r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout

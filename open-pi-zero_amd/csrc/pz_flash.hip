@@ -3184,6 +3184,16 @@ static int fa_device_cus() {
   return cache[dev];
 }
 
+// workgroups of the persistent SigLIP kernels: mult x the CU count (PZ_SIG_GRID = mult, read per call).  The units are
+// dealt statically (fs_unit), so a workgroup that cannot start because its CU is held by another stream's kernel (the
+// RCCL all-reduce under data parallelism) delays every unit it owns; with several workgroups per CU the hardware
+// dispatcher hands the queued workgroups to whichever CUs free up (tools/contention_probe.py)
+static int fa_sig_grid(const pz_flash_args* a) {
+  const char* e = getenv("PZ_SIG_GRID");
+  const int mult = e && e[0] >= '1' && e[0] <= '8' ? e[0] - '0' : 1;
+  return (int)std::min<int64_t>(a->Z * a->H, (int64_t)mult * fa_device_cus());
+}
+
 // the SigLIP training shape (256 x 256 keys, head 72, plain, one output group): the persistent pipelined
 // kernels; PZ_FLASH_SIG "0" keeps the one-workgroup-per-unit kernels (tests, A/B runs)
 static bool fa_sig(const pz_flash_args* a) {
@@ -3242,7 +3252,7 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
     static bool attr3 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {
-      const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
+      const int G = fa_sig_grid(a);
 #ifdef PZ_FLASH_AB
       const char* eq = getenv("PZ_SIG_QB");  // "2": 8 waves of 32 rows (A/B builds); default 16 waves of 16 rows
       if (eq && eq[0] == '2') {
@@ -3395,7 +3405,7 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     static bool aq = false, akv = false, aq2 = false, akv2 = false, aq3 = false, akv3 = false;
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
-      const int G = (int)std::min<int64_t>(a->Z * a->H, fa_device_cus());
+      const int G = fa_sig_grid(a);
       fa_smem_attr(flash_bwd_kv_sig_kernel, FS_SMEM, akv3);
 #ifdef PZ_FLASH_AB
       const char* ed = getenv("PZ_SIG_DELTA");  // "pass": the separate delta pass (A/B builds)

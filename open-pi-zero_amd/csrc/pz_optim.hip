@@ -47,7 +47,7 @@ __device__ __forceinline__ void quantize8x4(const float* __restrict__ sq, const 
   }
 }
 
-// A block's loads, issued one block ahead of its update (the loop below): p / g (8 B per lane), the two 4-code words
+// A block's loads, issued together before its update (the loop below): p / g (8 B per lane), the two 4-code words
 // and the two absmax.  Only for whole 8-bit-state lanes (nv == 4); the rest load inside adamw8_block.
 struct A8Pre {
   u32x2 pr, gr;
@@ -230,18 +230,17 @@ __global__ void __launch_bounds__(256) adamw8_kernel(pz_adamw8_args a, int64_t p
     else hi = mid - 1;
   }
   const float gs = a.gscale ? a.gscale[0] : 1.f;
-  // per tensor (segment) of the run: block bi + 1's loads are issued before block bi's update
+  // per tensor (segment) of the run, block by block: each block's loads, then its update.  (Issuing block bi + 1's
+  // loads before block bi's update measured no faster: 14.9 vs 14.4 ms per step, profiles/r06/optim_bench_r6b.log --
+  // the update's dependent search / division chain, not load latency, sets the time; profiles/r05/optim_bench_r5.txt)
   lo = rfl64(lo);
   for (int64_t bi = b0; bi < b1; ++lo) {
     const A8Seg sg = a8_seg(a, lo);
     const int64_t send = min(b1, lo + 1 < a.nseg ? rfl64(a.seg[4 * (lo + 1) + 2]) : a.nblocks);
-    A8Pre cur{};
-    if (bi < send) adamw8_fetch(a, bi, sg, lane, cur);
     for (; bi < send; ++bi) {
-      A8Pre nxt{};
-      if (bi + 1 < send) adamw8_fetch(a, bi + 1, sg, lane, nxt);  // in flight under block bi's update
+      A8Pre cur{};
+      adamw8_fetch(a, bi, sg, lane, cur);
       adamw8_block(a, q1, q2, e1, e2, bi, sg, lane, cur, gs);
-      cur = nxt;
     }
   }
 }

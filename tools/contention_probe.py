@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--hold-ms", type=float, default=20.0)
+    ap.add_argument("--sig-grids", default="1", help="PZ_SIG_GRID values to probe for the persistent SigLIP kernels")
+    ap.add_argument("--only", default="", help="substring filter on the case names")
     a = ap.parse_args()
     dev = "cuda"
     cus = torch.cuda.get_device_properties(0).multi_processor_count
@@ -95,17 +97,27 @@ def main():
     xs = torch.randn(Ms, 1152, device=dev).to(torch.bfloat16)
     W1 = (torch.randn(4304, 1152, device=dev) * 0.02).to(torch.bfloat16)
     g1 = torch.empty(Ms, 4304, device=dev, dtype=torch.bfloat16)
-    cases = {
-        "siglip fwd (persistent)": lambda: ops.flash_fwd(sa),
-        "siglip bwd dQ + dK/dV (persistent)": lambda: ops.flash_bwd(sa),
+    def sig(fn, grid):
+        def run():
+            os.environ["PZ_SIG_GRID"] = str(grid)
+            fn()
+        return run
+
+    cases = {}
+    for grid in a.sig_grids.split(","):
+        cases[f"siglip fwd (persistent, {grid} x CUs wgs)"] = sig(lambda: ops.flash_fwd(sa), grid)
+        cases[f"siglip bwd dQ + dK/dV (persistent, {grid} x CUs)"] = sig(lambda: ops.flash_bwd(sa), grid)
+    cases.update({
         "joint fwd + probs": lambda: ops.flash_fwd_probs(fa, Pm, tc, Lp),
         "joint bwd dS + dQ": lambda: ops.flash_bwd_ds(fa, Pm, tc, dS, Lp),
         f"GEMM {M}x32768x2048 GeGLU (8-phase)": lambda: ops.linear(x, Wgu, h, epi=ops.PZ_EPI_GEGLU, aux=gu),
         f"GEMM {Ms}x4304x1152 GELU (8-phase)": lambda: ops.linear(xs, W1, g1, epi=ops.PZ_EPI_GELU),
-    }
+    })
     ks = (0, 8, 32)
     print(f"{cus} CUs; side-stream spin holds k CUs for {a.hold_ms} ms; median of {a.rounds} rounds", flush=True)
     for name, fn in cases.items():
+        if a.only and a.only not in name:
+            continue
         for _ in range(2):
             fn()
         res = {k: [] for k in ks}

@@ -2109,13 +2109,70 @@ __device__ __forceinline__ void fs_glds16(const bf16_t* src, char* lds) {
                                    (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
-// unit of iteration t for this workgroup: G workgroups; with G % 8 == 0 and (G / 8) % H == 0 the G / 8
-// units an XCD runs together are whole images (all H heads: their 144-B q / k / v segments share lines)
-__device__ __forceinline__ int64_t fs_unit(const pz_flash_args& a, int G, int t) {
-  const int i = blockIdx.x;
-  if (G % 8 != 0 || (G / 8) % a.H != 0) return (int64_t)t * G + i;
-  return (int64_t)t * G + (i & 7) * (G / 8) + (i >> 3);
-}
+// ---- dynamic unit assignment of the persistent SigLIP kernels ------------------------------------------------------
+// A workgroup takes its next unit from a ticket counter instead of a fixed list, so units flow to whichever CUs run:
+// with statically dealt units a workgroup whose CU is held by another stream's kernel (RCCL under data parallelism)
+// delays all of its units -- measured x1.7-1.8 for these kernels with 8 or 32 CUs held, against the ideal x1.03 / x1.14
+// (tools/contention_probe.py, profiles/r06/contention_r6b.log).  Results per unit do not depend on which workgroup
+// computes it, so the output stays bitwise deterministic.
+//   * one counter per XCD (workgroup i runs on XCD i % 8): XCD x hands out the units of images x, x + 8, x + 16, ...,
+//     ticket k = head k % H of its (k / H)-th image, so the heads of an image run together on one XCD and share its L2
+//     (their 144-B q / k / v segments share lines), as the static order did;
+//   * wave 0 / lane 0 takes the ticket of the unit after next (inline-asm returning atomic, retired by the vmcnt(0)
+//     that ends every unit) and publishes it through 4 bytes of LDS that no read uses -- the tenth 16-B chunk of row
+//     0 (K image; the dK / dV kernel: row 1 of the Q image, whose chunk carries an lse copy nobody reads), whose only
+//     readers are the transposed reads of head dims 72..79 into discarded output rows -- before the barrier that ends
+//     the unit;
+//   * self-resetting: every workgroup takes tickets until one is past its XCD's units, so exactly units_x + G_x tickets
+//     are handed out; the workgroup that receives the last one resets the counter for the next launch (stream order,
+//     hipGraph replays included).  The kernels must not run concurrently with themselves (the engine runs SigLIP on
+//     one stream).
+__device__ unsigned g_fs_ctr[3][8];  // [kernel: 0 fwd, 1 dQ, 2 dK / dV][XCD]
+
+struct FsTickets {
+  unsigned* ctr;
+  int64_t units_x, units;
+  unsigned last;
+  int x, nx, H;
+  __device__ __forceinline__ FsTickets(const pz_flash_args& a, int kind) {
+    const int G = (int)gridDim.x;
+    nx = G % 8 == 0 ? 8 : 1;
+    x = (int)blockIdx.x % nx;
+    H = (int)a.H;
+    units = a.Z * a.H;
+    const int64_t zx = nx == 8 ? (a.Z > x ? (a.Z - x + 7) / 8 : 0) : a.Z;
+    units_x = zx * a.H;
+    last = (unsigned)(units_x + G / nx - 1);
+    ctr = &g_fs_ctr[kind][x];
+  }
+  // unit of ticket k (>= units: no more work)
+  __device__ __forceinline__ int64_t unit(unsigned k) const {
+    if ((int64_t)k >= units_x) return units;
+    return nx == 8 ? ((int64_t)(k / H) * 8 + x) * H + k % H : (int64_t)k;
+  }
+  // wave 0 / lane 0: take a ticket (returning atomic; the result lands with the caller's next vmcnt(0))
+  __device__ __forceinline__ void take(unsigned& tk) const {
+    asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(tk) : "v"(ctr), "v"(1u) : "memory");
+  }
+  // wave 0 / lane 0, after a vmcnt(0): publish the ticket to the slot; the receiver of the last ticket resets
+  __device__ __forceinline__ void publish(unsigned& tk, char* slot) const {
+    asm volatile("" : "+v"(tk));
+    if (tk == last) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(ctr), "v"(0u) : "memory");  // agent scope
+    // (LDS by inline asm: a C++ store through the generic pointer compiles to a flat store, counted by vmcnt too)
+    asm volatile("ds_write_b32 %0, %1" ::"v"((unsigned)(size_t)(__attribute__((address_space(3))) char*)slot), "v"(tk)
+                 : "memory");
+  }
+  __device__ __forceinline__ unsigned read(const char* slot) const {
+    unsigned v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                 : "=v"(v)
+                 : "v"((unsigned)(size_t)(const __attribute__((address_space(3))) char*)slot)
+                 : "memory");
+    return __builtin_amdgcn_readfirstlane(v);
+  }
+};
+constexpr int FS_SLOT0 = 9 * 16;             // byte offset of row 0's tenth chunk in an image
+constexpr int FS_SLOT1 = FS_ROW * 2 + 9 * 16;  // ... of row 1's
 
 // per-lane element offsets of this wave's FS_PER DMA pieces of a [256][72] operand with row stride ld
 __device__ __forceinline__ void fs_dma_offsets(int64_t ld, int wave, int lane, int (&off)[FS_PER]) {
@@ -2187,7 +2244,10 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
   // qn: hipcc would drain every in-flight LDS-DMA with vmcnt(0) at the first use of an ordinary load) and its
   // K / V images are issued before unit t's compute; one vmcnt(0) after the compute (long landed by then),
   // before unit t's O stores, and the barrier that ends unit t publish them, so no wait stalls in steady state.
-  int64_t u = fs_unit(a, G, 0);
+  (void)G;
+  const FsTickets tix(a, 0);
+  const bool w0 = wave == 0 && lane == 0;
+  unsigned tk = 0;
   bf16x8 qn[QB][3];
   auto issue = [&](int64_t un, int t1) {  // Q fragments + K / V images of unit un into buffer t1 & 1
     const int64_t bn = un / a.H, hn = un % a.H;
@@ -2210,8 +2270,19 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
       fs_dma(wave < 8 ? Kn : Vn, offk, nxt + (wave < 8 ? 0 : FS_IMG), wave & 7);
     }
   };
-  if (u < units) issue(u, 0);
+  // the first unit's ticket through buffer 1's slot (no DMA reaches buffer 1 before the loop), the second's through
+  // buffer 0's (after wave 0's own DMA of that chunk landed)
+  if (w0) tix.take(tk);
   FS_WAIT_VM(0);
+  if (w0) tix.publish(tk, fa_smem + 2 * FS_IMG + FS_SLOT0);
+  FS_BARRIER();
+  int64_t u = tix.unit(tix.read(fa_smem + 2 * FS_IMG + FS_SLOT0));
+  if (u < units) {
+    issue(u, 0);
+    if (w0) tix.take(tk);
+  }
+  FS_WAIT_VM(0);
+  if (u < units && w0) tix.publish(tk, fa_smem + FS_SLOT0);
   FS_BARRIER();
   for (int t = 0; u < units; ++t) {
     const int64_t b = u / a.H, h = u % a.H;
@@ -2225,8 +2296,11 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
       }
       if (g != 0) qf[qb][2] = bf16x8{};
     }
-    const int64_t un = fs_unit(a, G, t + 1);
-    if (un < units) issue(un, t + 1);  // uniform
+    const int64_t un = tix.unit(tix.read(fa_smem + (t & 1) * 2 * FS_IMG + FS_SLOT0));  // uniform
+    if (un < units) {
+      issue(un, t + 1);
+      if (w0) tix.take(tk);  // the unit after next
+    }
     const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
     const bf16_t* Kall = reinterpret_cast<const bf16_t*>(cur);
     const bf16_t* Vall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
@@ -2339,6 +2413,7 @@ __global__ void __launch_bounds__(16 / QB * 64, 1) flash_fwd_sig_kernel(pz_flash
       }
       if (g == 0 && a.lse) a.lse[u * FS_N + rq] = m[qb] * a.scale + __logf(l[qb]);
     }
+    if (un < units && w0) tix.publish(tk, fa_smem + ((t + 1) & 1) * 2 * FS_IMG + FS_SLOT0);
     FS_BARRIER();  // this buffer's readers are done; the next unit's pieces landed in every wave
     u = un;
   }
@@ -2396,7 +2471,10 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
   fs_dma_offsets(a.ldk, wave, lane, offk);
   fs_dma_offsets(a.ldv, wave, lane, offv);
   const float sl2 = a.scale * FA_LOG2E;
-  int64_t u = fs_unit(a, G, 0);
+  (void)G;
+  const FsTickets tix(a, 1);
+  const bool w0 = wave == 0 && lane == 0;
+  unsigned tk = 0;
   bf16x8 qn[2][3], dn[2][3];
   float ln[2], dln[2];
   auto issue = [&](int64_t un, int t1) {
@@ -2414,11 +2492,21 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
     fs_dma((const bf16_t*)a.k + bn * a.k_bstride + hn * a.k_hstride, offk, nxt, wave);
     fs_dma((const bf16_t*)a.v + bn * a.v_bstride + hn * a.v_hstride, offv, nxt + FS_IMG, wave);
   };
-  if (u < units) issue(u, 0);
+  if (w0) tix.take(tk);  // the first two tickets as in the forward
   FS_WAIT_VM(0);
+  if (w0) tix.publish(tk, fa_smem + 2 * FS_IMG + FS_SLOT0);
+  FS_BARRIER();
+  int64_t u = tix.unit(tix.read(fa_smem + 2 * FS_IMG + FS_SLOT0));
+  if (u < units) {
+    issue(u, 0);
+    if (w0) tix.take(tk);
+  }
+  FS_WAIT_VM(0);
+  if (u < units && w0) tix.publish(tk, fa_smem + FS_SLOT0);
   FS_BARRIER();
   for (int t = 0; u < units; ++t) {
     const int64_t b = u / a.H, h = u % a.H;
+    const int64_t un = tix.unit(tix.read(fa_smem + (t & 1) * 2 * FS_IMG + FS_SLOT0));  // uniform
     bf16x8 qf[2][3], df[2][3];
     float del[2], lse2[2];
 #pragma unroll
@@ -2453,8 +2541,10 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
         if (g == 0) a.delta[u * FS_N + r] = dl;
       }
     }
-    const int64_t un = fs_unit(a, G, t + 1);
-    if (un < units) issue(un, t + 1);  // uniform
+    if (un < units) {
+      issue(un, t + 1);
+      if (w0) tix.take(tk);
+    }
     const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
     const bf16_t* Kall = reinterpret_cast<const bf16_t*>(cur);
     const bf16_t* Vall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
@@ -2522,6 +2612,7 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
                                                     pack2bf(dq[db][qb][2] * a.scale, dq[db][qb][3] * a.scale)};
       }
     }
+    if (un < units && w0) tix.publish(tk, fa_smem + ((t + 1) & 1) * 2 * FS_IMG + FS_SLOT0);
     FS_BARRIER();
     u = un;
   }
@@ -2551,7 +2642,10 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
     }
   }
   const float sl2 = a.scale * FA_LOG2E;
-  int64_t u = fs_unit(a, G, 0);
+  (void)G;
+  const FsTickets tix(a, 2);
+  const bool w0 = wave == 0 && lane == 0;
+  unsigned tk = 0;
   bf16x8 kfr[2][3], vfr[2][3];
   // the wave's K / V fragments of unit un (inline-asm loads into kfr / vfr): issued in the last query step of
   // the previous unit, right after the last products that read kfr / vfr
@@ -2580,11 +2674,19 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
     for (int s2 = 0; s2 < FS_PER; ++s2)
       fs_glds16(side[s2] ? (const bf16_t*)(D + offl[s2]) : dO + offd[s2], nxt + FS_IMG + (wave * FS_PER + s2) * 1024);
   };
+  // tickets through row 1's tenth chunk of the Q image (an lse copy that no read uses)
+  if (w0) tix.take(tk);
+  FS_WAIT_VM(0);
+  if (w0) tix.publish(tk, fa_smem + 2 * FS_IMG + FS_SLOT1);
+  FS_BARRIER();
+  int64_t u = tix.unit(tix.read(fa_smem + 2 * FS_IMG + FS_SLOT1));
   if (u < units) {
     issue_kv(u);
     issue(u, 0);
+    if (w0) tix.take(tk);
   }
   FS_WAIT_VM(0);
+  if (u < units && w0) tix.publish(tk, fa_smem + FS_SLOT1);
   FS_BARRIER();
   for (int t = 0; u < units; ++t) {
     const int64_t b = u / a.H, h = u % a.H;
@@ -2594,8 +2696,11 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
       for (int ks = 0; ks < 3; ++ks) asm volatile("" : "+v"(kfr[kb2][ks]), "+v"(vfr[kb2][ks]));  // landed
       if (g != 0) kfr[kb2][2] = vfr[kb2][2] = bf16x8{};
     }
-    const int64_t un = fs_unit(a, G, t + 1);
-    if (un < units) issue(un, t + 1);  // uniform
+    const int64_t un = tix.unit(tix.read(fa_smem + (t & 1) * 2 * FS_IMG + FS_SLOT1));  // uniform
+    if (un < units) {
+      issue(un, t + 1);
+      if (w0) tix.take(tk);
+    }
     const char* cur = fa_smem + (t & 1) * 2 * FS_IMG;
     const bf16_t* Qall = reinterpret_cast<const bf16_t*>(cur);
     const bf16_t* Dall = reinterpret_cast<const bf16_t*>(cur + FS_IMG);
@@ -2698,6 +2803,7 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_kv_sig_kernel(pz_flas
         }
       }
     }
+    if (un < units && w0) tix.publish(tk, fa_smem + ((t + 1) & 1) * 2 * FS_IMG + FS_SLOT1);
     FS_BARRIER();
     u = un;
   }
@@ -3184,15 +3290,8 @@ static int fa_device_cus() {
   return cache[dev];
 }
 
-// workgroups of the persistent SigLIP kernels: mult x the CU count (PZ_SIG_GRID = mult, read per call).  The units are
-// dealt statically (fs_unit), so a workgroup that cannot start because its CU is held by another stream's kernel (the
-// RCCL all-reduce under data parallelism) delays every unit it owns; with several workgroups per CU the hardware
-// dispatcher hands the queued workgroups to whichever CUs free up (tools/contention_probe.py)
-static int fa_sig_grid(const pz_flash_args* a) {
-  const char* e = getenv("PZ_SIG_GRID");
-  const int mult = e && e[0] >= '1' && e[0] <= '8' ? e[0] - '0' : 1;
-  return (int)std::min<int64_t>(a->Z * a->H, (int64_t)mult * fa_device_cus());
-}
+// workgroups of the persistent SigLIP kernels: one per CU (units are taken from per-XCD ticket counters, FsTickets)
+static int fa_sig_grid(const pz_flash_args* a) { return (int)std::min<int64_t>(a->Z * a->H, fa_device_cus()); }
 
 // the SigLIP training shape (256 x 256 keys, head 72, plain, one output group): the persistent pipelined
 // kernels; PZ_FLASH_SIG "0" keeps the one-workgroup-per-unit kernels (tests, A/B runs)

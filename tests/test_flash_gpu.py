@@ -351,3 +351,53 @@ def test_flash_bwd_siglip_poisoned_lds(B, monkeypatch):
     for r, g in zip(ref, got):
         assert bool(torch.isfinite(g.float()).all())
         assert torch.equal(r, g)
+
+
+def test_flash_siglip_persistent_repeat_bitwise(monkeypatch):
+    """The persistent SigLIP kernels take their units from self-resetting per-XCD ticket counters (FsTickets): launches
+    of different unit counts back to back (B = 40, 2, 17 -- 17 images leave XCDs with 3 and 2 images, 2 leave six
+    XCDs without work) and a hipGraph replay must all reproduce each shape's first result bitwise"""
+    from pizero_native import ops
+
+    monkeypatch.setenv("PZ_FLASH_UNIT", "1")
+    monkeypatch.setenv("PZ_FLASH_SIG", "1")
+    nh, hd, N = 16, 72, 256
+    data = {}
+    for B in (40, 2, 17):
+        qkv = (torch.randn(B * N, 3 * nh * hd, device=dev) * 1.5).to(torch.bfloat16)
+        dO = torch.randn(B * N, nh * hd, device=dev).to(torch.bfloat16)
+        data[B] = (qkv, dO)
+
+    def run(B):
+        qkv, dO = data[B]
+        O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
+        lse = torch.empty(B * nh, N, device=dev)
+        delta = torch.empty(B * nh, N, device=dev)
+        dqkv = torch.empty_like(qkv)
+        ops.flash_fwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N))
+        ops.flash_bwd(ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv))
+        return O, lse, dqkv
+
+    first = {B: [t.clone() for t in run(B)] for B in (40, 2, 17)}
+    for B in (17, 40, 2, 40, 17):
+        for r, g in zip(first[B], run(B)):
+            assert torch.equal(r, g), B
+    # B = 17 itself against the fp32 reference (units of the uneven XCD split all computed, none twice)
+    qkv, dO = data[17]
+    x = qkv.float().view(17, N, 3, nh, hd).permute(2, 0, 3, 1, 4)
+    ref, _ = ref_attention(x[0], x[1], x[2], hd ** -0.5)
+    close(first[17][0].view(17, N, nh, hd).permute(0, 2, 1, 3), ref)
+    # captured into a hipGraph and replayed twice
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run(40)
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        outs = run(40)
+    for _ in range(2):
+        gr.replay()
+        torch.cuda.synchronize()
+        for r, g in zip(first[40], outs):
+            assert torch.equal(r, g)

@@ -93,7 +93,8 @@ def audit(lines, name):
             if VMEM.match(s):
                 op, _, rest = s.partition(" ")
                 ops = [o.strip() for o in rest.split(",")]
-                is_load = "load" in op and "lds" not in op
+                # loads, and atomics that return the old value (sc0 / glc), write a destination register
+                is_load = ("load" in op and "lds" not in op) or ("atomic" in op and re.search(r"\b(sc0|glc)\b", rest))
                 rd = regs(",".join(ops[1:])) if is_load else regs(rest)
                 for i, (d, _) in st.items():
                     if rd & d:

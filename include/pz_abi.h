@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 17
+#define PZ_ABI_VERSION 18
 
 enum {
   PZ_OK = 0,
@@ -94,6 +94,11 @@ int pz_gemm(const pz_gemm_args* args, void* stream);
  * pz_fp8_quant_tensor: q[i] = e4m3(x[i] * inv_scale) for n bf16 elements (n % 8 == 0): weights, with
  *   the per-tensor scale max|W| / 448 from pz_fp8_absmax (PZ_ABSMAX_PARTS fp32 partial maxima). */
 #define PZ_ABSMAX_PARTS 1024
+/* V^T codes for pz_flash_fwd_f8: per-head-dim scales vs [Z][256] = max over the nk keys of |V[:, d]| / 448, codes
+ * vt [Z][256][ldt] (k < nk; zero for nk <= k < ldt) from V bf16 rows [Z][.][256] (row stride ldv, sample stride
+ * v_bstride).  Replaces nothing in the reference (it has no fp8 path; BASELINE.json configs[4] asks for fp8 attention). */
+int pz_fp8_quant_vt(const void* v, int64_t ldv, int64_t v_bstride, int64_t Z, int64_t nk, void* vt, float* vs,
+                    int64_t ldt, void* stream);
 int pz_fp8_quant_rows(const void* x, int64_t ldx, void* q, int64_t ldq, float* row_scale, int64_t R, int64_t D,
                       void* stream);
 int pz_fp8_quant_tensor(const void* x, int64_t n, void* q, float inv_scale, void* stream);
@@ -259,6 +264,13 @@ int pz_flash_fwd(const pz_flash_args* a, void* stream);
  * pz_attn_softmax's conventions (fully masked rows uniform over the nk keys with tcap 0, zeros past
  * nk), so the GEMM-path backward (P / tcap consumers) runs unchanged.  Replaces the S GEMM +
  * pz_attn_softmax + P V GEMM of the reference's eager attention (joint_model.py:261-292). */
+/* fp8 attention forward (C5 prefill; joint_model.py:259-292 with e4m3 operands): the shape, mask, soft-cap,
+ * output groups and key-split workspace of *a (H == 1, head_dim 256; a->q / k / v are not read), Q codes qc [Z][nq][256]
+ * with row scales qs [Z*nq] (pz_fp8_quant_rows), key codes kc [Z][krows][256] with row scales ks [Z*krows], V^T codes
+ * vtc [Z][256][ldvt] with head-dim scales vs [Z][256] (pz_fp8_quant_vt; ldvt >= nk rounded up to 128).  S and P V on
+ * the fp8 MFMA, P quantised as e4m3(256 p). */
+int pz_flash_fwd_f8(const pz_flash_args* a, const void* qc, const float* qs, const void* kc, const float* ks,
+                    int64_t krows, const void* vtc, const float* vs, int64_t ldvt, void* stream);
 int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, int64_t ldp, void* stream);
 /* Joint attention backward from the exported softmax (head_dim 256, nk <= 320): dS[z][r][0..ldp) =
  * P (dP - sum_j P dP) scale (1 - tcap^2) in bf16 with dP = dO V^T computed in registers (dO from the

@@ -3232,6 +3232,199 @@ __global__ void __launch_bounds__(JP_NW * 64, 1) flash_bwd_ds_dma_kernel(pz_flas
   }
 }
 
+// ---- fp8 attention forward (C5 prefill, BASELINE.json configs[4] "fp8 MFMA attention") ---------------------------
+// S = Q K^T and O = P V on v_mfma_f32_16x16x128_f8f6f4 (OCP e4m3 codes, head_dim 256): per-row scales for Q (sq) and
+// the keys (sk), per-head-dim scales for V (sv: O[q][d] = sv_d sum_k P v_kd, exact factorisation), P quantised as
+// e4m3(256 p) with p <= 1 from the online softmax, so O = sv_d / 256 sum_k e4m3(256 p_qk) v_kd / l.  Soft-cap, block
+// mask and the online softmax are the bf16 kernel's (fa_logit on the dequantised score).  8 waves x 16 query rows per
+// workgroup, 128-key blocks double-buffered through LDS (register-staged):
+//   * K block [128 keys][256 codes]; MFMA row m of 16-key group i is key 32 (m >> 2) + 4 i + (m & 3), so lane group g
+//     of the S^T result holds keys 32 g .. 32 g + 31 of the block -- exactly the 32-code k set lane group g of P^T
+//     needs for ONE P V MFMA over the 128 keys; 16-B chunk c of key row r stored at c ^ ((r & 3) | (r >> 5) << 2):
+//     every ds_read_b128 of a fragment conflict-free;
+//   * V^T block [256 d][128 keys] (pz_fp8_quant_vt writes V^T codes), chunk c of row d at c ^ ((d & 6) | (d >> 3 & 1)):
+//     conflict-free;
+//   * key split over blockIdx.z with unnormalised fp32 partials (O sv / 256, m, l) merged by flash_fwd_combine_kernel.
+constexpr int F8_KB = 128, F8_KT = F8_KB * 256, F8_VT = 256 * F8_KB;
+constexpr int F8_SMEM = 2 * (F8_KT + F8_VT) + 2 * F8_KB * 4;
+
+__device__ __forceinline__ int f8_kswz(int r) { return (r & 3) | ((r >> 5) << 2); }
+__device__ __forceinline__ int f8_vswz(int d) { return (d & 6) | ((d >> 3) & 1); }
+__device__ __forceinline__ i32x8 f8_cat(const u32x4& lo, const u32x4& hi) {
+  return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+__device__ __forceinline__ unsigned f8_enc4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+
+__global__ void __launch_bounds__(512) flash_fwd_f8_kernel(pz_flash_args a, const uint8_t* __restrict__ qc,
+                                                          const float* __restrict__ qs, const uint8_t* __restrict__ kc,
+                                                          const float* __restrict__ ks, int64_t krows,
+                                                          const uint8_t* __restrict__ vtc,
+                                                          const float* __restrict__ vs, int64_t ldvt) {
+  extern __shared__ __attribute__((aligned(16))) char fa_smem[];
+  auto Kt = [&](int bi) { return fa_smem + bi * F8_KT; };
+  auto Vt = [&](int bi) { return fa_smem + 2 * F8_KT + bi * F8_VT; };
+  auto Sk = [&](int bi) { return reinterpret_cast<float*>(fa_smem + 2 * (F8_KT + F8_VT)) + bi * F8_KB; };
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, g = lane >> 4, l15 = lane & 15;
+  const int64_t b = blockIdx.y;
+  const int64_t q0 = (int64_t)blockIdx.x * 128 + wave * 16;
+  const int64_t r = q0 + l15;  // this lane's query row
+  const FaMask mk(a, b);
+  const int nkb = (int)((a.nk + F8_KB - 1) / F8_KB);
+  const int per = (nkb + (int)gridDim.z - 1) / (int)gridDim.z;
+  const int kb_begin = (int)blockIdx.z * per, kb_end = min(nkb, kb_begin + per);
+  // register-staged block loads: 4 K chunks, 4 V^T chunks, (threads < 128) one key scale
+  u32x4 sk_[4], sv_[4];
+  float sks = 0.f;
+  auto load = [&](int kb) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = t + 512 * j;
+      const int64_t kr = min((int64_t)kb * F8_KB + (c >> 4), krows - 1);
+      sk_[j] = *reinterpret_cast<const u32x4*>(kc + (b * krows + kr) * 256 + (c & 15) * 16);
+      sv_[j] = *reinterpret_cast<const u32x4*>(vtc + (b * 256 + (c >> 3)) * ldvt + (int64_t)kb * F8_KB + (c & 7) * 16);
+    }
+    if (t < F8_KB) sks = ks[b * krows + min((int64_t)kb * F8_KB + t, krows - 1)];
+  };
+  auto store = [&](int bi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = t + 512 * j;
+      const int kr = c >> 4, d = c >> 3;
+      *reinterpret_cast<u32x4*>(Kt(bi) + kr * 256 + (((c & 15) ^ f8_kswz(kr)) << 4)) = sk_[j];
+      *reinterpret_cast<u32x4*>(Vt(bi) + d * 128 + (((c & 7) ^ f8_vswz(d)) << 4)) = sv_[j];
+    }
+    if (t < F8_KB) Sk(bi)[t] = sks;
+  };
+  // Q^T fragments (B operand: codes 128 ks + 32 g .. + 31 of this lane's row) and the row scale
+  i32x8 qf[2];
+  float sq = 0.f;
+  {
+    const bool ok = r < a.nq;
+    const uint8_t* qr = qc + (b * a.nq + (ok ? r : 0)) * 256 + 32 * g;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2) {
+      const u32x4 lo = ok ? *reinterpret_cast<const u32x4*>(qr + 128 * k2) : u32x4{0u, 0u, 0u, 0u};
+      const u32x4 hi = ok ? *reinterpret_cast<const u32x4*>(qr + 128 * k2 + 16) : u32x4{0u, 0u, 0u, 0u};
+      qf[k2] = f8_cat(lo, hi);
+    }
+    if (ok) sq = qs[b * a.nq + r];
+  }
+  const int tq = mk.token((int)r);
+  f32x4 o[16];
+#pragma unroll
+  for (int db = 0; db < 16; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  if (kb_begin < kb_end) {
+    load(kb_begin);
+    store(0);
+  }
+  __syncthreads();
+  // this lane's K fragment rows (key within the block) per 16-key group: 32 (l15 >> 2) + 4 i + (l15 & 3)
+  const int krow0 = 32 * (l15 >> 2) + (l15 & 3);
+  for (int kb = kb_begin; kb < kb_end; ++kb) {
+    const int bi = (kb - kb_begin) & 1;
+    const bool more = kb + 1 < kb_end;
+    if (more) load(kb + 1);
+    const char* K = Kt(bi);
+    f32x4 sc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      sc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kr = krow0 + 4 * i, sw = f8_kswz(kr);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int c0 = 8 * k2 + 2 * g;
+        const u32x4 lo = *reinterpret_cast<const u32x4*>(K + kr * 256 + ((c0 ^ sw) << 4));
+        const u32x4 hi = *reinterpret_cast<const u32x4*>(K + kr * 256 + (((c0 + 1) ^ sw) << 4));
+        sc[i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(f8_cat(lo, hi), qf[k2], sc[i], 0, 0, 0, 0, 0, 0);
+      }
+    }
+    // dequantised logits of keys 32 g + 4 i + e, online softmax over the block
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f32x4 skv = *reinterpret_cast<const f32x4*>(Sk(bi) + 32 * g + 4 * i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = kb * F8_KB + 32 * g + 4 * i + e;
+        const float x = fa_logit(mk, sc[i][e] * sq * skv[e], tq, j);
+        sc[i][e] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = mn == -INFINITY ? 1.f : __expf(m - mn);
+    float sum = 0.f;
+    unsigned pw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float pv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        pv[e] = mn == -INFINITY ? 0.f : __expf(sc[i][e] - mn);
+        sum += pv[e];
+      }
+      pw[i] = f8_enc4(pv[0] * 256.f, pv[1] * 256.f, pv[2] * 256.f, pv[3] * 256.f);
+    }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l = l * alpha + sum;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < 16; ++db) o[db] *= alpha;
+    const i32x8 pf = i32x8{(int)pw[0], (int)pw[1], (int)pw[2], (int)pw[3], (int)pw[4], (int)pw[5], (int)pw[6], (int)pw[7]};
+    // O^T[d][q] += V^T[d][keys 32 g ..] P^T[..][q]
+    const char* V = Vt(bi);
+#pragma unroll
+    for (int db = 0; db < 16; ++db) {
+      const int d = 16 * db + l15, sw = f8_vswz(d);
+      const u32x4 lo = *reinterpret_cast<const u32x4*>(V + d * 128 + (((2 * g) ^ sw) << 4));
+      const u32x4 hi = *reinterpret_cast<const u32x4*>(V + d * 128 + (((2 * g + 1) ^ sw) << 4));
+      o[db] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(f8_cat(lo, hi), pf, o[db], 0, 0, 0, 0, 0, 0);
+    }
+    __syncthreads();  // every wave done with this block's buffers
+    if (more) store(bi ^ 1);
+    __syncthreads();
+  }
+  if (r >= a.nq) return;
+  // O^T rows d = 16 db + 4 g + e: the V column scales and the 1/256 of the P codes
+  const float* svb = vs + b * 256;
+  if (gridDim.z > 1) {
+    float* pO = (float*)a.ws;
+    float* pml = pO + (int64_t)gridDim.z * gridDim.y * a.nq * 256;
+    const int64_t row = ((int64_t)blockIdx.z * gridDim.y + b) * a.nq + r;
+#pragma unroll
+    for (int db = 0; db < 16; ++db) {
+      const int d = 16 * db + 4 * g;
+      const f32x4 sv4 = *reinterpret_cast<const f32x4*>(svb + d);
+      *reinterpret_cast<f32x4*>(pO + row * 256 + d) = o[db] * sv4 * (1.f / 256.f);
+    }
+    if (g == 0) {
+      pml[2 * row] = m;
+      pml[2 * row + 1] = l;
+    }
+    return;
+  }
+  const float inv = l > 0.f ? 1.f / (256.f * l) : 0.f;
+  const FaRow fr{&a};
+  const int gi = fr.grp(r);
+  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, 0, r, gi);
+#pragma unroll
+  for (int db = 0; db < 16; ++db) {
+    const int d = 16 * db + 4 * g;
+    const f32x4 sv4 = *reinterpret_cast<const f32x4*>(svb + d);
+    const f32x4 v = o[db] * sv4 * inv;
+    *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+  }
+  if (g == 0 && a.lse) a.lse[b * a.nq + r] = m + __logf(l);
+}
+
 }  // namespace
 
 // head dims with instantiated kernels: the Pi0 shapes (SigLIP 72, Gemma 256) and the tiny test config (16, 32)
@@ -3581,5 +3774,43 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
                 (int)splits);
   }
   PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_flash_fwd_f8(const pz_flash_args* a, const void* qc, const float* qs, const void* kc, const float* ks,
+                               int64_t krows, const void* vtc, const float* vs, int64_t ldvt, void* stream) {
+  PZ_CHECK_ARG(a && qc && qs && kc && ks && vtc && vs && a->Z > 0 && a->nq > 0 && a->nk > 0 && a->H == 1,
+               "flash_fwd_f8: bad args (one K / V head: H == 1)");
+  PZ_CHECK_ARG(a->head_dim == 256, "flash_fwd_f8: head_dim %lld (256 only)", (long long)a->head_dim);
+  PZ_CHECK_ARG(krows >= a->nk && ldvt >= (a->nk + F8_KB - 1) / F8_KB * F8_KB && ldvt % 16 == 0,
+               "flash_fwd_f8: krows %lld / ldvt %lld (ldvt >= nk rounded up to 128)", (long long)krows,
+               (long long)ldvt);
+  PZ_CHECK_ARG(PZ_ALIGNED(qc, 16) && PZ_ALIGNED(kc, 16) && PZ_ALIGNED(vtc, 16) && PZ_ALIGNED(vs, 16),
+               "flash_fwd_f8: 16-byte aligned codes / scales");
+  PZ_CHECK_ARG(a->n_groups >= 1 && a->n_groups <= 3 && a->g_row0[0] == 0 && a->o_hstride == 0, "flash_fwd_f8: groups");
+  for (int i = 0; i < a->n_groups; ++i) PZ_CHECK_ARG(a->g_o[i] && a->g_ld[i] % 4 == 0, "flash_fwd_f8: group %d", i);
+  PZ_CHECK_ARG(a->mask_mode == 0 || (a->mask_mode == 1 && a->cnt && a->rows_per_token > 0), "flash_fwd_f8: mask");
+  PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z < 65536, "flash_fwd_f8: nq / Z too large");
+  const int64_t qblk = (a->nq + 127) / 128, nkb = (a->nk + F8_KB - 1) / F8_KB;
+  int64_t sp = 1;  // key split (few query blocks: the B = 1 prefill) into the caller's workspace
+  if (a->ws && qblk * a->Z < 128 && nkb > 1) {
+    sp = (256 + qblk * a->Z - 1) / (qblk * a->Z);
+    sp = sp < nkb ? sp : nkb;
+    sp = sp < 16 ? sp : 16;
+    while (sp > 1 && sp * a->Z * a->nq * (256 + 2) * 4 > a->ws_bytes) --sp;
+    const int64_t per = (nkb + sp - 1) / sp;
+    sp = (nkb + per - 1) / per;
+  }
+  static bool attr = false;
+  fa_smem_attr(flash_fwd_f8_kernel, F8_SMEM, attr);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(flash_fwd_f8_kernel, dim3((unsigned)qblk, (unsigned)a->Z, (unsigned)sp), dim3(512), F8_SMEM, st, *a,
+                     (const uint8_t*)qc, qs, (const uint8_t*)kc, ks, krows, (const uint8_t*)vtc, vs, ldvt);
+  PZ_CHECK_LAUNCH();
+  if (sp > 1) {
+    const int64_t n = a->Z * a->nq * 64;
+    hipLaunchKernelGGL(flash_fwd_combine_kernel<256>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, *a, (int)sp);
+    PZ_CHECK_LAUNCH();
+  }
   return PZ_OK;
 }

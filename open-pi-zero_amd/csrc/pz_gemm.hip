@@ -30,7 +30,6 @@ constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE_BYTES = 128 * 64 * 2;  // one operand tile image in LDS
 
 
-typedef int i32x8 __attribute__((ext_vector_type(8)));
 // two bf16-shaped fragments (8 x 16 bit each = 16 fp8 codes) -> one 32-code f8f6f4 operand
 __device__ __forceinline__ i32x8 cat_f8(const bf16x8& lo, const bf16x8& hi) {
   const u32x4 a = __builtin_bit_cast(u32x4, lo), b = __builtin_bit_cast(u32x4, hi);
@@ -1829,7 +1828,7 @@ struct Plan {
   int64_t ksplit, ldw, tiles_m, tiles_n;
   int dp_tiles, tail_s, tail_kt;  // 8-phase split tail (tail_s == 0: none)
   int rows_w, rows_tnb, rows_tmb;  // row-slab kernel: waves, 16-column / 16-row blocks per tile
-  bool rows_f8;                    // ... with e4m3 weight codes (W8A16)
+  int rows_f8;                     // ... with e4m3 weight codes: 1 = W8A16, 2 = W8A8 (both operands codes)
   int tall_mi;                     // tall-tile kernel: 64 * tall_mi rows per tile (4 | 5)
 };
 
@@ -1986,8 +1985,25 @@ Plan make_plan(const pz_gemm_args* a) {
   pl.bkc = a->b_kcontig != 0;
   pl.geglu = a->epilogue == PZ_EPI_GEGLU;
   const int64_t ncols = pl.geglu ? a->geglu_inter : a->N;
-  // fp8 W8A8: the 8-phase 256-tile kernel on code pairs (K, lda, ldb halved by the caller of make_plan)
+  // fp8 W8A8: the 8-phase 256-tile kernel on code pairs (K, lda, ldb halved by the caller of make_plan); the row-slab
+  // shapes (64 < M <= 1024, <= 2048 codes of K in 128-code chunks, <= 4096 columns, no GeGLU: C5's prefill q|k|v / o)
+  // take the W8A8 row-slab kernel (PZ_ROWS_W8A8=0: the 8-phase kernel, A/B; read per call)
   if (a->fp8_mode == 1) {
+    const char* er8 = getenv("PZ_ROWS_W8A8");
+    if (!(er8 && er8[0] == '0') && !pl.geglu && a->M > 64 && a->M <= 1024 && a->K % 64 == 0 && a->K <= 1024 &&
+        ncols <= 4096 && a->a_row_scale) {
+      const int64_t tm = (a->M + 63) / 64;
+      int tnb = 4;
+      while (tnb > 1 && tm * ((ncols + 16 * tnb - 1) / (16 * tnb)) < 128) tnb /= 2;
+      pl.kind = PATH_ROWS;
+      pl.rows_f8 = 2;
+      pl.rows_w = a->K / 64 >= 8 ? 8 : 4;
+      pl.rows_tnb = tnb;
+      pl.rows_tmb = 4;
+      pl.tiles_m = tm;
+      pl.tiles_n = (ncols + 16 * tnb - 1) / (16 * tnb);
+      return pl;
+    }
     pl.kind = PATH_256;
     pl.tiles_m = (a->M + BT - 1) / BT;
     pl.tiles_n = (ncols + (pl.geglu ? BT / 2 : BT) - 1) / (pl.geglu ? BT / 2 : BT);
@@ -2140,6 +2156,14 @@ const char* bstr(bool b) { return b ? "true" : "false"; }
 extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
   static thread_local char buf[160];
   if (!a) return "";
+  pz_gemm_args a8;  // W8A8: the planner sees K / lda / ldb in code pairs, as in pz_gemm
+  if (a->fp8_mode == 1) {
+    a8 = *a;
+    a8.K = a->K / 2;
+    a8.lda = a->lda / 2;
+    a8.ldb = a->ldb / 2;
+    a = &a8;
+  }
   const Plan pl = make_plan(a);
   switch (pl.kind) {
     case PATH_SKINNY:
@@ -2168,8 +2192,11 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       snprintf(buf, sizeof(buf), "gemm_kernel<%s, %s, %d, %d>", bstr(pl.akc), bstr(pl.bkc), pl.wm, pl.tag);
       break;
     case PATH_ROWS:
-      snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
-               bstr(pl.geglu), bstr(pl.rows_f8));
+      if (pl.rows_f8 == 2)
+        snprintf(buf, sizeof(buf), "gemm_rows_f8a_kernel<%d, %d, %d>", pl.rows_w, pl.rows_tmb, pl.rows_tnb);
+      else
+        snprintf(buf, sizeof(buf), "gemm_rows_kernel<%d, %d, %d, %s, %s>", pl.rows_w, pl.rows_tmb, pl.rows_tnb,
+                 bstr(pl.geglu), bstr(pl.rows_f8 == 1));
       break;
     case PATH_TALL:
       snprintf(buf, sizeof(buf), "gemm_tall_kernel<%d, %d, %d, %d, %s, %s>%s", pl.tall_mi, pl.geglu ? 4 : 2,
@@ -2407,6 +2434,12 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
       p.ldw = pl.ldw;
     }
     return pz_sk64_launch(p, pl.skinny_w, pl.skinny_nc, pl.skinny_mb, a->fp8_mode == 2, pl.tiles_n, st);
+  }
+  if (a->fp8_mode == 1 && pl.kind == PATH_ROWS) {  // W8A8 row slab
+    p.tiles_m = (int)pl.tiles_m;
+    p.tiles_n = (int)pl.tiles_n;
+    PZ_CHECK_ARG(PZ_ALIGNED(a->A, 16) && PZ_ALIGNED(a->B, 16), "pz_gemm: W8A8 rows need 16-byte aligned codes");
+    return pz_rows_launch(p, pl.rows_w, pl.rows_tnb, false, 2, st);
   }
   if (a->fp8_mode == 1) {
     p.tiles_m = (int)pl.tiles_m;

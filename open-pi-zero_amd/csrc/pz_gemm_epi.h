@@ -334,7 +334,7 @@ __device__ __forceinline__ void store_geglu4(const GemmP& p, int64_t cofs, int64
 }
 }  // namespace
 // row-slab GEMM launcher (pz_gemm_rows.hip): w waves, tnb 16-column blocks per 64-row tile
-int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, bool f8w, hipStream_t st);
+int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, int f8w, hipStream_t st);
 // skinny-64 GEMM launcher (pz_gemm_rows.hip): 16 < M <= 64 rows (and fp8-weight W8A16), w waves, nc columns
 // per block, mb 16-row blocks
 int pz_sk64_launch(const GemmP& p, int w, int nc, int mb, bool f8w, int64_t tiles_n, hipStream_t st);

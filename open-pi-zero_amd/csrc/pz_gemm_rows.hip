@@ -162,6 +162,87 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_kernel(GemmP
 }
 
 // -------------------------------------------------------------------------
+// W8A8 row slab (C5's fp8 prefill q|k|v / o at 768-789 rows): the row-slab scheme with BOTH
+// operands OCP e4m3 codes, on the fp8 MFMA.  p.K / p.lda / p.ldb arrive in code PAIRS (pz_gemm's W8A8 convention), so
+// chunk c covers 128 codes (64 pairs) of a row; lane group g takes codes 128c + 32g + [0, 32) of the A row and of the
+// B row (two 16-B loads each) and ONE v_mfma_f32_16x16x128_f8f6f4 sums them -- the same k set on both operands, so
+// the plain dot product.  After the fixed-order LDS reduction each row's sum is scaled by its activation scale
+// (p.rs[m]) and the weight scale (alpha, in the shared epilogue).  K % 128 codes == 0 (host-checked), no GeGLU.
+template <int W, int TMB, int TNB>
+__global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_f8a_kernel(GemmP p) {
+  constexpr int NB = TMB * TNB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  f32x4* red = reinterpret_cast<f32x4*>(smem);  // [W][NB][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, rl = lane & 15;
+  int tm, tn;
+  tile_coords(blockIdx.x, gridDim.x, p.tiles_m, p.tiles_n, tm, tn);
+  const int64_t m0 = (int64_t)tm * (16 * TMB), n0 = (int64_t)tn * (16 * TNB);
+  const unsigned char* Ar[TMB];
+  const unsigned char* Br[TNB];
+#pragma unroll
+  for (int mb = 0; mb < TMB; ++mb)
+    Ar[mb] = reinterpret_cast<const unsigned char*>(p.A) + min(m0 + 16 * mb + rl, p.M - 1) * (2 * p.lda) + 32 * g;
+#pragma unroll
+  for (int nb = 0; nb < TNB; ++nb)
+    Br[nb] = reinterpret_cast<const unsigned char*>(p.B) + min(n0 + 16 * nb + rl, p.N - 1) * (2 * p.ldb) + 32 * g;
+  const int nch = (int)(p.K / 64);  // 128-code chunks
+  const int per = (nch + W - 1) / W;
+  const int kb = min(nch, wave * per), ke = min(nch, kb + per);
+  f32x4 acc[TMB][TNB];
+#pragma unroll
+  for (int mb = 0; mb < TMB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < TNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  i32x8 fa[2][TMB], fb[2][TNB];
+  auto ld32 = [](const unsigned char* q) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(q), hi = *reinterpret_cast<const u32x4*>(q + 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+  };
+  auto load = [&](auto B_, int c) {
+    constexpr int bi = decltype(B_)::value;
+#pragma unroll
+    for (int mb = 0; mb < TMB; ++mb) fa[bi][mb] = ld32(Ar[mb] + (int64_t)c * 128);
+#pragma unroll
+    for (int nb = 0; nb < TNB; ++nb) fb[bi][nb] = ld32(Br[nb] + (int64_t)c * 128);
+  };
+  auto mma = [&](auto B_) {
+    constexpr int bi = decltype(B_)::value;
+#pragma unroll
+    for (int mb = 0; mb < TMB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < TNB; ++nb)
+        acc[mb][nb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(fb[bi][nb], fa[bi][mb], acc[mb][nb], 0, 0, 0, 0,
+                                                                        0, 0);
+  };
+  const std::integral_constant<int, 0> B0;
+  const std::integral_constant<int, 1> B1;
+  int c = kb;
+  if (c < ke) load(B0, c);
+  while (c < ke) {
+    if (c + 1 < ke) load(B1, c + 1);
+    mma(B0);
+    if (++c >= ke) break;
+    if (c + 1 < ke) load(B0, c + 1);
+    mma(B1);
+    ++c;
+  }
+#pragma unroll
+  for (int mb = 0; mb < TMB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < TNB; ++nb) red[(wave * NB + mb * TNB + nb) * 64 + lane] = acc[mb][nb];
+  __syncthreads();
+  for (int blk = wave; blk < NB; blk += W) {
+    f32x4 o = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < W; ++w) o += red[(w * NB + blk) * 64 + lane];
+    const int mb = blk / TNB, nb = blk % TNB;
+    const int64_t m = m0 + 16 * mb + rl, n = n0 + 16 * nb + 4 * g;
+    o *= p.rs[min(m, p.M - 1)];
+    store_out4(p, 0, 0, m, n, o);
+  }
+}
+
+// -------------------------------------------------------------------------
 // Skinny GEMM for 16 < M <= 64 rows, and for fp8 (OCP e4m3) weights at M <= 64 (W8A16): the C5
 // denoise steps (an action chunk of 50 rows per sample).  The scheme of gemm_skinny_kernel -- W waves
 // per NC output columns, K split into W contiguous ranges, weights streamed once into VGPRs, LDS
@@ -431,7 +512,30 @@ static int launch_rows_f8(const GemmP& p, int tnb, bool geglu, hipStream_t st) {
   return launch_rows_k<W, 4, 1, false, true>(p, st);
 }
 
-int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, bool f8w, hipStream_t st) {
+template <int W, int TNB>
+static int launch_rows_f8a_k(const GemmP& p, hipStream_t st) {
+  constexpr int smem = W * 4 * TNB * 1024;
+  auto kern = gemm_rows_f8a_kernel<W, 4, TNB>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)(p.tiles_m * p.tiles_n)), dim3(W * 64), smem, st, p);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+template <int W>
+static int launch_rows_f8a(const GemmP& p, int tnb, hipStream_t st) {
+  if (tnb == 4) return launch_rows_f8a_k<W, 4>(p, st);
+  if (tnb == 2) return launch_rows_f8a_k<W, 2>(p, st);
+  return launch_rows_f8a_k<W, 1>(p, st);
+}
+
+// f8w: 1 = W8A16 (bf16 rows, e4m3 weights), 2 = W8A8 (both e4m3, per-row activation scales)
+int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, int f8w, hipStream_t st) {
+  if (f8w == 2) return w == 8 ? launch_rows_f8a<8>(p, tnb, st) : launch_rows_f8a<4>(p, tnb, st);
   if (f8w) return w == 8 ? launch_rows_f8<8>(p, tnb, geglu, st) : launch_rows_f8<4>(p, tnb, geglu, st);
   return w == 8 ? launch_rows_w<8>(p, tnb, geglu, st) : launch_rows_w<4>(p, tnb, geglu, st);
 }

@@ -93,7 +93,50 @@ __global__ void __launch_bounds__(256) absmax_kernel(const bf16_t* __restrict__ 
   if (threadIdx.x == 0) parts[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
+// V^T codes for the fp8 attention (pz_flash_fwd_f8): one scale per head dim d (the column max over the nk keys:
+// O[q][d] = s_d sum_k P[q][k] v_kd, so a per-column scale factors out of the P V sum exactly), codes written transposed
+// [256 d][ldt keys], zeros for nk <= k < ldt.  Workgroup (sample, 64 d-columns): pass 1 -- thread (key phase kp, column
+// dl) takes the max over keys kp, kp + 4, ... (the 64 columns of a key row are one 128-B read); pass 2 -- thread (dl,
+// 16-key group) reads its 16 keys' values and writes their 16 codes as one 16-B store.
+__global__ void __launch_bounds__(256) quant_vt_kernel(const bf16_t* __restrict__ v, int64_t ldv, int64_t vb, int64_t nk,
+                                                       uint8_t* vt, float* vs, int64_t ldt) {
+  __shared__ float red[4][64];
+  const int64_t b = blockIdx.x;
+  const int dl = threadIdx.x & 63, kp = threadIdx.x >> 6;
+  const int64_t d = (int64_t)blockIdx.y * 64 + dl;
+  const bf16_t* V = v + b * vb + d;
+  float m = 0.f;
+  for (int64_t k = kp; k < nk; k += 4) m = fmaxf(m, fabsf(bf2f(V[k * ldv])));
+  red[kp][dl] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0][dl], red[1][dl]), fmaxf(red[2][dl], red[3][dl]));
+  const float s = m > 0.f ? __fdiv_rn(m, E4M3_MAX) : 1.f;
+  const float inv = __fdiv_rn(1.f, s);
+  if (kp == 0) vs[b * 256 + d] = s;
+  uint8_t* T = vt + (b * 256 + d) * ldt;
+  for (int64_t k0 = (int64_t)kp * 16; k0 < ldt; k0 += 64) {
+    float f[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t k = k0 + e;
+      f[e] = k < nk ? fminf(fmaxf(bf2f(V[k * ldv]) * inv, -E4M3_MAX), E4M3_MAX) : 0.f;
+    }
+    *reinterpret_cast<u32x4*>(T + k0) = u32x4{enc4(f[0], f[1], f[2], f[3]), enc4(f[4], f[5], f[6], f[7]),
+                                              enc4(f[8], f[9], f[10], f[11]), enc4(f[12], f[13], f[14], f[15])};
+  }
+}
+
 }  // namespace
+
+extern "C" int pz_fp8_quant_vt(const void* v, int64_t ldv, int64_t v_bstride, int64_t Z, int64_t nk, void* vt,
+                               float* vs, int64_t ldt, void* stream) {
+  PZ_CHECK_ARG(v && vt && vs && Z > 0 && nk > 0 && ldt >= nk && ldt % 16 == 0 && PZ_ALIGNED(vt, 16) && Z < 65536,
+               "fp8_quant_vt: bad args (ldt >= nk, ldt %% 16 == 0, 16-byte aligned codes)");
+  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)Z, 4), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)v, ldv,
+                     v_bstride, nk, (uint8_t*)vt, vs, ldt);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
 
 extern "C" int pz_fp8_quant_rows(const void* x, int64_t ldx, void* q, int64_t ldq, float* row_scale, int64_t R,
                                  int64_t D, void* stream) {

@@ -242,6 +242,10 @@ class Engine:
         # FloatingPointError naming the stage, the tensor and the kernels launched since the previous check
         self.check_finite = os.environ.get("PZ_CHECK_FINITE", "0") == "1"
         # fp8 inference (C5): weight key -> (e4m3 codes, per-tensor scale); built by prepare_fp8()
+        # in fp8 mode the prefill's joint attention runs S = Q K^T and P V on the fp8 MFMA (pz_flash_fwd_f8;
+        # PZ_FP8_ATTN=0: the bf16 kernel, A/B) and the 65..1024-row q|k|v / o projections run W8A8 on the row-slab
+        # kernel (activation rows quantised per row; PZ_ROWS_W8A8=0: W8A16 as in round 5)
+        self.f8_attn = os.environ.get("PZ_FP8_ATTN", "1") == "1"
         self.f8 = None
         self.f8_version = None
         if self.d.nkv != 1:
@@ -334,7 +338,13 @@ class Engine:
                 return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
             return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
         ncols = W.shape[0] // 2 if epi == PZ_EPI_GEGLU else W.shape[0]
-        if norm is None and ops.rows_w8a16_ok(M, K, ncols):  # C5 prefill rows: W8A16 on the row-slab kernel
+        if norm is None and ops.rows_w8a8_ok(M, K, ncols, epi) and x.stride(0) % 16 == 0:
+            # C5 prefill q|k|v / o rows: W8A8 on the fp8 MFMA (row-slab kernel), per-row activation scales
+            xq = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+            xs = torch.empty(M, device=x.device, dtype=F32)
+            ops.fp8_quant_rows(x, xq, xs)
+            return ops.linear_fp8(xq, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=xs)
+        if norm is None and ops.rows_w8a16_ok(M, K, ncols):  # (PZ_ROWS_W8A8=0) W8A16 on the row-slab kernel
             return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux)
         if norm is not None:
             raise ValueError("lin: a fused norm needs <= 64 rows")
@@ -1305,8 +1315,11 @@ class Engine:
                 break
             if self.infer_flash and not isinstance(cnt, GeneralMask):  # fused attention over the L1 prefix keys
                 Os = {g.name: torch.empty(B * g.T, nh * hd, device=dev, dtype=BF16) for g in groups}
-                ops.flash_fwd(self._attn_flash_infer(Q, Kj, Vj, [(g.off, g.T, Os[g.name]) for g in groups], L1, L1, 0,
-                                                     cnt, B))
+                fa = self._attn_flash_infer(Q, Kj, Vj, [(g.off, g.T, Os[g.name]) for g in groups], L1, L1, 0, cnt, B)
+                if self.f8 is not None and self.f8_attn and hd == 256:
+                    self._flash_f8(fa, Q, Kj, Vj, B, L1 * nh, L1)  # fp8 MFMA attention (C5, configs[4])
+                else:
+                    ops.flash_fwd(fa)
                 for g in groups:
                     p = f"{g.prefix}{l}."
                     X[g.name] = self._post_attn_O(g, p, X[g.name], Os[g.name])
@@ -1383,6 +1396,22 @@ class Engine:
         ops.gemv_qkv_rope(x, self.ar.span(p + "self_attn.k_proj.weight", p + "self_attn.v_proj.weight"), pos,
                           self.rope(g.theta), None, Kj, Vj, g.T, 0, d.hd, L1, g.off, Lp, g.off,
                           norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
+
+    def _flash_f8(self, fa, Q, K, V, B, nq, nk):
+        """the joint attention of fa on the fp8 MFMA: Q rows / key rows quantised per row, V^T per head dim
+        (pz_fp8_quant_rows, pz_fp8_quant_vt), then pz_flash_fwd_f8 (+ its key-split combine)"""
+        dev = Q.device
+        hd, Lp = self.d.hd, K.shape[1]
+        qc = torch.empty(B * nq, hd, device=dev, dtype=torch.uint8)
+        qs = torch.empty(B * nq, device=dev, dtype=F32)
+        ops.fp8_quant_rows(Q.reshape(B * nq, hd), qc, qs)
+        kc = torch.empty(B * Lp, hd, device=dev, dtype=torch.uint8)
+        ks = torch.empty(B * Lp, device=dev, dtype=F32)
+        ops.fp8_quant_rows(K.reshape(B * Lp, hd), kc, ks)
+        vt = torch.empty(B, hd, (nk + 127) // 128 * 128, device=dev, dtype=torch.uint8)
+        vs = torch.empty(B, hd, device=dev, dtype=F32)
+        ops.fp8_quant_vt(V, B, nk, vt, vs)
+        ops.flash_fwd_f8(fa, qc, qs, kc, ks, Lp, vt, vs)
 
     def _attn_flash_infer(self, Q, K, V, outs, Lq, nk, tok0, cnt, B):
         """pz_flash_args for the inference attention: queries = Lq tokens starting at joint token tok0

@@ -139,13 +139,17 @@ def _gemm(M, N, K, A, lda, a_kc, B, ldb, b_kc, Cm, ldc, epi, alpha, beta, bias, 
 
 
 def gemm_kernel_name(M, N, K, *, a_kc=True, b_kc=True, epi=PZ_EPI_NONE, geglu_inter=0, batch=1, c_fp32=False,
-                     workspace_bytes=_WS_BYTES):
-    """Name of the kernel pz_gemm dispatches for this problem (bench / profile labels)."""
+                     workspace_bytes=_WS_BYTES, fp8_mode=0):
+    """Name of the kernel pz_gemm dispatches for this problem (bench / profile labels; fp8_mode 1 = W8A8 with row
+    scales, 2 = W8A16, K in codes)."""
     a = GemmArgs()
     a.M, a.N, a.K = int(M), int(N), int(K)
     a.a_kcontig, a.b_kcontig, a.c_fp32 = int(a_kc), int(b_kc), int(c_fp32)
     a.batch, a.batch_inner, a.epilogue, a.geglu_inter = int(batch), 1, int(epi), int(geglu_inter)
     a.workspace, a.ws_bytes = (256 if workspace_bytes else None), int(workspace_bytes)
+    a.fp8_mode = int(fp8_mode)
+    if fp8_mode == 1:
+        a.a_row_scale, a.lda, a.ldb = 256, int(K), int(K)
     return lib().pz_gemm_kernel_name(C.byref(a)).decode()
 
 
@@ -204,6 +208,16 @@ def linear_fp8(x, Wq, w_scale, out, *, bias=None, resid=None, epi=PZ_EPI_NONE, a
     a.a_row_scale = _p(x_scale)
     call("pz_gemm", C.byref(a), _st())
     return out
+
+
+def rows_w8a8_ok(M, K, ncols, epi=PZ_EPI_NONE):
+    """both operands e4m3 above 64 rows on the W8A8 row-slab kernel (pz_gemm.hip make_plan: 64 < M <= 1024, K % 128
+    == 0, K <= 2048, <= 4096 output columns, no GeGLU; PZ_ROWS_W8A8=0 disables: W8A16 as before)"""
+    import os
+
+    if os.environ.get("PZ_ROWS_W8A8") == "0":
+        return False
+    return 64 < M <= 1024 and K % 128 == 0 and K <= 2048 and ncols <= 4096 and epi != PZ_EPI_GEGLU
 
 
 def rows_w8a16_ok(M, K, ncols):
@@ -497,6 +511,16 @@ def flash_workspace(device):
 
 def flash_fwd(a):
     call("pz_flash_fwd", C.byref(a), _st())
+
+
+def fp8_quant_vt(v, Z, nk, vt, vs):
+    """V^T e4m3 codes vt [Z, 256, ldt] (zero past nk) and per-head-dim scales vs [Z, 256] of bf16 V [Z, rows, 256]"""
+    call("pz_fp8_quant_vt", _p(v), v.stride(1), v.stride(0), Z, nk, _p(vt), _p(vs), vt.shape[2], _st())
+
+
+def flash_fwd_f8(a, qc, qs, kc, ks, krows, vt, vs):
+    """fp8 attention forward (pz_flash_fwd_f8): shape / mask / outputs from the pz_flash_args a"""
+    call("pz_flash_fwd_f8", C.byref(a), _p(qc), _p(qs), _p(kc), _p(ks), int(krows), _p(vt), _p(vs), vt.shape[2], _st())
 
 
 def flash_bwd_ds(a, P, tcap, dS, ldp):

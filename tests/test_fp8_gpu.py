@@ -200,3 +200,118 @@ def test_bf16_skinny64(M, N, K, epi):
     assert _rel(out.float(), ref) < 1e-2, _rel(out.float(), ref)
     if epi == PZ_EPI_GEGLU:
         assert _rel(aux.float(), x.float() @ W.float().t()) < 1e-2
+
+
+# ---- round 6: W8A8 row slab, V^T quantisation, fp8 attention (VERDICT r5 Missing 1) -------------------------------
+
+
+@pytest.mark.parametrize("M,K,N,bias,resid", [(788, 2048, 2560, False, False), (788, 2048, 2048, False, True),
+                                              (768, 1152, 3456, True, False), (768, 1152, 1152, True, True),
+                                              (100, 2048, 640, False, False)])
+def test_w8a8_rows_kernel(M, K, N, bias, resid):
+    """64 < M <= 1024 W8A8 GEMMs (C5 prefill q|k|v / o: vlm 788 x 2048, SigLIP 768 x 1152) take the fp8 row-slab
+    kernel (gemm_rows_f8a_kernel): against torch fp32 of the dequantised operands"""
+    x = _rand(M, K, scale=2.0, seed=M + K)
+    W = _rand(N, K, scale=0.05, seed=N)
+    xq = torch.empty(M, K, device=DEV, dtype=torch.uint8)
+    xs = torch.empty(M, device=DEV, dtype=torch.float32)
+    ops.fp8_quant_rows(x, xq, xs)
+    ws = ops.fp8_weight_scale(W)
+    wq = torch.empty(N, K, device=DEV, dtype=torch.uint8)
+    ops.fp8_quant_tensor(W, wq, ws)
+    b = _rand(N, scale=0.5, seed=5) if bias else None
+    r = _rand(M, N, seed=6) if resid else None
+    assert ops.gemm_kernel_name(M, N, K, fp8_mode=1).startswith("gemm_rows_f8a_kernel")
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.linear_fp8(xq, wq, ws, out, bias=b, resid=r, x_scale=xs)
+    ref = _epi_ref(_deq(xq, xs) @ _deq(wq, ws).T, PZ_EPI_NONE, bias=b, resid=r)
+    assert _rel(out.float(), ref) <= 1e-2, _rel(out.float(), ref)
+
+
+def test_quant_vt():
+    """per-head-dim V scales and transposed codes (pz_fp8_quant_vt): codes = e4m3(V / s_d), zero past nk"""
+    Z, rows, nk, ldt = 2, 792, 789, 896
+    V = _rand(Z, rows, 256, scale=1.5, seed=11)
+    V[:, nk:] = float("nan")  # rows past nk are never read
+    vt = torch.full((Z, 256, ldt), 0x55, device=DEV, dtype=torch.uint8)
+    vs = torch.empty(Z, 256, device=DEV, dtype=torch.float32)
+    ops.fp8_quant_vt(V, Z, nk, vt, vs)
+    Vf = V[:, :nk].float()
+    amax = Vf.abs().amax(1).double()
+    s_ref = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax)).float()
+    torch.testing.assert_close(vs, s_ref, rtol=0, atol=0)
+    inv = (1.0 / s_ref.double()).float()
+    q_ref = (Vf * inv[:, None, :]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8).transpose(1, 2)
+    assert torch.equal(vt[:, :, :nk], q_ref)
+    assert (vt[:, :, nk:] == 0).all()
+
+
+def _joint_ref(q, k, v, cnt, P, C, L, nh):
+    """fp32 joint attention of the prefix pass (soft-cap 50, Pi0 block mask, dead pad rows uniform)"""
+    import math
+
+    B = q.shape[0]
+    s = (q @ k.transpose(-1, -2)) / math.sqrt(256)
+    s = 50.0 * torch.tanh(s / 50.0)
+    i = torch.arange(L, device=DEV).view(L, 1)
+    j = torch.arange(L, device=DEV).view(1, L)
+    out = []
+    for b in range(B):
+        c = cnt[b]
+        allowed = ((i < P) & (i < c) & (j < c)) | ((i >= P) & (i < P + C) & ((j < c) | ((j >= P) & (j < P + C))))
+        dead = (torch.arange(L, device=DEV) < P) & (torch.arange(L, device=DEV) >= c)
+        sb = s[b].masked_fill(~allowed.repeat_interleave(nh, 0), float("-inf"))
+        sb = torch.where(dead.repeat_interleave(nh)[:, None], torch.zeros_like(sb), sb)
+        out.append(torch.softmax(sb, -1) @ v[b])
+    return torch.stack(out)
+
+
+@pytest.mark.parametrize("B,P,cnt,key_split", [(1, 788, [788], True), (2, 276, [276, 200], True),
+                                               (2, 276, [276, 9], False)])
+def test_flash_fwd_f8(B, P, cnt, key_split):
+    """the prefill's joint attention on the fp8 MFMA (pz_flash_fwd_f8): Q / K per-row and V per-head-dim e4m3, P as
+    e4m3(256 p), against fp32 attention of the DEQUANTISED Q / K / V (the remaining error: P's quantisation and the
+    output rounding) and against the bf16 kernel (C5 shape: 789 prefix tokens x 8 heads, key split + combine)"""
+    import math
+
+    C, nh, hd = 1, 8, 256
+    L = P + C
+    Lp = (L + 3 + 7) // 8 * 8  # the cache rows past the prefix (the action rows) hold stale data: NaN here
+    Q = _rand(B, L * nh, hd, scale=2.0, seed=21)
+    K = _rand(B, Lp, hd, scale=2.0, seed=22)
+    V = _rand(B, Lp, hd, seed=23)
+    K[:, L:] = float("nan")
+    V[:, L:] = float("nan")
+    Ov = torch.empty(B * P, nh * hd, device=DEV, dtype=torch.bfloat16)
+    Oe = torch.empty(B * C, nh * hd, device=DEV, dtype=torch.bfloat16)
+    cnt_t = torch.tensor(cnt, device=DEV, dtype=torch.int32)
+
+    def args(Ov, Oe):
+        return ops.flash_args(B, 1, L * nh, L, hd, Q, (hd, L * nh * hd, 0), K, (hd, Lp * hd, 0), V, (hd, Lp * hd, 0),
+                              [(0, Ov, P * nh * hd, hd), (P * nh, Oe, C * nh * hd, hd)], 0, None, 1 / math.sqrt(hd),
+                              cap=50.0, mask_mode=1, cnt=cnt_t, prefix=P, cond=C, rows_per_token=nh,
+                              key_split=key_split)
+
+    qc = torch.empty(B * L * nh, hd, device=DEV, dtype=torch.uint8)
+    qs = torch.empty(B * L * nh, device=DEV, dtype=torch.float32)
+    ops.fp8_quant_rows(Q.reshape(-1, hd), qc, qs)
+    kc = torch.empty(B * Lp, hd, device=DEV, dtype=torch.uint8)
+    ks = torch.empty(B * Lp, device=DEV, dtype=torch.float32)
+    ops.fp8_quant_rows(K.reshape(-1, hd), kc, ks)
+    vt = torch.empty(B, hd, (L + 127) // 128 * 128, device=DEV, dtype=torch.uint8)
+    vs = torch.empty(B, hd, device=DEV, dtype=torch.float32)
+    ops.fp8_quant_vt(V, B, L, vt, vs)
+    ops.flash_fwd_f8(args(Ov, Oe), qc, qs, kc, ks, Lp, vt, vs)
+    got = torch.cat([Ov.view(B, P, nh, hd), Oe.view(B, C, nh, hd)], 1).float()
+    assert bool(torch.isfinite(got).all())
+    qd = _deq(qc, qs).view(B, L * nh, hd)
+    kd = _deq(kc, ks).view(B, Lp, hd)[:, :L]
+    vd = (vt[:, :, :L].view(torch.float8_e4m3fn).float() * vs[:, :, None]).transpose(1, 2)
+    ref = _joint_ref(qd, kd, vd, cnt, P, C, L, nh).view(B, L, nh, hd)
+    # pad rows (dead prefix tokens) are uniform averages: compare the live rows and the dead ones together
+    assert _rel(got, ref) <= 3e-2, _rel(got, ref)
+    # the bf16 kernel on the unquantised operands
+    Ov2, Oe2 = torch.empty_like(Ov), torch.empty_like(Oe)
+    ops.flash_fwd(args(Ov2, Oe2))
+    bf = torch.cat([Ov2.view(B, P, nh, hd), Oe2.view(B, C, nh, hd)], 1).float()
+    assert _rel(got, bf) <= 6e-2, _rel(got, bf)

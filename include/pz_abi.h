@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 18
+#define PZ_ABI_VERSION 19
 
 enum {
   PZ_OK = 0,
@@ -99,6 +99,18 @@ int pz_gemm(const pz_gemm_args* args, void* stream);
  * v_bstride).  Replaces nothing in the reference (it has no fp8 path; BASELINE.json configs[4] asks for fp8 attention). */
 int pz_fp8_quant_vt(const void* v, int64_t ldv, int64_t v_bstride, int64_t Z, int64_t nk, void* vt, float* vs,
                     int64_t ldt, void* stream);
+/* every operand of one pz_flash_fwd_f8 launch in one launch: Q rows q [nqr][256] -> qc / qs and key rows k [nkr][256]
+ * -> kc / ks (per-row, as pz_fp8_quant_rows), V -> vt / vs (as pz_fp8_quant_vt) */
+int pz_fp8_quant_attn(const void* q, int64_t nqr, const void* k, int64_t nkr, const void* v, int64_t ldv,
+                      int64_t v_bstride, int64_t Z, int64_t nk, void* qc, float* qs, void* kc, float* ks, void* vt,
+                      float* vs, int64_t ldt, void* stream);
+/* fp8 inference: Gemma RMSNorm / LayerNorm whose bf16-rounded output rows are quantised to e4m3 codes q [R][ldq] with
+ * per-row scales qscale [R] in the same pass (= pz_rmsnorm_fwd / pz_layernorm_fwd then pz_fp8_quant_rows) -- the A
+ * operand of the next W8A8 GEMM (paligemma/modules.py:7-21, siglip.py:211,217) */
+int pz_rmsnorm_fwd_f8(const void* x, int64_t ldx, const void* w, void* q, int64_t ldq, float* qscale, int64_t R,
+                      int64_t D, float eps, void* stream);
+int pz_layernorm_fwd_f8(const void* x, int64_t ldx, const void* w, const void* b, void* q, int64_t ldq, float* qscale,
+                        int64_t R, int64_t D, float eps, void* stream);
 int pz_fp8_quant_rows(const void* x, int64_t ldx, void* q, int64_t ldq, float* row_scale, int64_t R, int64_t D,
                       void* stream);
 int pz_fp8_quant_tensor(const void* x, int64_t n, void* q, float inv_scale, void* stream);

@@ -3792,8 +3792,12 @@ extern "C" int pz_flash_fwd_f8(const pz_flash_args* a, const void* qc, const flo
   PZ_CHECK_ARG(a->mask_mode == 0 || (a->mask_mode == 1 && a->cnt && a->rows_per_token > 0), "flash_fwd_f8: mask");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z < 65536, "flash_fwd_f8: nq / Z too large");
   const int64_t qblk = (a->nq + 127) / 128, nkb = (a->nk + F8_KB - 1) / F8_KB;
-  int64_t sp = 1;  // key split (few query blocks: the B = 1 prefill) into the caller's workspace
-  if (a->ws && qblk * a->Z < 128 && nkb > 1) {
+  // key split (few query blocks: the B = 1 prefill) into the caller's workspace; PZ_F8_SPLIT "0": never (A/B), "1":
+  // whenever fewer than 128 workgroups (read per call)
+  const char* esp = getenv("PZ_F8_SPLIT");
+  const bool split_ok = !(esp && esp[0] == '0');
+  int64_t sp = 1;
+  if (split_ok && a->ws && qblk * a->Z < 128 && nkb > 1) {
     sp = (256 + qblk * a->Z - 1) / (qblk * a->Z);
     sp = sp < nkb ? sp : nkb;
     sp = sp < 16 ? sp : 16;

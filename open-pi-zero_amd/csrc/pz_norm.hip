@@ -600,6 +600,124 @@ __global__ void __launch_bounds__(256) norm_bwd_row_kernel(
   }
 }
 
+// ---- fp8 inference (C5): the norm with the per-row e4m3 quantisation of its output in the same pass ----------------
+// (the A operand of the following W8A8 GEMM: the output is rounded to bf16 first, so the codes and the scale equal
+// pz_rmsnorm_fwd / pz_layernorm_fwd followed by pz_fp8_quant_rows -- one launch and no bf16 row written)
+__device__ __forceinline__ unsigned q8enc4(float a, float b, float c, float d) {
+  int v = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  v = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, v, true);
+  return (unsigned)v;
+}
+
+template <int MAXC>
+__device__ __forceinline__ void q8_store_row(float (&o)[MAXC][8], int nc, int lane, uint8_t* q, float* qscale) {
+  float m = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    if (lane + 64 * c < nc)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        o[c][i] = bf2f(f2bf(o[c][i]));
+        m = fmaxf(m, fabsf(o[c][i]));
+      }
+  }
+  m = warp_max(m);
+  const float sc = m > 0.f ? __fdiv_rn(m, 448.f) : 1.f;
+  const float inv = __fdiv_rn(1.f, sc);
+  if (lane == 0) *qscale = sc;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      float f[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) f[i] = fminf(fmaxf(o[c][i] * inv, -448.f), 448.f);
+      *reinterpret_cast<u32x2*>(q + ch * 8) = u32x2{q8enc4(f[0], f[1], f[2], f[3]), q8enc4(f[4], f[5], f[6], f[7])};
+    }
+  }
+}
+
+template <int MAXC>
+__global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                         const bf16_t* __restrict__ w, uint8_t* q, int64_t ldq,
+                                                         float* qscale, int64_t R, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nc = D / 8;
+  float v[MAXC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      load8(x + row * ldx + ch * 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = warp_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      float wv[8];
+      load8(w + ch * 8, wv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = v[c][i] * r * (1.f + wv[i]);
+    }
+  }
+  q8_store_row<MAXC>(v, nc, lane, q + row * ldq, qscale + row);
+}
+
+template <int MAXC>
+__global__ void __launch_bounds__(256) layernorm_q8_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                           const bf16_t* __restrict__ w, const bf16_t* __restrict__ b,
+                                                           uint8_t* q, int64_t ldq, float* qscale, int64_t R, int D,
+                                                           float eps) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int nc = D / 8;
+  float v[MAXC][8];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      load8(x + row * ldx + ch * 8, v[c]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[c][i];
+    }
+  }
+  const float mu = warp_sum(s) / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = v[c][i] - mu;
+        ss += d * d;
+      }
+  }
+  const float r = rsqrtf(warp_sum(ss) / (float)D + eps);
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      float wv[8], bv[8];
+      load8(w + ch * 8, wv);
+      load8(b + ch * 8, bv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[c][i] = (v[c][i] - mu) * r * wv[i] + bv[i];
+    }
+  }
+  q8_store_row<MAXC>(v, nc, lane, q + row * ldq, qscale + row);
+}
+
 static bool norm_bwd_rows() {
   const char* e = getenv("PZ_NORM_BWD");
   return !(e && e[0] == 'w');
@@ -798,6 +916,34 @@ extern "C" int pz_batch_sum(const void* X, int64_t B, int64_t stride, int64_t n,
   PZ_CHECK_ARG(X && out && B > 0 && n > 0, "batch_sum: bad args");
   hipLaunchKernelGGL(batch_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      (const bf16_t*)X, B, stride, n, (bf16_t*)out, (int)beta);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_rmsnorm_fwd_f8(const void* x, int64_t ldx, const void* w, void* q, int64_t ldq, float* qscale,
+                                 int64_t R, int64_t D, float eps, void* stream) {
+  PZ_CHECK_ARG(x && w && q && qscale && D % 8 == 0 && D <= 2048 && ldx % 8 == 0 && ldq % 8 == 0 &&
+                   PZ_ALIGNED(x, 16) && PZ_ALIGNED(q, 8),
+               "rmsnorm_fwd_f8: bad args (D %% 8 == 0, D <= 2048, aligned rows)");
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + 3) / 4));
+  NORM_DISPATCH(rmsnorm_q8_kernel, grid, (const bf16_t*)x, ldx, (const bf16_t*)w, (uint8_t*)q, ldq, qscale, R, (int)D,
+                eps);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_layernorm_fwd_f8(const void* x, int64_t ldx, const void* w, const void* b, void* q, int64_t ldq,
+                                   float* qscale, int64_t R, int64_t D, float eps, void* stream) {
+  PZ_CHECK_ARG(x && w && b && q && qscale && D % 8 == 0 && D <= 2048 && ldx % 8 == 0 && ldq % 8 == 0 &&
+                   PZ_ALIGNED(x, 16) && PZ_ALIGNED(q, 8),
+               "layernorm_fwd_f8: bad args (D %% 8 == 0, D <= 2048, aligned rows)");
+  if (R == 0) return PZ_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)((R + 3) / 4));
+  NORM_DISPATCH(layernorm_q8_kernel, grid, (const bf16_t*)x, ldx, (const bf16_t*)w, (const bf16_t*)b, (uint8_t*)q, ldq,
+                qscale, R, (int)D, eps);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

@@ -95,44 +95,142 @@ __global__ void __launch_bounds__(256) absmax_kernel(const bf16_t* __restrict__ 
 
 // V^T codes for the fp8 attention (pz_flash_fwd_f8): one scale per head dim d (the column max over the nk keys:
 // O[q][d] = s_d sum_k P[q][k] v_kd, so a per-column scale factors out of the P V sum exactly), codes written transposed
-// [256 d][ldt keys], zeros for nk <= k < ldt.  Workgroup (sample, 64 d-columns): pass 1 -- thread (key phase kp, column
-// dl) takes the max over keys kp, kp + 4, ... (the 64 columns of a key row are one 128-B read); pass 2 -- thread (dl,
-// 16-key group) reads its 16 keys' values and writes their 16 codes as one 16-B store.
+// [256 d][ldt keys], zeros for nk <= k < ldt.  Workgroup (sample, 8 d-columns): pass 1 -- thread (key phase kp of 32,
+// column dl of 8) takes the max over keys kp, kp + 32, ... (8 loads in flight), reduced through LDS; pass 2 -- thread
+// (dl, 16-key group) reads its 16 keys' values and writes their 16 codes as one 16-B store.
 __global__ void __launch_bounds__(256) quant_vt_kernel(const bf16_t* __restrict__ v, int64_t ldv, int64_t vb, int64_t nk,
                                                        uint8_t* vt, float* vs, int64_t ldt) {
-  __shared__ float red[4][64];
+  __shared__ float red[32][8];
+  __shared__ float sc[8];
   const int64_t b = blockIdx.x;
-  const int dl = threadIdx.x & 63, kp = threadIdx.x >> 6;
-  const int64_t d = (int64_t)blockIdx.y * 64 + dl;
-  const bf16_t* V = v + b * vb + d;
+  const int dl = threadIdx.x & 7, kp = threadIdx.x >> 3;
+  const int64_t d0 = (int64_t)blockIdx.y * 8;
+  const bf16_t* V = v + b * vb + d0 + dl;
   float m = 0.f;
-  for (int64_t k = kp; k < nk; k += 4) m = fmaxf(m, fabsf(bf2f(V[k * ldv])));
+  int64_t k = kp;
+  for (; k + 7 * 32 < nk; k += 8 * 32) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = fabsf(bf2f(V[(k + 32 * u) * ldv]));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m = fmaxf(m, x[u]);
+  }
+  for (; k < nk; k += 32) m = fmaxf(m, fabsf(bf2f(V[k * ldv])));
   red[kp][dl] = m;
   __syncthreads();
-  m = fmaxf(fmaxf(red[0][dl], red[1][dl]), fmaxf(red[2][dl], red[3][dl]));
-  const float s = m > 0.f ? __fdiv_rn(m, E4M3_MAX) : 1.f;
-  const float inv = __fdiv_rn(1.f, s);
-  if (kp == 0) vs[b * 256 + d] = s;
-  uint8_t* T = vt + (b * 256 + d) * ldt;
-  for (int64_t k0 = (int64_t)kp * 16; k0 < ldt; k0 += 64) {
+  if (threadIdx.x < 8) {
+    float mm = 0.f;
+    for (int i = 0; i < 32; ++i) mm = fmaxf(mm, red[i][threadIdx.x]);
+    const float s = mm > 0.f ? __fdiv_rn(mm, E4M3_MAX) : 1.f;
+    sc[threadIdx.x] = s;
+    vs[b * 256 + d0 + threadIdx.x] = s;
+  }
+  __syncthreads();
+  const float inv = __fdiv_rn(1.f, sc[dl]);
+  uint8_t* T = vt + (b * 256 + d0 + dl) * ldt;
+  for (int64_t k0 = (int64_t)kp * 16; k0 < ldt; k0 += 32 * 16) {
     float f[16];
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int64_t k = k0 + e;
-      f[e] = k < nk ? fminf(fmaxf(bf2f(V[k * ldv]) * inv, -E4M3_MAX), E4M3_MAX) : 0.f;
+      const int64_t kk = k0 + e;
+      f[e] = kk < nk ? fminf(fmaxf(bf2f(V[kk * ldv]) * inv, -E4M3_MAX), E4M3_MAX) : 0.f;
     }
     *reinterpret_cast<u32x4*>(T + k0) = u32x4{enc4(f[0], f[1], f[2], f[3]), enc4(f[4], f[5], f[6], f[7]),
                                               enc4(f[8], f[9], f[10], f[11]), enc4(f[12], f[13], f[14], f[15])};
   }
 }
 
+// all operands of one fp8 attention launch in ONE launch (pz_fp8_quant_attn): rows of Q then rows of K (256 wide,
+// per-row scales as quant_rows_kernel: one wave per row, 4 values per lane), then V^T (quant_vt_kernel's workgroups)
+__global__ void __launch_bounds__(256) quant_attn_kernel(const bf16_t* __restrict__ q, int64_t nqr,
+                                                         const bf16_t* __restrict__ k, int64_t nkr,
+                                                         const bf16_t* __restrict__ v, int64_t ldv, int64_t vb,
+                                                         int64_t Z, int64_t nk, uint8_t* qc, float* qs, uint8_t* kc,
+                                                         float* ks, uint8_t* vt, float* vs, int64_t ldt) {
+  const int64_t row_wgs = (nqr + nkr + 3) / 4;
+  if ((int64_t)blockIdx.x >= row_wgs) {  // V^T: workgroup (sample, 8 columns) of the quant_vt_kernel scheme
+    const int64_t u = blockIdx.x - row_wgs;
+    __shared__ float red[32][8];
+    __shared__ float sc[8];
+    const int64_t b = u / 32;
+    const int dl = threadIdx.x & 7, kp = threadIdx.x >> 3;
+    const int64_t d0 = (u % 32) * 8;
+    const bf16_t* V = v + b * vb + d0 + dl;
+    float m = 0.f;
+    int64_t kk = kp;
+    for (; kk + 7 * 32 < nk; kk += 8 * 32) {
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = fabsf(bf2f(V[(kk + 32 * e) * ldv]));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, x[e]);
+    }
+    for (; kk < nk; kk += 32) m = fmaxf(m, fabsf(bf2f(V[kk * ldv])));
+    red[kp][dl] = m;
+    __syncthreads();
+    if (threadIdx.x < 8) {
+      float mm = 0.f;
+      for (int i = 0; i < 32; ++i) mm = fmaxf(mm, red[i][threadIdx.x]);
+      const float s = mm > 0.f ? __fdiv_rn(mm, E4M3_MAX) : 1.f;
+      sc[threadIdx.x] = s;
+      vs[b * 256 + d0 + threadIdx.x] = s;
+    }
+    __syncthreads();
+    const float inv = __fdiv_rn(1.f, sc[dl]);
+    uint8_t* T = vt + (b * 256 + d0 + dl) * ldt;
+    for (int64_t k0 = (int64_t)kp * 16; k0 < ldt; k0 += 32 * 16) {
+      float f[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t key = k0 + e;
+        f[e] = key < nk ? fminf(fmaxf(bf2f(V[key * ldv]) * inv, -E4M3_MAX), E4M3_MAX) : 0.f;
+      }
+      *reinterpret_cast<u32x4*>(T + k0) = u32x4{enc4(f[0], f[1], f[2], f[3]), enc4(f[4], f[5], f[6], f[7]),
+                                                enc4(f[8], f[9], f[10], f[11]), enc4(f[12], f[13], f[14], f[15])};
+    }
+    return;
+  }
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nqr + nkr) return;
+  const int lane = threadIdx.x & 63;
+  const bool isq = r < nqr;
+  const int64_t rr = isq ? r : r - nqr;
+  const u32x2 w = *reinterpret_cast<const u32x2*>((isq ? q : k) + rr * 256 + 4 * lane);
+  float f[4] = {__uint_as_float(w[0] << 16), __uint_as_float(w[0] & 0xffff0000u), __uint_as_float(w[1] << 16),
+                __uint_as_float(w[1] & 0xffff0000u)};
+  float m = fmaxf(fmaxf(fabsf(f[0]), fabsf(f[1])), fmaxf(fabsf(f[2]), fabsf(f[3])));
+  m = warp_max(m);
+  const float s = m > 0.f ? __fdiv_rn(m, E4M3_MAX) : 1.f;
+  const float inv = __fdiv_rn(1.f, s);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) f[e] = fminf(fmaxf(f[e] * inv, -E4M3_MAX), E4M3_MAX);
+  *reinterpret_cast<unsigned*>((isq ? qc : kc) + rr * 256 + 4 * lane) = enc4(f[0], f[1], f[2], f[3]);
+  if (lane == 0) (isq ? qs : ks)[rr] = s;
+}
+
 }  // namespace
+
+extern "C" int pz_fp8_quant_attn(const void* q, int64_t nqr, const void* k, int64_t nkr, const void* v, int64_t ldv,
+                                 int64_t v_bstride, int64_t Z, int64_t nk, void* qc, float* qs, void* kc, float* ks,
+                                 void* vt, float* vs, int64_t ldt, void* stream) {
+  PZ_CHECK_ARG(q && k && v && qc && qs && kc && ks && vt && vs && nqr > 0 && nkr > 0 && Z > 0 && nk > 0 &&
+                   ldt >= nk && ldt % 16 == 0 && PZ_ALIGNED(q, 8) && PZ_ALIGNED(k, 8) && PZ_ALIGNED(qc, 4) &&
+                   PZ_ALIGNED(kc, 4) && PZ_ALIGNED(vt, 16),
+               "fp8_quant_attn: bad args (rows of 256, ldt >= nk, ldt %% 16 == 0, aligned)");
+  const int64_t wgs = (nqr + nkr + 3) / 4 + Z * 32;
+  PZ_CHECK_ARG(wgs < (1LL << 31), "fp8_quant_attn: too many rows");
+  hipLaunchKernelGGL(quant_attn_kernel, dim3((unsigned)wgs), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q, nqr,
+                     (const bf16_t*)k, nkr, (const bf16_t*)v, ldv, v_bstride, Z, nk, (uint8_t*)qc, qs, (uint8_t*)kc,
+                     ks, (uint8_t*)vt, vs, ldt);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
 
 extern "C" int pz_fp8_quant_vt(const void* v, int64_t ldv, int64_t v_bstride, int64_t Z, int64_t nk, void* vt,
                                float* vs, int64_t ldt, void* stream) {
   PZ_CHECK_ARG(v && vt && vs && Z > 0 && nk > 0 && ldt >= nk && ldt % 16 == 0 && PZ_ALIGNED(vt, 16) && Z < 65536,
                "fp8_quant_vt: bad args (ldt >= nk, ldt %% 16 == 0, 16-byte aligned codes)");
-  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)Z, 4), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)v, ldv,
+  hipLaunchKernelGGL(quant_vt_kernel, dim3((unsigned)Z, 32), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)v, ldv,
                      v_bstride, nk, (uint8_t*)vt, vs, ldt);
   PZ_CHECK_LAUNCH();
   return PZ_OK;

@@ -19,7 +19,7 @@ if os.environ.get("PZ_LIB_PATH"):
     print(f"[pizero_native] PZ_LIB_PATH override: loading {LIB_PATH} instead of the default libpizero_hip.so",
           file=_sys.stderr, flush=True)
 
-ABI_VERSION = 18  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 19  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -124,6 +124,9 @@ SIGNATURES = {
     "pz_fp8_quant_rows": [vp, i64, vp, i64, vp, i64, i64, vp],
     "pz_fp8_quant_tensor": [vp, i64, vp, f32, vp],
     "pz_fp8_quant_vt": [vp, i64, i64, i64, i64, vp, vp, i64, vp],
+    "pz_rmsnorm_fwd_f8": [vp, i64, vp, vp, i64, vp, i64, i64, f32, vp],
+    "pz_layernorm_fwd_f8": [vp, i64, vp, vp, vp, i64, vp, i64, i64, f32, vp],
+    "pz_fp8_quant_attn": [vp, i64, vp, i64, vp, i64, i64, i64, i64, vp, vp, vp, vp, vp, vp, i64, vp],
     "pz_flash_fwd_f8": [C.POINTER(FlashArgs), vp, vp, vp, vp, i64, vp, vp, i64, vp],
     "pz_fp8_absmax": [vp, i64, vp, vp],
     "pz_gemm_kernel_name": [C.POINTER(GemmArgs)],

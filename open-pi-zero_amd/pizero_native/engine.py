@@ -332,19 +332,18 @@ class Engine:
         if f is None:
             return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
         q, sc = f
+        if isinstance(x, tuple):  # (e4m3 codes, row scales) from a fused norm + quantisation (w8a8_in): W8A8
+            return ops.linear_fp8(x[0], q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=x[1])
         M, K = x.shape
         if M <= 64:
             if K % 64:  # (SigLIP fc2, K = 4304, never has so few rows in practice)
                 return ops.linear(x, W, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
             return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, norm=norm)
         ncols = W.shape[0] // 2 if epi == PZ_EPI_GEGLU else W.shape[0]
-        if norm is None and ops.rows_w8a8_ok(M, K, ncols, epi) and x.stride(0) % 16 == 0:
-            # C5 prefill q|k|v / o rows: W8A8 on the fp8 MFMA (row-slab kernel), per-row activation scales
-            xq = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
-            xs = torch.empty(M, device=x.device, dtype=F32)
-            ops.fp8_quant_rows(x, xq, xs)
-            return ops.linear_fp8(xq, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=xs)
-        if norm is None and ops.rows_w8a16_ok(M, K, ncols):  # (PZ_ROWS_W8A8=0) W8A16 on the row-slab kernel
+        if norm is None and ops.rows_w8a16_ok(M, K, ncols):
+            # bf16 rows from a producer that cannot emit codes (the attention output into o_proj): W8A16 on the
+            # row-slab kernel -- quantising them costs a launch (~5 us) that the latency-bound W8A8 GEMM does not win
+            # back (profiles/r06/c5_fp8_ab.txt)
             return ops.linear_fp8(x, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux)
         if norm is not None:
             raise ValueError("lin: a fused norm needs <= 64 rows")
@@ -354,6 +353,23 @@ class Engine:
         xs = torch.empty(M, device=x.device, dtype=F32)
         ops.fp8_quant_rows(x, xq, xs)
         return ops.linear_fp8(xq, q, sc, out, bias=bias, resid=resid, epi=epi, aux=aux, x_scale=xs)
+
+    def w8a8_in(self, key, M, K):
+        """fp8 mode: True if the Linear ``key`` on M > 64 rows should get its A operand as e4m3 codes from a fused norm
+        (pz_rmsnorm_fwd_f8 / pz_layernorm_fwd_f8): W8A8 on the fp8 MFMA (row slab or 8-phase) with no quantisation
+        launch (PZ_FUSED_NORM_F8=0: bf16 norm output, lin() quantises or runs W8A16)"""
+        return (self.f8 is not None and key in self.f8 and M > 64 and K % 16 == 0 and
+                os.environ.get("PZ_FUSED_NORM_F8", "1") != "0")
+
+    def norm_codes(self, x, w, eps, b=None):
+        """(codes [M, K], row scales [M]) of RMSNorm (b None) / LayerNorm (b given) of x, in one launch"""
+        xq = torch.empty(x.shape, device=x.device, dtype=torch.uint8)
+        xs = torch.empty(x.shape[0], device=x.device, dtype=F32)
+        if b is None:
+            ops.rmsnorm_f8(x, w, xq, xs, eps)
+        else:
+            ops.layernorm_f8(x, w, b, xq, xs, eps)
+        return xq, xs
 
     def rope(self, theta, maxpos=None):
         """fp32 cos|sin table for positions 0..maxpos (default L + 8: every training / action position);
@@ -469,10 +485,15 @@ class Engine:
         for i in range(d.vL):
             p = f"{vt}encoder.layers.{i}."
             st = {"x": x}
-            h1 = torch.empty_like(x)
-            mu1 = torch.empty(M, device=dev, dtype=F32)
-            r1 = torch.empty(M, device=dev, dtype=F32)
-            ops.layernorm(x, self.w(p + "layer_norm1.weight"), self.w(p + "layer_norm1.bias"), h1, mu1, r1, d.ln_eps)
+            if save is None and self.w8a8_in(p + "self_attn.q_proj.weight", M, d.vH):  # fp8: LayerNorm -> codes
+                h1 = self.norm_codes(x, self.w(p + "layer_norm1.weight"), d.ln_eps, self.w(p + "layer_norm1.bias"))
+                mu1 = r1 = None
+            else:
+                h1 = torch.empty_like(x)
+                mu1 = torch.empty(M, device=dev, dtype=F32)
+                r1 = torch.empty(M, device=dev, dtype=F32)
+                ops.layernorm(x, self.w(p + "layer_norm1.weight"), self.w(p + "layer_norm1.bias"), h1, mu1, r1,
+                              d.ln_eps)
             qkv = torch.empty(M, 3 * d.vH, device=dev, dtype=BF16)
             L(h1, "self_attn.q_proj.weight", self.ar.span(p + "self_attn.q_proj.weight", p + "self_attn.v_proj.weight"),
               qkv, bias=self.ar.span(p + "self_attn.q_proj.bias", p + "self_attn.v_proj.bias"))
@@ -484,10 +505,15 @@ class Engine:
             xm = torch.empty_like(x)
             L(O, "self_attn.out_proj.weight", self.w(p + "self_attn.out_proj.weight"), xm,
               bias=self.w(p + "self_attn.out_proj.bias"), resid=x)
-            h2 = torch.empty_like(x)
-            mu2 = torch.empty(M, device=dev, dtype=F32)
-            r2 = torch.empty(M, device=dev, dtype=F32)
-            ops.layernorm(xm, self.w(p + "layer_norm2.weight"), self.w(p + "layer_norm2.bias"), h2, mu2, r2, d.ln_eps)
+            if save is None and self.w8a8_in(p + "mlp.fc1.weight", M, d.vH):  # fp8: LayerNorm -> codes
+                h2 = self.norm_codes(xm, self.w(p + "layer_norm2.weight"), d.ln_eps, self.w(p + "layer_norm2.bias"))
+                mu2 = r2 = None
+            else:
+                h2 = torch.empty_like(x)
+                mu2 = torch.empty(M, device=dev, dtype=F32)
+                r2 = torch.empty(M, device=dev, dtype=F32)
+                ops.layernorm(xm, self.w(p + "layer_norm2.weight"), self.w(p + "layer_norm2.bias"), h2, mu2, r2,
+                              d.ln_eps)
             a1 = self._sig_rows(M, dev) if save is not None else None
             g1 = self._sig_rows(M, dev)
             L(h2, "mlp.fc1.weight", self.w(p + "mlp.fc1.weight"), g1, bias=self.w(p + "mlp.fc1.bias"), epi=PZ_EPI_GELU,
@@ -1292,6 +1318,14 @@ class Engine:
                                           hd, L1, g.off, Lp, g.off,
                                           norm=(self.w(p + "input_layernorm.weight"), d.rms_eps))
                     continue
+                if not last and self.w8a8_in(p + "self_attn.q_proj.weight", M, x.shape[1]):
+                    # fp8 (C5): input RMSNorm straight to e4m3 codes, q|k|v W8A8 on the fp8 MFMA, RoPE + scatter
+                    qkv = torch.empty(M, (nh + 2) * hd, device=dev, dtype=BF16)
+                    self.lin(self.norm_codes(x, self.w(p + "input_layernorm.weight"), d.rms_eps),
+                             p + "self_attn.q_proj.weight", self.qkv_w(p), qkv)
+                    ops.qkv_rope_split(qkv, pos[g.pos_key], self.rope(g.theta), Q, Kj, Vj, B, g.T, nh, 1, hd, L1,
+                                       g.off, Lp, g.off)
+                    continue
                 h = torch.empty_like(x)
                 ops.rmsnorm(x, self.w(p + "input_layernorm.weight"), h, None, d.rms_eps)
                 if last:  # only K/V are consumed downstream (pizero.py:451, skipped post-attn)
@@ -1404,13 +1438,11 @@ class Engine:
         hd, Lp = self.d.hd, K.shape[1]
         qc = torch.empty(B * nq, hd, device=dev, dtype=torch.uint8)
         qs = torch.empty(B * nq, device=dev, dtype=F32)
-        ops.fp8_quant_rows(Q.reshape(B * nq, hd), qc, qs)
         kc = torch.empty(B * Lp, hd, device=dev, dtype=torch.uint8)
         ks = torch.empty(B * Lp, device=dev, dtype=F32)
-        ops.fp8_quant_rows(K.reshape(B * Lp, hd), kc, ks)
         vt = torch.empty(B, hd, (nk + 127) // 128 * 128, device=dev, dtype=torch.uint8)
         vs = torch.empty(B, hd, device=dev, dtype=F32)
-        ops.fp8_quant_vt(V, B, nk, vt, vs)
+        ops.fp8_quant_attn(Q.reshape(B * nq, hd), K.reshape(B * Lp, hd), V, B, nk, qc, qs, kc, ks, vt, vs)
         ops.flash_fwd_f8(fa, qc, qs, kc, ks, Lp, vt, vs)
 
     def _attn_flash_infer(self, Q, K, V, outs, Lq, nk, tok0, cnt, B):
@@ -1436,6 +1468,9 @@ class Engine:
         if self.few_rows(M, x.shape[1]):  # few rows (denoise / proprio): RMSNorm fused into the gate|up GEMM
             self.lin(xm, p + "mlp.gate_proj.weight", self.gu_w(p), hm, epi=PZ_EPI_GEGLU,
                      norm=(self.w(p + "post_attention_layernorm.weight"), d.rms_eps))
+        elif self.w8a8_in(p + "mlp.gate_proj.weight", M, x.shape[1]):  # fp8: RMSNorm -> codes -> W8A8 GeGLU
+            self.lin(self.norm_codes(xm, self.w(p + "post_attention_layernorm.weight"), d.rms_eps),
+                     p + "mlp.gate_proj.weight", self.gu_w(p), hm, epi=PZ_EPI_GEGLU)
         else:
             h2 = torch.empty_like(x)
             ops.rmsnorm(xm, self.w(p + "post_attention_layernorm.weight"), h2, None, d.rms_eps)

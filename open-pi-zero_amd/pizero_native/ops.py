@@ -180,6 +180,19 @@ def fp8_quant_rows(x, q, row_scale):
     call("pz_fp8_quant_rows", _p(x), x.stride(0), _p(q), q.stride(0), _p(row_scale), R, D, _st())
 
 
+def rmsnorm_f8(x, w, q, qscale, eps):
+    """Gemma RMSNorm of x [R, D] straight to e4m3 codes q [R, D] + per-row scales (pz_rmsnorm_fwd_f8)"""
+    R, D = x.shape
+    call("pz_rmsnorm_fwd_f8", _p(x), x.stride(0), _p(w), _p(q), q.stride(0), _p(qscale), R, D, float(eps), _st())
+
+
+def layernorm_f8(x, w, b, q, qscale, eps):
+    """LayerNorm of x [R, D] straight to e4m3 codes q [R, D] + per-row scales (pz_layernorm_fwd_f8)"""
+    R, D = x.shape
+    call("pz_layernorm_fwd_f8", _p(x), x.stride(0), _p(w), _p(b), _p(q), q.stride(0), _p(qscale), R, D, float(eps),
+         _st())
+
+
 def fp8_quant_tensor(x, q, scale):
     """q = e4m3(x / scale) elementwise (weights; scale = max|x| / 448 from fp8_weight_scale)"""
     call("pz_fp8_quant_tensor", _p(x), x.numel(), _p(q), 1.0 / float(scale), _st())
@@ -516,6 +529,13 @@ def flash_fwd(a):
 def fp8_quant_vt(v, Z, nk, vt, vs):
     """V^T e4m3 codes vt [Z, 256, ldt] (zero past nk) and per-head-dim scales vs [Z, 256] of bf16 V [Z, rows, 256]"""
     call("pz_fp8_quant_vt", _p(v), v.stride(1), v.stride(0), Z, nk, _p(vt), _p(vs), vt.shape[2], _st())
+
+
+def fp8_quant_attn(q, k, v, Z, nk, qc, qs, kc, ks, vt, vs):
+    """pz_fp8_quant_attn: Q rows q [R, 256] and key rows k [Rk, 256] per row, V [Z, rows, 256] per head dim (V^T codes
+    vt [Z, 256, ldt]) -- the operands of flash_fwd_f8 in one launch"""
+    call("pz_fp8_quant_attn", _p(q), q.shape[0], _p(k), k.shape[0], _p(v), v.stride(1), v.stride(0), Z, nk, _p(qc),
+         _p(qs), _p(kc), _p(ks), _p(vt), _p(vs), vt.shape[2], _st())
 
 
 def flash_fwd_f8(a, qc, qs, kc, ks, krows, vt, vs):

@@ -310,8 +310,36 @@ def test_flash_fwd_f8(B, P, cnt, key_split):
     ref = _joint_ref(qd, kd, vd, cnt, P, C, L, nh).view(B, L, nh, hd)
     # pad rows (dead prefix tokens) are uniform averages: compare the live rows and the dead ones together
     assert _rel(got, ref) <= 3e-2, _rel(got, ref)
-    # the bf16 kernel on the unquantised operands
+    # the bf16 kernel on the unquantised operands: the fp8 deviation itself (e4m3's 3 mantissa bits on these synthetic
+    # logits of std ~4 -- sharp softmax rows; measured 0.085 at the C5 shape), bounded loosely; the model-level C5 gate
+    # (tests/test_c5_pizero_gpu.py) holds the fp8 chunk to the bf16 chunk
     Ov2, Oe2 = torch.empty_like(Ov), torch.empty_like(Oe)
     ops.flash_fwd(args(Ov2, Oe2))
     bf = torch.cat([Ov2.view(B, P, nh, hd), Oe2.view(B, C, nh, hd)], 1).float()
-    assert _rel(got, bf) <= 6e-2, _rel(got, bf)
+    print(f"[fp8 attention] rel-L2 vs dequantised fp32 {_rel(got, ref):.4f}, vs the bf16 kernel {_rel(got, bf):.4f}")
+    assert _rel(got, bf) <= 0.15, _rel(got, bf)
+
+
+@pytest.mark.parametrize("R,D", [(788, 2048), (768, 1152), (5, 1024)])
+def test_fused_norm_quant_matches_two_step(R, D):
+    """pz_rmsnorm_fwd_f8 / pz_layernorm_fwd_f8 (the fp8 prefill's norm + activation quantisation in one launch) give
+    the codes and scales of the bf16 norm followed by pz_fp8_quant_rows, bit for bit"""
+    x = _rand(R, D, scale=2.0, seed=R)
+    w = _rand(D, scale=0.3, seed=1)
+    b = _rand(D, scale=0.3, seed=2)
+    for ln in (False, True):
+        h = torch.empty(R, D, device=DEV, dtype=torch.bfloat16)
+        if ln:
+            ops.layernorm(x, w, b, h, None, None, 1e-6)
+        else:
+            ops.rmsnorm(x, w, h, None, 1e-6)
+        q_ref = torch.empty(R, D, device=DEV, dtype=torch.uint8)
+        s_ref = torch.empty(R, device=DEV, dtype=torch.float32)
+        ops.fp8_quant_rows(h, q_ref, s_ref)
+        q = torch.empty_like(q_ref)
+        s = torch.empty_like(s_ref)
+        if ln:
+            ops.layernorm_f8(x, w, b, q, s, 1e-6)
+        else:
+            ops.rmsnorm_f8(x, w, q, s, 1e-6)
+        assert torch.equal(s, s_ref) and torch.equal(q, q_ref), (ln, int((q != q_ref).sum()))

@@ -236,9 +236,11 @@ def c5_inference(cfg, dev, iters):
     return {"metric": "action-chunk infer ms, Pi0-paper shape (3 images = 768 img tokens + 20 text + "
                       "1 proprio, chunk 50, B=1, prefill + 10 Euler steps)",
             "graph_ms": ms, "dtype": "bf16", "fp8_graph_ms": ms8,
-            "fp8": "e4m3 weights (per-tensor scales) for every SigLIP / vlm / action-expert Linear: prefill MLP "
-                   "GEMMs W8A8 on the fp8 MFMA (per-row activation scales), prefill q|k|v / o and denoise W8A16 "
-                   "(codes expanded to bf16); attention QK^T / PV bf16",
+            "fp8": "e4m3 weights (per-tensor scales) for every SigLIP / vlm / action-expert Linear: prefill q|k|v and "
+                   "MLP GEMMs W8A8 on the fp8 MFMA (per-row activation scales; the q|k|v / gate|up / fc1 inputs "
+                   "quantised inside the preceding RMSNorm / LayerNorm), prefill o and the denoise W8A16 (codes expanded "
+                   "to bf16); prefill joint attention QK^T and PV on the fp8 MFMA (pz_flash_fwd_f8: per-row Q / K, "
+                   "per-head-dim V scales, P as e4m3(256 p)); SigLIP and denoise attention bf16",
             "fp8_vs_bf16_chunk_rel_l2": rel, "replays_timed": iters, "higher_is_better": False, "baseline_ms": 73.0,
             "baseline_source": "Pi0 paper figure quoted in the reference README.md:80,84 (other hardware)",
             "vs_baseline": 73.0 / ms, "fp8_vs_baseline": 73.0 / ms8,
@@ -246,7 +248,8 @@ def c5_inference(cfg, dev, iters):
                          "fp8": roof(pre8, den8, PEAK_FP8_TFLOPS, den_b8),
                          "note": "phases timed as separate hipGraphs on the graph's static inputs; prefill flop = the "
                                  "reference's FlopCounterMode count (SURVEY 8(d) C5), priced for fp8 against the fp8 "
-                                 "dense peak although its q|k|v / o and attention run on the bf16 MFMA; denoise bytes = "
+                                 "dense peak although its o projection, SigLIP attention and few-row GEMMs run on the "
+                                 "bf16 MFMA; denoise bytes = "
                                  "10 x (action-expert layers + norm + action encoder / decoder weights, proj weights "
                                  "1 B in fp8) + the K/V rows each step reads"}}
 

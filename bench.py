@@ -67,10 +67,10 @@ def synthetic_batch(model, B, device, gen):
 
 def pmc_traffic(kname, shape):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes
-    (the newest of profiles/r05, r04, r03 pmc_dominant.json; tools/pmc_dominant.sh + tools/pmc_summary.py):
+    (the newest of profiles/r06, r05, r04, r03 pmc_dominant.json; tools/pmc_dominant.sh + tools/pmc_summary.py):
     FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md "HBM") + WRITE_SIZE; None if it is for another
     kernel/shape."""
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_dominant.json")
         if os.path.exists(path):
             break

@@ -18,6 +18,25 @@ sig = [r for r in rows if "flash_fwd_sig" in r["Kernel_Name"]]
 print(len(rows), "dispatches;", len(sig), "flash_fwd_sig")
 keys = [k for k in rows[0] if "Queue" in k or "Stream" in k]
 print("queue/stream columns:", keys)
+# every kernel's longest dispatch against its median (a stalled dispatch stands out), and same-queue overlaps:
+# dispatch n + 1 starting before dispatch n ends on one queue (in-order streams: a timestamp artefact or a real race)
+import statistics
+by = {}
+for r in rows:
+    by.setdefault(r["Kernel_Name"][:80], []).append(r["e"] - r["s"])
+print("longest dispatch / median per kernel (top 8 by ratio):")
+rat = sorted(((max(v) / max(1, statistics.median(v)), k, max(v), statistics.median(v), len(v)) for k, v in by.items()),
+             reverse=True)
+for q, k, mx, md, n in rat[:8]:
+    print(f"    x{q:8.1f}  max {mx / 1e6:9.3f} ms  median {md / 1e6:8.3f} ms  n {n:5d}  {k}")
+byq = {}
+for r in rows:
+    byq.setdefault((r.get("Queue_Id"), r.get("Stream_Id")), []).append(r)
+for q, lst in byq.items():
+    lst.sort(key=lambda r: r["s"])
+    ov = [(a["e"] - b["s"]) for a, b in zip(lst, lst[1:]) if b["s"] < a["e"]]
+    print(f"queue/stream {q}: {len(lst)} dispatches, {len(ov)} start before the previous one ends"
+          + (f" (overlap max {max(ov) / 1e3:.1f} us, median {statistics.median(ov) / 1e3:.1f} us)" if ov else ""))
 for r in sig[:6] + sig[-3:]:
     d = (r["e"] - r["s"]) / 1e6
     ov = [o for o in rows if o is not r and o["s"] < r["e"] and o["e"] > r["s"]]

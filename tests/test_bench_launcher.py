@@ -105,3 +105,25 @@ def test_bench_two_ranks_one_gpu():
     assert dd["buckets_reduced_per_step"] >= 2
     assert dd["replica_weights_equal"] is True
     assert out["value"] > 0 and out["loss_mean"] == out["loss_mean"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_bench_four_ranks_one_gpu():
+    """The data-parallel path at world size 4 on one card (gloo, PZ_RANKS_PER_GPU=4): the launcher's sysfs count (1
+    GPU x 4 ranks), 4 replicas that each run one micro-batch per step, gradient buckets reduced across 4 ranks, equal
+    replica weights after the step and a finite loss -- the widest rehearsal of the driver's 8-GPU run one card holds
+    (C3 itself needs 8 cards: RCCL refuses two ranks on one device)."""
+    r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "4", "--micro-batch", "4", "--global-batch", "16",
+                        "--steps", "1", "--warmup", "1", "--no-infer", "--no-cpu-baseline"],
+                       env=_env(PZ_DIST_BACKEND="gloo", PZ_RANKS_PER_GPU="4"), capture_output=True, text=True,
+                       timeout=840)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    print(json.dumps({k: out[k] for k in ("n_gpus", "value", "ms_per_step", "ddp", "config", "loss_per_step")}))
+    assert out["n_gpus"] == 4 and out["config"]["parallelism"] == "dp4"
+    assert out["config"]["global_batch"] == 16 and out["config"]["grad_accum"] == 1
+    assert out["ddp"]["replica_weights_equal"] is True
+    assert all(v == v for v in out["loss_per_step"])

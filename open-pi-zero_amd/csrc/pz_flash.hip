@@ -2559,13 +2559,6 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2) {
         f32x4 dsv[2][2];  // dS^T (without the scale) [16-key block of the k-step][query block]
-        // K^T fragments of this k-step (inline-asm transposed reads, waited for before the dQ MFMAs below): issued
-        // first, so their LDS latency runs under the S / dP MFMAs
-        s16x4 tk[5][2];
-#define FS_TR(db, hf) tk[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(ka + k2 * 32 * FS_ROW * 2)
-        FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1); FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
-        FS_TR(4, 0); FS_TR(4, 1);
-#undef FS_TR
 #pragma unroll
         for (int i2 = 0; i2 < 2; ++i2) {
           const int i = 2 * k2 + i2;
@@ -2589,7 +2582,12 @@ __global__ void __launch_bounds__(FS_NW * 64, 1) flash_bwd_q_sig_kernel(pz_flash
           }
         }
         const bf16x8 sb0 = pack8(dsv[0][0], dsv[1][0]), sb1 = pack8(dsv[0][1], dsv[1][1]);
-        // dQ^T += K^T dS^T over these 32 keys (the K^T fragments were issued at the top of the k-step)
+        // dQ^T += K^T dS^T over these 32 keys: K^T fragments by inline-asm transposed reads (see the forward)
+        s16x4 tk[5][2];
+#define FS_TR(db, hf) tk[db][hf] = fs_tr<(16 * (hf)) * FS_ROW * 2 + (db) * 32>(ka + k2 * 32 * FS_ROW * 2)
+        FS_TR(0, 0); FS_TR(0, 1); FS_TR(1, 0); FS_TR(1, 1); FS_TR(2, 0); FS_TR(2, 1); FS_TR(3, 0); FS_TR(3, 1);
+        FS_TR(4, 0); FS_TR(4, 1);
+#undef FS_TR
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(tk[0][0]), "+v"(tk[0][1]), "+v"(tk[1][0]), "+v"(tk[1][1]), "+v"(tk[2][0]), "+v"(tk[2][1]),
                        "+v"(tk[3][0]), "+v"(tk[3][1]), "+v"(tk[4][0]), "+v"(tk[4][1]));

@@ -1820,6 +1820,12 @@ static bool use_8phase();
 static bool use_khalf(bool akc, bool bkc, int64_t m, int64_t n, int64_t k);
 
 namespace {
+// skinny-64 split-K: partials summed in the launch (default) or by splitk_epilogue_kernel (PZ_SK64_FUSED=0)
+static bool sk64_two_launch() {
+  const char* e = getenv("PZ_SK64_FUSED");
+  return e && e[0] == '0';
+}
+
 enum PathKind { PATH_SKINNY, PATH_256, PATH_TILE, PATH_SPLIT, PATH_GEMV, PATH_SKINNY64, PATH_ROWS, PATH_TALL };
 struct Plan {
   PathKind kind;
@@ -1979,6 +1985,14 @@ bool plan_tall(Plan& pl, const pz_gemm_args* a, int64_t ncols) {
 }
 
 // Kernel choice for a validated argument set (shared by pz_gemm and pz_gemm_kernel_name).
+// skinny-64 split-K combined in the launch: S tile-private [64][nc] fp32 slabs per tile fit the workspace (bf16 C,
+// forward epilogue)
+static bool sk64_fits(const Plan& pl, const pz_gemm_args* a) {
+  const int64_t tiles = pl.tiles_n * ((a->M + 63) / 64);
+  return (int64_t)pl.splits * tiles * 64 * pl.skinny_nc * 4 <= a->ws_bytes && !a->c_fp32 &&
+         a->epilogue < PZ_EPI_DGELU;
+}
+
 Plan make_plan(const pz_gemm_args* a) {
   Plan pl{};
   pl.akc = a->a_kcontig != 0;
@@ -2171,7 +2185,8 @@ extern "C" const char* pz_gemm_kernel_name(const pz_gemm_args* a) {
       break;
     case PATH_SKINNY64:
       snprintf(buf, sizeof(buf), "gemm_skinny64_kernel<%d, %d, %d, %s>%s", pl.skinny_w, pl.skinny_nc, pl.skinny_mb,
-               bstr(a->fp8_mode == 2), pl.ksplit > 0 ? "+splitk_epilogue_kernel" : "");
+               bstr(a->fp8_mode == 2),
+               pl.ksplit > 0 && (sk64_two_launch() || !sk64_fits(pl, a)) ? "+splitk_epilogue_kernel" : "");
       break;
     case PATH_GEMV:
       snprintf(buf, sizeof(buf), "gemv_kernel<M<=%d>", a->M <= 4 ? 4 : 8);
@@ -2432,6 +2447,8 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
       p.ws = (float*)a->workspace;
       p.ksplit = pl.ksplit;
       p.ldw = pl.ldw;
+      // in-launch combine: S tile-private [64][nc] fp32 slabs per tile, bf16 C with a forward epilogue
+      p.sk_tk = sk64_fits(pl, a) ? 0 : -1;
     }
     return pz_sk64_launch(p, pl.skinny_w, pl.skinny_nc, pl.skinny_mb, a->fp8_mode == 2, pl.tiles_n, st);
   }

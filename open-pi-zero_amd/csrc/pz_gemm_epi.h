@@ -21,6 +21,9 @@ struct GemmP {
   // split-K (batch-1 only): blockIdx.y = split index; raw fp32 partials -> ws[z][M][ldw]
   float* ws;
   int64_t ksplit, ldw;
+  // skinny-64 split-K combined inside the launch (gemm_skinny64_kernel): first arrival counter of this launch's
+  // tiles in g_sk_ctr; -1 = partials summed by a separate splitk_epilogue_kernel launch
+  int sk_tk;
   // batched 128-tile launches (gemm_kernel, batch % 8 == 0, no split-K): 1-D grid, the tiles of one batch
   // entry on one XCD so its operand panels are shared in that XCD's L2 (batch_xcd = number of batch entries)
   int batch_xcd;

@@ -1,4 +1,6 @@
 // Few-row (skinny-64) and row-slab GEMM kernels (own translation unit: pz_gemm.hip takes minutes to compile).
+#include <atomic>
+
 #include "pz_gemm_epi.h"
 
 namespace {
@@ -255,6 +257,66 @@ __global__ void __launch_bounds__(W * 64, W == 4 ? 2 : 1) gemm_rows_f8a_kernel(G
 // Requires K % 64 == 0, k-contiguous A and B, batch 1.
 // -------------------------------------------------------------------------
 
+// Split-K combined inside the launch (the C5 denoise o / down projections: 64 tiles x 4 K-slices): every slice
+// writes its fp32 partial tile write-through (sc1, 16 B per lane) into a slab private to the tile
+// (ws[z][tile][64][NC]: no 128-B line is shared by two tiles), drains its stores and joins a barrier; one lane adds to
+// the tile's arrival counter (relaxed, agent scope); the slice that arrives last resets the counter and sums the S
+// slabs in slice order with sc1 loads (L1 bypassed: cdna_hip_programming.md Guideline 16's counter hand-off, every
+// store and load of the slabs sc1, so no release or acquire fence) and runs the epilogue, whose residual / bias
+// loads every slice issued before the hand-off.  Same partials, same order: the bits of the two-launch form
+// (splitk_epilogue_kernel), one kernel boundary less per projection.  Counters live in g_sk_ctr (zero at load,
+// reset by each tile's reducer); the host hands every launch its own range (launch_sk64), so launches on concurrent
+// streams never share one.
+constexpr int SK_CTRS = 1 << 16;
+__device__ unsigned g_sk_ctr[SK_CTRS];
+
+template <int NC>
+__device__ __forceinline__ void sk64_combine(const GemmP& p, const f32x4& o, bool mine, int64_t row0, int64_t Mc,
+                                             int64_t n0, int64_t ncols, int g, f32x4* lds) {
+  constexpr int Q = NC / 4;
+  const int S = (int)gridDim.z, T = (int)(gridDim.x * gridDim.y), tile = (int)(blockIdx.y * gridDim.x + blockIdx.x);
+  const int t = (int)threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.ws, (short)0, 0x7fffffff, 0x00020000);
+  if (mine && 4 * g < NC) {
+    const int rl = (t >> 6) * 16 + (t & 15);
+    const int off = (((int)blockIdx.z * T + tile) * 64 + rl) * NC + 4 * g;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), rs, off * 4, 0, 16);  // aux 16: sc1
+  }
+  // the reducer's epilogue side inputs (residual, bias), loaded by every slice before the hand-off
+  const bool red_ok = t < Mc * Q && n0 + 4 * (t % Q) < ncols;
+  const int64_t m = row0 + t / Q, n = n0 + 4 * (t % Q);
+  Side sd;
+  u32x2 bias = {0u, 0u};
+  if (red_ok) {
+    epi_load4<EM_BF16>(p, 0, 0, m, n, sd);
+    bias = epi_load_bias(p, n);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before the arrival
+  __syncthreads();
+  unsigned* flag = reinterpret_cast<unsigned*>(lds);  // (the reduction array: every wave has read it)
+  if (t == 0) {
+    unsigned* ctr = g_sk_ctr + p.sk_tk + tile;
+    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = old == (unsigned)(S - 1);
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0u || !red_ok) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the hand-off)
+  // reducer: one thread per (row, 4 columns) = 16 contiguous bytes of each slab; all S loads in flight (clamped
+  // slice index, no branch around a load), summed from +0 in slice order
+  u32x4 v[8];
+#pragma unroll
+  for (int z = 0; z < 8; ++z)
+    v[z] = __builtin_amdgcn_raw_buffer_load_b128(rs, ((min(z, S - 1) * T + tile) * 64 * NC + 4 * t) * 4, 0, 16);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int z = 0; z < 8; ++z)
+    if (z < S) acc += __builtin_bit_cast(f32x4, v[z]);
+  epi_store4<EM_BF16>(p, 0, 0, m, n, acc, sd, bias);
+}
+
 template <int W, int NC, int MB, bool F8W>
 __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   static_assert(W >= MB, "one wave per row block in the epilogue");
@@ -391,6 +453,10 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
     if (mb < MB)
       for (int w = 0; w < W; ++w) o2 += red[w][mb][lane];
   }
+  if (split && p.sk_tk >= 0) {  // every wave joins the combine's barriers (host: no norm / GeGLU / RoPE with split)
+    sk64_combine<NC>(p, o, mb < MB && mb * 16 + (lane & 15) < Mc, row0, Mc, n0, ncols, g, &red[0][0][0]);
+    return;
+  }
   if (mb >= MB) return;
   const int64_t ml = mb * 16 + (lane & 15);
   if (rope) {  // (host: no split, no GeGLU / bias / residual)
@@ -436,7 +502,7 @@ __global__ void __launch_bounds__(W * 64) gemm_skinny64_kernel(GemmP p) {
   }
   if (ml >= Mc) return;
   const int64_t mm = row0 + ml;
-  if (split) {  // (host: no fused norm, no GeGLU with split)
+  if (split) {  // two-launch form: partials for splitk_epilogue_kernel
     float* wz = p.ws + (int64_t)blockIdx.z * p.M * p.ldw + mm * p.ldw;
     for (int r = 0; r < 4; ++r) {
       const int64_t nn = n0 + 4 * g + r;
@@ -541,12 +607,23 @@ int pz_rows_launch(const GemmP& p, int w, int tnb, bool geglu, int f8w, hipStrea
 }
 
 template <int W, int NC, int MB, bool F8W>
-static int launch_sk64(const GemmP& p, int64_t tiles_n, hipStream_t st) {
+static int launch_sk64(const GemmP& p0, int64_t tiles_n, hipStream_t st) {
+  GemmP p = p0;
   const int S = p.ksplit > 0 ? (int)((p.K / 64 + p.ksplit / 64 - 1) / (p.ksplit / 64)) : 1;
+  const int64_t tiles = tiles_n * ((p.M + 63) / 64);
+  // in-launch combine (PZ_SK64_FUSED=0: the two-launch form, A/B; read per call): each launch gets its own range
+  // of arrival counters, dealt round-robin in 256-counter steps (256 launches in flight before a range is reused)
+  const char* e = getenv("PZ_SK64_FUSED");
+  const bool fits = p.sk_tk >= 0;  // (pz_gemm: the tile-private slabs fit the workspace, forward bf16 epilogue)
+  p.sk_tk = -1;
+  if (S > 1 && S <= 8 && tiles <= 256 && fits && !(e && e[0] == '0')) {
+    static std::atomic<unsigned> next{0};
+    p.sk_tk = (int)((next.fetch_add(1) % (SK_CTRS / 256)) * 256);
+  }
   hipLaunchKernelGGL((gemm_skinny64_kernel<W, NC, MB, F8W>), dim3((unsigned)tiles_n, (unsigned)((p.M + 63) / 64), S),
                      dim3(W * 64), 0, st, p);
   PZ_CHECK_LAUNCH();
-  if (S > 1) return pz_splitk_epi_launch(p, S, st);
+  if (S > 1 && p.sk_tk < 0) return pz_splitk_epi_launch(p, S, st);
   return PZ_OK;
 }
 

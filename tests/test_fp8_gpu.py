@@ -343,3 +343,51 @@ def test_fused_norm_quant_matches_two_step(R, D):
         else:
             ops.rmsnorm_f8(x, w, q, s, 1e-6)
         assert torch.equal(s, s_ref) and torch.equal(q, q_ref), (ln, int((q != q_ref).sum()))
+
+
+# ---- round 6: skinny-64 split-K combined inside the launch -------------------------------------------------------
+
+
+@pytest.mark.parametrize("f8w", [False, True])
+@pytest.mark.parametrize("M", [17, 50, 64])
+@pytest.mark.parametrize("N,K,epi", [(1024, 4096, PZ_EPI_NONE), (1024, 2048, PZ_EPI_SILU), (1000, 2048, PZ_EPI_GELU),
+                                     (520, 4096, PZ_EPI_NONE)])
+def test_skinny64_inlaunch_splitk_bitwise(f8w, M, N, K, epi, monkeypatch):
+    """The narrow C5 denoise projections (o / down: 64 column blocks) split K over 4 slices; the slice that arrives
+    last sums the partial slabs and runs the epilogue inside the launch (gemm_skinny64_kernel + sk64_combine).
+    Bitwise equal to the two-launch form (PZ_SK64_FUSED=0: the same partials summed in the same order by
+    splitk_epilogue_kernel), over 12 calls with new inputs each (the workspace slabs and this CU's caches hold the
+    previous call's partials) while a side stream holds 32 CUs for the first 6 (slices of a tile land on uneven
+    CUs / XCDs) -- a reducer that read a stale slab would differ."""
+    name = ops.gemm_kernel_name(M, N, K, epi=epi, fp8_mode=2 if f8w else 0)
+    assert name.startswith("gemm_skinny64_kernel") and "splitk" not in name, name
+    monkeypatch.setenv("PZ_SK64_FUSED", "0")
+    assert ops.gemm_kernel_name(M, N, K, epi=epi, fp8_mode=2 if f8w else 0).endswith("+splitk_epilogue_kernel")
+    monkeypatch.delenv("PZ_SK64_FUSED")
+    W = _rand(N, K, scale=0.03, seed=N + K)
+    Wq, ws = _quant_w(W)
+    bias = _rand(N, scale=0.1, seed=4) if epi != PZ_EPI_NONE else None
+    aux = [torch.empty(M, N, device=DEV, dtype=torch.bfloat16) for _ in range(2)] if epi != PZ_EPI_NONE else [None] * 2
+    side = torch.cuda.Stream()
+    for it in range(12):
+        x = _rand(M, K, scale=1.0 + it, seed=100 * it + M)
+        resid = _rand(M, N, seed=it) if epi == PZ_EPI_NONE else None
+        outs = [torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16) for _ in range(2)]
+        for j, fused in enumerate((True, False)):
+            if it < 6:
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    ops.debug_spin(32, 200000)
+            monkeypatch.setenv("PZ_SK64_FUSED", "1" if fused else "0")
+            if f8w:
+                ops.linear_fp8(x, Wq, ws, outs[j], bias=bias, resid=resid, epi=epi, aux=aux[j])
+            else:
+                ops.linear(x, W, outs[j], bias=bias, resid=resid, epi=epi, aux=aux[j])
+            torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (it, int((outs[0] != outs[1]).sum()))
+        if aux[0] is not None:
+            assert torch.equal(aux[0], aux[1]), it
+    monkeypatch.delenv("PZ_SK64_FUSED")
+    ref = _epi_ref(x.float() @ (_deq(Wq, ws) if f8w else W.float()).t(), epi, bias, resid)
+    assert _rel(outs[0].float(), ref) < 1e-2, _rel(outs[0].float(), ref)

@@ -40,6 +40,19 @@ def graph_us(fn, n, reps=5):
     return e0.elapsed_time(e1) * 1e3 / (reps * n)
 
 
+def eager_us(fn, n, reps=3):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps * n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * n)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=500)
@@ -50,10 +63,12 @@ def main():
     t = torch.zeros(16, device=dev)
     res = {}
     res["torch add_ (16 fp32)"] = graph_us(lambda: t.add_(1.0), a.n)
+    res["torch add_ (16 fp32), eager"] = eager_us(lambda: t.add_(1.0), a.n)
     res["pz_copy_rows 4x1024"] = graph_us(lambda: ops.copy_rows(x, 1024, 0, y, 1024, 0, 1, 4, 1024), a.n)
     tt = torch.rand(1, device=dev)
     te = torch.empty(1, 1024, device=dev, dtype=torch.bfloat16)
     res["pz_time_embed 1x1024"] = graph_us(lambda: ops.time_embed(tt, te, 100.0), a.n)
+    res["pz_time_embed 1x1024, eager"] = eager_us(lambda: ops.time_embed(tt, te, 100.0), a.n)
     for (N, K) in ((1024, 2048), (1024, 4096), (2560, 1024), (8192, 1024)):
         W = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         xa = torch.randn(4, K, device=dev).to(torch.bfloat16)

@@ -524,7 +524,7 @@ __global__ void __launch_bounds__(256) flash_bwd_prep_kernel(pz_flash_args a) {
 
 // dK, dV: grid (ceil(nk / 64), Z * H), 4 waves; wave w owns keys kb*64 + 16w + (lane & 15) and
 // sweeps every query row of the unit in staged steps of 32 (Q, dO, lse, delta in LDS)
-// FM: 0 generic element-wise (fa_logit_d), 1 fast path (FaFast), 2 fast path with the soft-cap.
+// FM: 1 fast element-wise path (FaFast), 2 the same with the soft-cap.
 // 1-D grid of nkb x (units x splits) workgroups, the key blocks of one (unit, split) on one XCD.
 template <int HD, int FM>
 __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_kernel(pz_flash_args a, int splits) {
@@ -572,12 +572,10 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     const int64_t rr = r0 + threadIdx.x;
     lse_v = threadIdx.x < FA_QS && rr < a.nq ? a.lse[zh * a.nq + rr] : 0.f;
     del_v = threadIdx.x < FA_QS && rr < a.nq ? a.delta[zh * a.nq + rr] : 0.f;
-    if constexpr (FM != 0) {
-      const int t = mk.token((int)rr);
-      lse_v *= 1.4426950408889634f;
-      rbw_v = fa_row_bits(mk, t);
-      crw_v = mk.dead(t) ? 0.f : ff.crow_live;
-    }
+    const int t = mk.token((int)rr);
+    lse_v *= 1.4426950408889634f;
+    rbw_v = fa_row_bits(mk, t);
+    crw_v = mk.dead(t) ? 0.f : ff.crow_live;
   };
   load_rows((int64_t)qs0 * FA_QS);
   // this workgroup's keys / values, read as B operands (n = key, k = head dim) from LDS:
@@ -644,16 +642,10 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int rr = i * 16 + 4 * g + e;
-        const int r = (int)r0 + rr;
         float pe = 0.f, dse = 0.f;
-        if constexpr (FM != 0) {  // rows past nq: zero Q / dO rows and delta, no contribution
-          const bool ok = wfull || ((rbw_s[rr] >> kcl) & 1);
-          ff.eval<FM == 2>(sv[e], dp[e], lse_s[rr], crw_s[rr], del_s[rr], ok, pe, dse);
-        } else if (r < a.nq) {
-          const FaLogit lg = fa_logit_d(mk, sv[e], mk.token(r), key);
-          pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse_s[rr]);
-          dse = pe * (dp[e] - del_s[rr]) * lg.dxds;
-        }
+        // (rows past nq: zero Q / dO rows and delta, no contribution)
+        const bool ok = wfull || ((rbw_s[rr] >> kcl) & 1);
+        ff.eval<FM == 2>(sv[e], dp[e], lse_s[rr], crw_s[rr], del_s[rr], ok, pe, dse);
         p[i][e] = pe;
         ds[i][e] = dse;
       }
@@ -695,10 +687,8 @@ __global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_kv_ke
     __syncthreads();
   }
   if (key >= a.nk) return;
-  if constexpr (FM != 0) {  // the fast path's dS' excludes the softmax scale
 #pragma unroll
-    for (int db = 0; db < D::NDB; ++db) dk[db] *= ff.scale;
-  }
+  for (int db = 0; db < D::NDB; ++db) dk[db] *= ff.scale;  // the fast path's dS' excludes the softmax scale
   if (splits > 1) {  // fp32 partial sums of this query split -> ws[split][unit][key][HD] (dK), then dV
     const int64_t slab = ZH * a.nk * HD;
     float* pk = a.ws + ((int64_t)split * ZH + zh) * a.nk * HD + (int64_t)key * HD;
@@ -744,129 +734,7 @@ __global__ void __launch_bounds__(256) flash_bwd_kv_reduce_kernel(pz_flash_args 
   *reinterpret_cast<u32x2*>(dst + d) = u32x2{pack2bf(acc[0], acc[1]), pack2bf(acc[2], acc[3])};
 }
 
-// dQ: grid (ceil(nq / 64), Z * H), 4 waves x 16 query rows; recomputes S^T, dP^T per staged key
-// block.  Also produces delta = rowsum(dO * O) of its rows (read by the dK/dV pass, launched after).
-template <int HD>
-__global__ void __launch_bounds__(FA_NW * 64, HD == 256 ? 1 : 2) flash_bwd_q_kernel(pz_flash_args a) {
-  using D = FaDims<HD>;
-  constexpr int NT = FA_NW * 64;
-  __shared__ __attribute__((aligned(16))) bf16_t Ks2[2][FA_KB * D::ROW];  // double-buffered K / V tiles
-  __shared__ __attribute__((aligned(16))) bf16_t Vs2[2][FA_KB * D::ROW];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const int64_t zh = blockIdx.y, b = zh / a.H, h = zh % a.H;
-  const int64_t r = (int64_t)blockIdx.x * FA_KB + wave * 16 + (lane & 15);  // this lane's query column
-  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
-  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
-  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
-  const FaMask mk(a, b);
-  const FaRow fr{&a};
-
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi) {
-    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ks2[bi]);
-    zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Vs2[bi]);
-  }
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);
-  TileStager<HD, D::ROW, FA_KB, NT> stk, stv;
-  stk.load(K, a.ldk, 0, a.nk);
-  stv.load(V, a.ldv, 0, a.nk);
-  bf16x8 qf[D::NKS], df[D::NKS];
-  const bool live = r < a.nq;
-  const bf16_t* dOr = nullptr;
-  const bf16_t* Or = nullptr;
-  if (live) {
-    const int gi = fr.grp(r);
-    dOr = (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi);
-    Or = (const bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
-  }
-  float del = 0.f;
-#pragma unroll
-  for (int ks = 0; ks < D::NKS; ++ks) {
-    const int c = ks * 32 + 8 * g;
-    const bool ok = live && c < HD;
-    qf[ks] = ok ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
-    df[ks] = ok ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
-    if (ok) {
-      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(Or + c);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) del += (float)df[ks][e] * (float)ov[e];
-    }
-  }
-  del += __shfl_xor(del, 16, 64);
-  del += __shfl_xor(del, 32, 64);
-  if (live && g == 0) a.delta[zh * a.nq + r] = del;
-  const float lse = live ? a.lse[zh * a.nq + r] : 0.f;
-  const int tq = mk.token((int)r);
-  f32x4 dq[D::NDB];
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  __syncthreads();  // pad columns zeroed
-  stk.store(Ks2[0]);
-  stv.store(Vs2[0]);
-  __syncthreads();
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bf16_t* Ks = Ks2[kb & 1];
-    const bf16_t* Vs = Vs2[kb & 1];
-    const bool more = kb + 1 < nkb;
-    if (more) {
-      stk.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
-      stv.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
-    }
-    f32x4 ds[4];  // dS^T[key 16i + 4g + e][q]
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-      bf16x8 kfr[D::NKS], vfr[D::NKS];  // all LDS reads of the key block issued ahead of its MFMAs
-#pragma unroll
-      for (int ks = 0; ks < D::NKS; ++ks) {
-        kfr[ks] = frag_row<D::ROW>(Ks, i * 16, ks * 32, lane);
-        vfr[ks] = frag_row<D::ROW>(Vs, i * 16, ks * 32, lane);
-      }
-#pragma unroll
-      for (int ks = 0; ks < D::NKS; ++ks) {
-        sv = mfma(kfr[ks], qf[ks], sv);
-        dp = mfma(vfr[ks], df[ks], dp);
-      }
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = kb * FA_KB + i * 16 + 4 * g + e;
-        float dse = 0.f;
-        if (live) {
-          const FaLogit lg = fa_logit_d(mk, sv[e], tq, j);
-          const float pe = lg.x == -INFINITY ? 0.f : __expf(lg.x - lse);
-          dse = pe * (dp[e] - del) * lg.dxds;
-        }
-        ds[i][e] = dse;
-      }
-    }
-    // dQ^T[d][q] += K^T[d][key] dS^T[key][q]
-#pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2) {
-      const bf16x8 sb = pack8(ds[2 * k2], ds[2 * k2 + 1]);
-      bf16x8 kt[D::NDB];
-#pragma unroll
-      for (int db = 0; db < D::NDB; ++db) kt[db] = frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane);
-#pragma unroll
-      for (int db = 0; db < D::NDB; ++db) dq[db] = mfma(kt[db], sb, dq[db]);
-    }
-    if (more) {
-      stk.store(Ks2[(kb + 1) & 1]);
-      stv.store(Vs2[(kb + 1) & 1]);
-    }
-    __syncthreads();
-  }
-  if (!live) return;
-  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) {
-    const int d = db * 16 + 4 * g;
-    if (d < HD) *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
-  }
-}
-
-// dQ (+ delta), fast path: 4 waves x 32 query rows (two 16-row blocks per K / V fragment read, half
-// the LDS reads per score of flash_bwd_q_kernel), 32-key blocks double-buffered in LDS (70 KiB), the
+// dQ (+ delta): 4 waves x 32 query rows (two 16-row blocks per K / V fragment read), 32-key blocks double-buffered in LDS (70 KiB), the
 // query blocks of one unit on one XCD (its K / V served from that L2).  1-D grid.
 constexpr int JQ_NW = 4, JQ_KB = 32;
 template <int HD, bool CAP>
@@ -1013,293 +881,8 @@ __global__ void __launch_bounds__(JQ_NW * 64, 1) flash_bwd_q2_kernel(pz_flash_ar
   }
 }
 
-// ---- joint forward with the softmax probabilities exported (training default) ----------------
-// One pass over K (S^T for all keys of the row block held in registers: nk <= 320), the EXACT row
-// softmax (no online rescaling: every key of a row is in the wave's registers), P and tanh(cap)
-// stored as the bf16 [row][ldp] tensors the GEMM-path backward reads (pz_attn_softmax's contract:
-// pizero.py:271-306 mask, fully masked rows uniform over the N keys with tcap 0, zeros past N), then
-// one pass over V for O = P V with the bf16 P as the MFMA operand (what the GEMM path's P V GEMM
-// reads).  No fp32 S, no separate softmax launch.  HD 256 (joint), 8 waves x 16 query rows.
+// ---- joint attention with the softmax probabilities exported (training default): see flash_fwd_probs_dma_kernel
 constexpr int JP_NW = 8, JP_MAXKB = 5;
-template <int HD>
-__global__ void __launch_bounds__(JP_NW * 64) flash_fwd_probs_kernel(pz_flash_args a, bf16_t* P, bf16_t* TC,
-                                                                      int64_t ldp) {
-  using D = FaDims<HD>;
-  constexpr int NT = JP_NW * 64, RPW = JP_NW * 16;
-  __shared__ __attribute__((aligned(16))) bf16_t Ts2[2][FA_KB * D::ROW];  // K blocks, then V blocks
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  int64_t zh;
-  int qblk;
-  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
-  const int64_t b = zh / a.H, h = zh % a.H;
-  const int64_t r = (int64_t)qblk * RPW + wave * 16 + (lane & 15);  // this lane's query row
-  const bool live = r < a.nq;
-  const bf16_t* Q = (const bf16_t*)a.q + b * a.q_bstride + h * a.q_hstride;
-  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
-  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
-  const FaMask mk(a, b);
-  const FaFast ff(a);
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ts2[bi]);
-  TileStager<HD, D::ROW, FA_KB, NT> st;
-  st.load(K, a.ldk, 0, a.nk);
-  bf16x8 qf[D::NKS];
-#pragma unroll
-  for (int ks = 0; ks < D::NKS; ++ks) {
-    const int c = ks * 32 + 8 * g;
-    qf[ks] = (live && c < HD) ? *reinterpret_cast<const bf16x8*>(Q + r * a.ldq + c) : bf16x8{};
-  }
-  const int t = mk.token((int)r);
-  const bool dead = mk.dead(t);
-  const int rb = fa_row_bits(mk, t), full_keys = fa_full_keys(mk);
-  __syncthreads();  // pad columns zeroed
-  st.store(Ts2[0]);
-  __syncthreads();
-  // pass 1: S^T[key][q] for every key of the row block (stage kb = K block kb)
-  f32x4 sc[JP_MAXKB][4];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) sc[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kb < nkb) {
-      const bf16_t* Ks = Ts2[kb & 1];
-      if (kb + 1 < nkb) st.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
-      else st.load(V, a.ldv, 0, a.nk);  // stage nkb: V block 0
-#pragma unroll
-      for (int ks = 0; ks < D::NKS; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) sc[kb][i] = mfma(frag_row<D::ROW>(Ks, i * 16, ks * 32, lane), qf[ks], sc[kb][i]);
-      st.store(Ts2[(kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  // logits (log2 domain) + the tanh(cap) export; keys past nk / masked -> -inf
-  bf16_t* prow = P + (b * a.nq + r) * ldp;
-  bf16_t* trow = TC ? TC + (b * a.nq + r) * ldp : nullptr;
-  float mx = -INFINITY;
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float tv[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = kb * FA_KB + i * 16 + 4 * g + e;
-        const float sv = sc[kb][i][e];
-        float th = 0.f, x2;
-        if (a.cap > 0.f) {
-          th = fmaf(-2.f, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(sv * ff.k2) + 1.f), 1.f);
-          x2 = th * ff.crow_live;
-        } else {
-          x2 = sv * ff.crow_live;
-        }
-        const bool ok = j < (int)a.nk && (j < full_keys || ((rb >> fa_key_class(mk, j)) & 1));
-        x2 = ok ? x2 : -INFINITY;
-        sc[kb][i][e] = x2;
-        mx = fmaxf(mx, x2);
-        tv[e] = (dead || j >= (int)a.nk) ? 0.f : th;
-      }
-      const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      if (trow && live && kb < nkb && j0 < ldp)
-        *reinterpret_cast<u32x2*>(trow + j0) = u32x2{pack2bf(tv[0], tv[1]), pack2bf(tv[2], tv[3])};
-    }
-  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  float sum = 0.f;
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float pv = __builtin_amdgcn_exp2f(sc[kb][i][e] - mx);  // exp2(-inf) = 0
-        sc[kb][i][e] = pv;
-        sum += pv;
-      }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
-  // fully masked (dead) rows: uniform over the N keys (the finfo.min mask absorbs the logits)
-  const float inv = 1.f / sum, uni = 1.f / (float)a.nk;
-  bf16x8 pf[JP_MAXKB][2];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = kb * FA_KB + i * 16 + 4 * g + e;
-        sc[kb][i][e] = dead ? (j < (int)a.nk ? uni : 0.f) : sc[kb][i][e] * inv;
-      }
-      const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      if (live && kb < nkb && j0 < ldp)
-        *reinterpret_cast<u32x2*>(prow + j0) =
-            u32x2{pack2bf(sc[kb][i][0], sc[kb][i][1]), pack2bf(sc[kb][i][2], sc[kb][i][3])};
-    }
-    pf[kb][0] = pack8(sc[kb][0], sc[kb][1]);
-    pf[kb][1] = pack8(sc[kb][2], sc[kb][3]);
-  }
-  // pass 2: O^T[d][q] = V^T[d][key] P^T[key][q] with the bf16 P (stage nkb + kb = V block kb)
-  f32x4 o[D::NDB];
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) o[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    if (kb < nkb) {
-      const bf16_t* Vs = Ts2[(nkb + kb) & 1];
-      const bool more = kb + 1 < nkb;
-      if (more) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-        for (int db = 0; db < D::NDB; ++db) o[db] = mfma(frag_tr<D::ROW>(Vs, k2 * 32, db * 16, lane), pf[kb][k2], o[db]);
-      if (more) st.store(Ts2[(nkb + kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  if (!live) return;
-  const FaRow fr{&a};
-  const int gi = fr.grp(r);
-  bf16_t* O = (bf16_t*)a.g_o[gi] + fr.off(b, h, r, gi);
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) {
-    const int d = db * 16 + 4 * g;
-    if (d < HD) *reinterpret_cast<u32x2*>(O + d) = u32x2{pack2bf(o[db][0], o[db][1]), pack2bf(o[db][2], o[db][3])};
-  }
-}
-
-// ---- joint backward: dS from the exported softmax (training default) --------------------------
-// dP^T = V dO^T for every key of a 16-row block in registers (V staged through LDS, dO rows straight
-// into MFMA B fragments), delta = sum_j P dP over the whole row, dS = P (dP - delta) scale (1 - tc^2)
-// written in bf16 -- pz_attn_softmax_bwd's result without the fp32 dP tensor (one launch instead of
-// the dP GEMM + the softmax-backward pass).  Mixtures without dO (g_do NULL) contribute dP = 0.
-template <int HD>
-__global__ void __launch_bounds__(JP_NW * 64) flash_bwd_ds_kernel(pz_flash_args a, const bf16_t* P,
-                                                                   const bf16_t* TC, bf16_t* dS, int64_t ldp) {
-  using D = FaDims<HD>;
-  constexpr int NT = JP_NW * 64, RPW = JP_NW * 16;
-  __shared__ __attribute__((aligned(16))) bf16_t Ts2[2][FA_KB * D::ROW];  // V blocks, then (dQ) K blocks
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  int64_t zh;
-  int qblk;
-  fa_unit_block((int)((a.nq + RPW - 1) / RPW), (int)(a.Z * a.H), zh, qblk);
-  const int64_t b = zh / a.H, h = zh % a.H;
-  const int64_t r = (int64_t)qblk * RPW + wave * 16 + (lane & 15);
-  const bool live = r < a.nq;
-  const bool want_dq = a.dq != nullptr;
-  const bf16_t* V = (const bf16_t*)a.v + b * a.v_bstride + h * a.v_hstride;
-  const bf16_t* K = (const bf16_t*)a.k + b * a.k_bstride + h * a.k_hstride;
-  const int nkb = (int)((a.nk + FA_KB - 1) / FA_KB);  // <= JP_MAXKB (host-checked)
-#pragma unroll
-  for (int bi = 0; bi < 2; ++bi) zero_pad_cols<HD, D::HDK, D::ROW, FA_KB, NT>(Ts2[bi]);
-  TileStager<HD, D::ROW, FA_KB, NT> st;
-  st.load(V, a.ldv, 0, a.nk);
-  bf16x8 df[D::NKS];
-  {
-    const FaRow fr{&a};
-    const int gi = live ? fr.grp(r) : 0;
-    const bf16_t* dOr = live && a.g_do[gi] ? (const bf16_t*)a.g_do[gi] + fr.off(b, h, r, gi) : nullptr;
-#pragma unroll
-    for (int ks = 0; ks < D::NKS; ++ks) {
-      const int c = ks * 32 + 8 * g;
-      df[ks] = (dOr && c < HD) ? *reinterpret_cast<const bf16x8*>(dOr + c) : bf16x8{};
-    }
-  }
-  __syncthreads();
-  st.store(Ts2[0]);
-  __syncthreads();
-  // pass 1 (stage kb = V block kb): dP^T[key][q] = V dO^T
-  f32x4 dp[JP_MAXKB][4];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dp[kb][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (kb < nkb) {
-      const bf16_t* Vs = Ts2[kb & 1];
-      const bool more = kb + 1 < nkb || want_dq;
-      if (kb + 1 < nkb) st.load(V, a.ldv, (int64_t)(kb + 1) * FA_KB, a.nk);
-      else if (want_dq) st.load(K, a.ldk, 0, a.nk);  // stage nkb: K block 0
-#pragma unroll
-      for (int ks = 0; ks < D::NKS; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dp[kb][i] = mfma(frag_row<D::ROW>(Vs, i * 16, ks * 32, lane), df[ks], dp[kb][i]);
-      if (more) st.store(Ts2[(kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  // dS = P (dP - delta) scale (1 - tc^2) for the row (kept in dp as fp32; stored in bf16)
-  const bf16_t* prow = P + (b * a.nq + r) * ldp;
-  const bf16_t* trow = TC + (b * a.nq + r) * ldp;
-  bf16_t* orow = dS + (b * a.nq + r) * ldp;
-  const int N = (int)a.nk;
-  u32x2 pw[JP_MAXKB][4];
-  float dot = 0.f;
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      pw[kb][i] = live && j0 < N ? *reinterpret_cast<const u32x2*>(prow + j0) : u32x2{0u, 0u};  // P = 0 past N
-      const float p0 = __uint_as_float(pw[kb][i][0] << 16), p1 = __uint_as_float(pw[kb][i][0] & 0xffff0000u);
-      const float p2 = __uint_as_float(pw[kb][i][1] << 16), p3 = __uint_as_float(pw[kb][i][1] & 0xffff0000u);
-      dot += p0 * dp[kb][i][0] + p1 * dp[kb][i][1] + p2 * dp[kb][i][2] + p3 * dp[kb][i][3];
-    }
-  dot += __shfl_xor(dot, 16, 64);
-  dot += __shfl_xor(dot, 32, 64);
-  const bool cap = a.cap > 0.f;
-  bf16x8 dsf[JP_MAXKB][2];
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j0 = kb * FA_KB + i * 16 + 4 * g;
-      u32x2 tw = {0u, 0u};
-      if (live && cap && j0 < N) tw = *reinterpret_cast<const u32x2*>(trow + j0);
-      const float pv[4] = {__uint_as_float(pw[kb][i][0] << 16), __uint_as_float(pw[kb][i][0] & 0xffff0000u),
-                           __uint_as_float(pw[kb][i][1] << 16), __uint_as_float(pw[kb][i][1] & 0xffff0000u)};
-      const float tv[4] = {__uint_as_float(tw[0] << 16), __uint_as_float(tw[0] & 0xffff0000u),
-                           __uint_as_float(tw[1] << 16), __uint_as_float(tw[1] & 0xffff0000u)};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = j0 + e < N ? pv[e] * (dp[kb][i][e] - dot) * a.scale : 0.f;
-        if (cap) x *= 1.f - tv[e] * tv[e];
-        dp[kb][i][e] = x;
-      }
-      if (live && kb < nkb && j0 < ldp)
-        *reinterpret_cast<u32x2*>(orow + j0) =
-            u32x2{pack2bf(dp[kb][i][0], dp[kb][i][1]), pack2bf(dp[kb][i][2], dp[kb][i][3])};
-    }
-    dsf[kb][0] = pack8(dp[kb][0], dp[kb][1]);
-    dsf[kb][1] = pack8(dp[kb][2], dp[kb][3]);
-  }
-  if (!want_dq) return;  // uniform: every thread takes the same branch
-  // pass 2 (stage nkb + kb = K block kb): dQ^T[d][q] = K^T[d][key] dS^T[key][q] with the bf16 dS (what the
-  // GEMM path's dS K product reads)
-  f32x4 dq[D::NDB];
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) dq[db] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kb = 0; kb < JP_MAXKB; ++kb) {
-    if (kb < nkb) {
-      const bf16_t* Ks = Ts2[(nkb + kb) & 1];
-      const bool more = kb + 1 < nkb;
-      if (more) st.load(K, a.ldk, (int64_t)(kb + 1) * FA_KB, a.nk);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-        for (int db = 0; db < D::NDB; ++db) dq[db] = mfma(frag_tr<D::ROW>(Ks, k2 * 32, db * 16, lane), dsf[kb][k2], dq[db]);
-      if (more) st.store(Ts2[(nkb + kb + 1) & 1]);
-      __syncthreads();
-    }
-  }
-  if (!live) return;
-  bf16_t* dQ = (bf16_t*)a.dq + b * a.q_bstride + h * a.q_hstride + r * a.ldq;
-#pragma unroll
-  for (int db = 0; db < D::NDB; ++db) {
-    const int d = db * 16 + 4 * g;
-    if (d < HD) *reinterpret_cast<u32x2*>(dQ + d) = u32x2{pack2bf(dq[db][0], dq[db][1]), pack2bf(dq[db][2], dq[db][3])};
-  }
-}
 
 // ---- resident variants (SigLIP: nq, nk <= 256) ---------------------------------
 // The whole key side (forward, dQ) or query side (dK/dV) of a unit is staged in LDS once, by
@@ -2429,35 +2012,6 @@ __device__ __forceinline__ void fs_load_rows(bf16x8 (&f)[3], const bf16_t* row, 
   }
 }
 
-#ifdef PZ_FLASH_AB
-// (A/B builds only, -DPZ_FLASH_AB: the default dQ kernel computes delta itself)
-// delta[zh][r] = sum_d dO[r][d] O[r][d] for the SigLIP shape (head 72, one output group): one thread per (token,
-// head), the 16 heads of a token row on 16 adjacent lanes (their 144-B segments tile the row), 9 + 9 16-B loads
-__global__ void __launch_bounds__(256) flash_delta72_kernel(pz_flash_args a) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= a.Z * a.nq * a.H) return;
-  const int64_t h = t % a.H, br = t / a.H, r = br % a.nq, b = br / a.nq;
-  const int64_t off = b * a.g_bstride[0] + r * a.g_ld[0] + h * a.o_hstride;
-  const u32x4* O = reinterpret_cast<const u32x4*>((const bf16_t*)a.g_o[0] + off);
-  const u32x4* dO = reinterpret_cast<const u32x4*>((const bf16_t*)a.g_do[0] + off);
-  u32x4 x[9], y[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    x[i] = O[i];
-    y[i] = dO[i];
-  }
-  float acc = 0.f;
-#pragma unroll
-  for (int i = 0; i < 9; ++i)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      acc = fmaf(__uint_as_float(x[i][e] << 16), __uint_as_float(y[i][e] << 16), acc);
-      acc = fmaf(__uint_as_float(x[i][e] & 0xffff0000u), __uint_as_float(y[i][e] & 0xffff0000u), acc);
-    }
-  a.delta[(b * a.H + h) * a.nq + r] = acc;
-}
-#endif  // PZ_FLASH_AB
-
 // dQ with K / V resident (delta = rowsum(dO O) from flash_bwd_prep_kernel): wave w owns query rows 32w ..
 // 32w + 31; the next unit's Q / dO rows, lse and delta (inline-asm loads) and K / V images (LDS-DMA) are issued
 // before this unit's compute
@@ -3442,12 +2996,8 @@ struct FaT2 {
   template <int HD> static constexpr auto flash_bwd_q2_kernel_t = flash_bwd_q2_kernel<HD, (bool)X>;
   template <int HD> static constexpr auto flash_bwd_kv_kernel_t = flash_bwd_kv_kernel<HD, (int)X>;
 };
-// joint backward element-wise path: 0 generic, 1 fast, 2 fast + soft-cap ("0" in PZ_FLASH_FAST: generic)
-static int fa_fast_bwd(const pz_flash_args* a) {
-  const char* e = getenv("PZ_FLASH_FAST");
-  if (e && e[0] == '0') return 0;
-  return a->cap > 0.f ? 2 : 1;
-}
+// joint backward element-wise path: 1 fast, 2 fast + soft-cap
+static int fa_fast_bwd(const pz_flash_args* a) { return a->cap > 0.f ? 2 : 1; }
 static bool fa_hd_ok(int64_t hd) { return hd == 256 || hd == 72 || hd == 32 || hd == 16; }
 
 // SigLIP shape: the whole key / query side of a unit fits the resident kernels' LDS images
@@ -3545,15 +3095,7 @@ extern "C" int pz_flash_fwd(const pz_flash_args* a, void* stream) {
     const dim3 gu((unsigned)(a->Z * a->H));
     if (fa_sig(a)) {
       const int G = fa_sig_grid(a);
-#ifdef PZ_FLASH_AB
-      const char* eq = getenv("PZ_SIG_QB");  // "2": 8 waves of 32 rows (A/B builds); default 16 waves of 16 rows
-      if (eq && eq[0] == '2') {
-        fa_smem_attr(flash_fwd_sig_kernel<2>, FS_SMEM, attr3);
-        hipLaunchKernelGGL(flash_fwd_sig_kernel<2>, dim3((unsigned)G), dim3(8 * 64), FS_SMEM, st, *a, G);
-      } else
-#else
       (void)attr3;
-#endif
       {
         static bool attr4 = false;
         fa_smem_attr(flash_fwd_sig_kernel<1>, FS_SMEM, attr4);
@@ -3605,15 +3147,6 @@ extern "C" int pz_flash_fwd_probs(const pz_flash_args* a, void* P, void* tcap, i
                "flash_fwd_probs: operands need 16-byte aligned rows");
   PZ_CHECK_ARG(a->nq + a->mask_row0 < (1 << 22) && a->Z * a->H < 65536, "flash_fwd_probs: nq / units too large");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
-#ifdef PZ_FLASH_AB
-  const char* e = getenv("PZ_PROBS_DMA");  // "0": the round-4 register-staged kernel (A/B builds)
-  if (e && e[0] == '0') {
-    hipLaunchKernelGGL(flash_fwd_probs_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
-                       (hipStream_t)stream, *a, (bf16_t*)P, (bf16_t*)tcap, ldp);
-    PZ_CHECK_LAUNCH();
-    return PZ_OK;
-  }
-#endif
   {
     static bool attr0 = false, attr1 = false;
     if (a->cap > 0.f) {
@@ -3648,15 +3181,6 @@ extern "C" int pz_flash_bwd_ds(const pz_flash_args* a, const void* P, const void
                  "flash_bwd_ds: dQ needs K (16-byte rows) and an 8-byte aligned dQ");
   PZ_CHECK_ARG(a->Z * a->H < 65536, "flash_bwd_ds: too many units");
   const int64_t units = a->Z * a->H, nqb = (a->nq + JP_NW * 16 - 1) / (JP_NW * 16);
-#ifdef PZ_FLASH_AB
-  const char* e = getenv("PZ_PROBS_DMA");  // "0": the round-4 register-staged kernel (A/B builds)
-  if (e && e[0] == '0') {
-    hipLaunchKernelGGL(flash_bwd_ds_kernel<256>, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), 0,
-                       (hipStream_t)stream, *a, (const bf16_t*)P, (const bf16_t*)tcap, (bf16_t*)dS, ldp);
-    PZ_CHECK_LAUNCH();
-    return PZ_OK;
-  }
-#endif
   static bool attr = false;
   fa_smem_attr(flash_bwd_ds_dma_kernel, JD_SMEM, attr);
   hipLaunchKernelGGL(flash_bwd_ds_dma_kernel, dim3((unsigned)(nqb * units)), dim3(JP_NW * 64), JD_SMEM,
@@ -3691,7 +3215,6 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     splits = splits < 8 ? splits : 8;
     while (splits > 1 && splits * 2 * a->Z * a->H * a->nk * a->head_dim * 4 > a->ws_bytes) --splits;
   }
-  dim3 gq((unsigned)((a->nq + FA_KB - 1) / FA_KB), (unsigned)(a->Z * a->H));
   // dQ pass first: it also writes delta, which the dK/dV pass reads
   if (fa_resident(a) && fa_unit(a)) {
     static bool aq = false, akv = false, aq2 = false, akv2 = false, aq3 = false, akv3 = false;
@@ -3699,18 +3222,7 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     if (fa_sig(a)) {  // delta pass, then the persistent dQ and dK / dV kernels
       const int G = fa_sig_grid(a);
       fa_smem_attr(flash_bwd_kv_sig_kernel, FS_SMEM, akv3);
-#ifdef PZ_FLASH_AB
-      const char* ed = getenv("PZ_SIG_DELTA");  // "pass": the separate delta pass (A/B builds)
-      if (ed && ed[0] == 'p') {
-        const int64_t rows = a->Z * a->H * a->nq;
-        hipLaunchKernelGGL(flash_delta72_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, *a);
-        PZ_CHECK_LAUNCH();
-        fa_smem_attr(flash_bwd_q_sig_kernel<false>, FS_SMEM, aq3);
-        hipLaunchKernelGGL(flash_bwd_q_sig_kernel<false>, dim3((unsigned)G), dim3(FS_NW * 64), FS_SMEM, st, *a, G);
-      } else
-#else
       (void)aq3;
-#endif
       {
         static bool aq4 = false;
         fa_smem_attr(flash_bwd_q_sig_kernel<true>, FS_SMEM, aq4);
@@ -3747,7 +3259,7 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     return PZ_OK;
   }
   const int fm = fa_fast_bwd(a);
-  if (fm) {
+  {
     const int64_t units = a->Z * a->H, nqb = (a->nq + JQ_NW * 32 - 1) / (JQ_NW * 32);
     const dim3 gq2((unsigned)(nqb * units));
     if (fm == 2) {
@@ -3755,17 +3267,13 @@ extern "C" int pz_flash_bwd(const pz_flash_args* a, void* stream) {
     } else {
       FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_q2_kernel, false), gq2, dim3(JQ_NW * 64), 0, st, *a);
     }
-  } else {
-    FA_DISPATCH(a->head_dim, flash_bwd_q_kernel, gq, dim3(FA_NW * 64), 0, st, *a);
   }
   PZ_CHECK_LAUNCH();
   const dim3 gkv1((unsigned)(nkb * a->Z * a->H * splits));
   if (fm == 2) {
     FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 2), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
-  } else if (fm == 1) {
-    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 1), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
   } else {
-    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 0), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
+    FA_DISPATCH(a->head_dim, FA_T2(flash_bwd_kv_kernel, 1), gkv1, dim3(FA_NW * 64), 0, st, *a, (int)splits);
   }
   if (splits > 1) {
     PZ_CHECK_LAUNCH();

@@ -119,8 +119,7 @@ def test_flash_fwd_joint_block_mask(cnt, key_split):
 def test_flash_fwd_probs_joint_block_mask(cnt):
     """pz_flash_fwd_probs (training-default joint forward): O, and the exported bf16 softmax P and
     tanh(cap) with pz_attn_softmax's conventions (dead rows uniform over L keys with tcap 0, zeros in
-    the L..Lp pad columns), against torch fp32 (the LDS-DMA ring kernel; the round-4 register-staged one is built
-    only with -DPZ_FLASH_AB)"""
+    the L..Lp pad columns), against torch fp32 (the LDS-DMA ring kernel)"""
     from pizero_native import ops
 
     B, P, C, Hc, nh, hd = len(cnt), 276, 1, 4, 8, 256

@@ -5,8 +5,10 @@ joint: B samples x (281 tokens x 8 heads) queries, 281 keys, head 256, soft-cap 
 siglip: B x 16 heads x 256 x 256, head 72.  Prints fwd / bwd ms and TF/s (algorithmic
 FLOP: fwd 4*nq*nk*hd per unit, bwd 2.5x fwd).
 
-The non-default variants (PZ_PROBS_DMA=0, PZ_SIG_DELTA=pass, PZ_SIG_QB=2) exist only in a -DPZ_FLASH_AB build of the
-library; in the product build those settings run the default kernels (use --default-only there).
+Non-default variants timed beside the defaults: the all-fused joint kernels (pz_flash_fwd / pz_flash_bwd, the
+PZ_JOINT_ATTN=flash path) and the one-workgroup-per-unit / resident SigLIP kernels (PZ_FLASH_SIG=0, PZ_FLASH_UNIT=0).
+(The round-4 register-staged joint kernels, the separate SigLIP delta pass and the 8 x 32-row SigLIP forward were
+measured slower and removed in round 6: profiles/r05/flash_bench_r5l.log.)
 """
 import argparse
 import math
@@ -62,24 +64,18 @@ def main():
     Pm = torch.empty(B, L * nh, Lp, device=dev, dtype=torch.bfloat16)
     tcm = torch.empty_like(Pm)
     dSm = torch.empty_like(Pm)
-    jt = {dma: ([], []) for dma in (("1",) if a.default_only else ("1", "0"))}  # PZ_PROBS_DMA: LDS-DMA ring / registers
+    tps, tds = [], []
     for _ in range(1 if a.default_only else a.rounds):
-        for dma in jt:
-            os.environ["PZ_PROBS_DMA"] = dma
-            jt[dma][0].append(timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters))
-            jt[dma][1].append(timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters))
-    os.environ.pop("PZ_PROBS_DMA")
-    for dma, (tps, tds) in jt.items():
-        tp, td = sorted(tps)[len(tps) // 2], sorted(tds)[len(tds) // 2]
-        print(f"joint(dma={dma})  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)   "
-              f"bwd dS {td:.3f} ms (+ dQ)  (median of {len(tps)} rounds)", flush=True)
-    for fast in () if a.default_only else ("1", "0"):  # PZ_FLASH_FAST: fast element-wise joint backward vs the generic kernels
-        os.environ["PZ_FLASH_FAST"] = fast
+        tps.append(timeit(lambda: ops.flash_fwd_probs(fa, Pm, tcm, Lp), a.iters))
+        tds.append(timeit(lambda: ops.flash_bwd_ds(fa, Pm, tcm, dSm, Lp), a.iters))
+    tp, td = sorted(tps)[len(tps) // 2], sorted(tds)[len(tds) // 2]
+    print(f"joint(dma=1)  fwd+probs {tp:.3f} ms {fl / tp / 1e9:.0f} TF/s (O + bf16 P / tanh(cap) export)   "
+          f"bwd dS {td:.3f} ms (+ dQ)  (median of {len(tps)} rounds)", flush=True)
+    if not a.default_only:  # the all-fused joint kernels (PZ_JOINT_ATTN=flash)
         tf = timeit(lambda: ops.flash_fwd(fa), a.iters)
         tb = timeit(lambda: ops.flash_bwd(fa), a.iters)
-        print(f"joint(fast={fast})  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
+        print(f"joint(fused)  fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
               f"{2.5 * fl / tb / 1e9:.0f} TF/s", flush=True)
-    os.environ.pop("PZ_FLASH_FAST", None)
     nh, hd, N = 16, 72, 256
     qkv = torch.randn(B * N, 3 * nh * hd, device=dev).to(torch.bfloat16)
     O = torch.empty(B * N, nh * hd, device=dev, dtype=torch.bfloat16)
@@ -90,25 +86,21 @@ def main():
     sa = ops.siglip_flash_args(qkv, O, lse, B, nh, hd, N, dO=dO, delta=delta, dqkv=dqkv)
     fl = 4.0 * B * nh * N * N * hd
     # PZ_FLASH_SIG / PZ_FLASH_UNIT: the persistent pipelined kernels (default), one workgroup per (image, head)
-    # unit, the 2-/4-workgroup resident kernels; "1p": the persistent kernels with the separate delta pass
-    # (PZ_SIG_DELTA=pass); "1q": the forward with 8 waves of 32 rows (PZ_SIG_QB=2).  The variants are timed in
-    # interleaved rounds (clock drift between back-to-back runs of the same kernel reaches ~10 %) and the median
-    # of the rounds is printed.
-    variants = [("1", "1")] if a.default_only else [("1", "1"), ("1q", "1"), ("1p", "1"), ("0", "1"), ("0", "0")]
+    # unit, the 2-/4-workgroup resident kernels.  The variants are timed in interleaved rounds (clock drift between
+    # back-to-back runs of the same kernel reaches ~10 %) and the median of the rounds is printed.
+    variants = [("1", "1")] if a.default_only else [("1", "1"), ("0", "1"), ("0", "0")]
     times = {v: ([], []) for v in variants}
     for _ in range(1 if a.default_only else a.rounds):
         for v in variants:
             sig, unit = v
-            os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig[0]
-            os.environ["PZ_SIG_DELTA"] = "pass" if sig == "1p" else "fused"
-            os.environ["PZ_SIG_QB"] = "2" if sig == "1q" else "1"
+            os.environ["PZ_FLASH_UNIT"], os.environ["PZ_FLASH_SIG"] = unit, sig
             times[v][0].append(timeit(lambda: ops.flash_fwd(sa), a.iters))
             times[v][1].append(timeit(lambda: ops.flash_bwd(sa), a.iters))
     for (sig, unit), (tfs, tbs) in times.items():
         tf, tb = sorted(tfs)[len(tfs) // 2], sorted(tbs)[len(tbs) // 2]
         print(f"siglip(sig={sig},unit={unit}) fwd {tf:.3f} ms {fl / tf / 1e9:.0f} TF/s   bwd {tb:.3f} ms "
               f"{2.5 * fl / tb / 1e9:.0f} TF/s  (median of {len(tfs)} rounds)", flush=True)
-    for k in ("PZ_FLASH_UNIT", "PZ_FLASH_SIG", "PZ_SIG_DELTA", "PZ_SIG_QB"):
+    for k in ("PZ_FLASH_UNIT", "PZ_FLASH_SIG"):
         os.environ.pop(k)
 
 if __name__ == "__main__":

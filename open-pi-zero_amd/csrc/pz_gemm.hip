@@ -2057,6 +2057,8 @@ Plan make_plan(const pz_gemm_args* a) {
         int64_t S = (256 + nblk - 1) / nblk;
         S = S < kch / 8 ? S : kch / 8;
         S = S < 8 ? S : 8;
+        const char* esn = getenv("PZ_SK64_S");  // A/B override of the slice count (read per call)
+        if (esn && atoi(esn) >= 2 && atoi(esn) <= 8 && atoi(esn) <= kch / 4) S = atoi(esn);
         const int64_t ldw = (a->N + 3) / 4 * 4;
         if (S >= 2 && S * a->M * ldw * 4 <= a->ws_bytes && PZ_ALIGNED(a->workspace, 16)) {
           const int64_t per = (kch + S - 1) / S;

@@ -73,12 +73,23 @@ __device__ __forceinline__ float gelu_tanh(float x) {
   const float e = __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x * x, c0));  // e^{-2u}
   return x * fast_rcp(1.f + e);
 }
+// d/dx gelu_tanh = 0.5 (1 + t) + 0.5 x (1 - t^2) u', t = tanh(u), u' = k0 (1 + 3 k1 x^2).  With s = sigmoid(2u) =
+// 0.5 (1 + t) (gelu_tanh's rcp(1 + e^{-2u})) and 1 - t^2 = 4 s (1 - s): grad = s + 2 x s (1 - s) u' -- the same
+// exp / rcp as the forward value, so the DGEGLU epilogues get gelu and its derivative from ONE v_exp_f32 and ONE
+// v_rcp_f32 (gelu_tanh_both): 12 VALU + 2 transcendental ops per element instead of 23 + 4 (the round-5 tanh form).
+// s -> 1 for large x (grad -> 1), e -> inf, s -> 0 for very negative x (grad -> 0): no NaN.
+__device__ __forceinline__ void gelu_tanh_both(float x, float& gl, float& gr) {
+  constexpr float c0 = -2.f * 0.7978845608028654f * 1.4426950408889634f, c1 = c0 * 0.044715f;
+  constexpr float k0 = 0.7978845608028654f, k3 = 3.f * 0.044715f * 0.7978845608028654f;
+  const float x2 = x * x;
+  const float s = fast_rcp(1.f + __builtin_amdgcn_exp2f(x * __builtin_fmaf(c1, x2, c0)));  // sigmoid(2u)
+  gl = x * s;  // == gelu_tanh(x), bit for bit
+  gr = __builtin_fmaf(2.f * x * s * (1.f - s), __builtin_fmaf(k3, x2, k0), s);
+}
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanh_fast(u);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  float gl, gr;
+  gelu_tanh_both(x, gl, gr);
+  return gr;
 }
 
 __device__ __forceinline__ float silu(float x) { return x * fast_rcp(1.f + fast_exp(-x)); }

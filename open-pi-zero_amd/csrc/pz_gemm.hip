@@ -693,8 +693,10 @@ __device__ __forceinline__ void epi8p_fast(const GemmP& p, int64_t cofs, int64_t
           float dg[4], du[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            dg[r] = v[r] * x1[r] * gelu_tanh_grad(x0[r]);
-            du[r] = v[r] * gelu_tanh(x0[r]);
+            float gl_, gr_;
+            gelu_tanh_both(x0[r], gl_, gr_);
+            dg[r] = v[r] * x1[r] * gr_;
+            du[r] = v[r] * gl_;
           }
           *reinterpret_cast<u32x2*>(Cp) = pk4(dg);
           *reinterpret_cast<u32x2*>(Cp + p.geglu_I) = pk4(du);
@@ -834,8 +836,10 @@ __device__ __forceinline__ void epi8p_staged(const GemmP& p, int64_t cofs, int64
         float dg[8], du[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          dg[e] = v[e] * x1[e] * gelu_tanh_grad(x0[e]);
-          du[e] = v[e] * gelu_tanh(x0[e]);
+          float gl_, gr_;
+          gelu_tanh_both(x0[e], gl_, gr_);
+          dg[e] = v[e] * x1[e] * gr_;
+          du[e] = v[e] * gl_;
         }
         st16(Cp, pack8v(dg), p.nt_store);
         st16(Cp + p.geglu_I, pack8v(du), p.nt_store);

@@ -160,8 +160,10 @@ __device__ __forceinline__ void epi_store4(const GemmP& p, int64_t cofs, int64_t
     float dg[4], du[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      dg[r] = v[r] * x1[r] * gelu_tanh_grad(x0[r]);
-      du[r] = v[r] * gelu_tanh(x0[r]);
+      float gl_, gr_;
+      gelu_tanh_both(x0[r], gl_, gr_);
+      dg[r] = v[r] * x1[r] * gr_;
+      du[r] = v[r] * gl_;
     }
     store4(Cb, full, n, p.N, dg);
     store4(Cb + p.geglu_I, full, n, p.N, du);
@@ -245,8 +247,10 @@ __device__ __forceinline__ void store_out4_rt(const GemmP& p, int64_t cofs, int6
     unpack4(ld4bf(X + p.geglu_I, full, n, p.N), u);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      dg[r] = v[r] * u[r] * gelu_tanh_grad(g[r]);
-      du[r] = v[r] * gelu_tanh(g[r]);
+      float gl_, gr_;
+      gelu_tanh_both(g[r], gl_, gr_);
+      dg[r] = v[r] * u[r] * gr_;
+      du[r] = v[r] * gl_;
     }
     bf16_t* Cp = reinterpret_cast<bf16_t*>(p.C) + cofs + m * p.ldc + n;
     store4(Cp, full, n, p.N, dg);

@@ -198,9 +198,10 @@ __global__ void geglu_bwd_kernel(const bf16_t* __restrict__ dh, int64_t lddh, co
   const int64_t m = idx / I, n = idx % I;
   const float g = bf2f(gu[m * ldgu + n]), u = bf2f(gu[m * ldgu + I + n]);
   const float d = bf2f(dh[m * lddh + n]);
-  const float ge = gelu_tanh(g);
+  float ge, gr;
+  gelu_tanh_both(g, ge, gr);
   if (h_out) h_out[m * ldh + n] = f2bf(ge * u);
-  dgu[m * ldgu + n] = f2bf(d * u * gelu_tanh_grad(g));
+  dgu[m * ldgu + n] = f2bf(d * u * gr);
   dgu[m * ldgu + I + n] = f2bf(d * ge);
 }
 
@@ -229,8 +230,10 @@ __global__ void __launch_bounds__(256) geglu_bwd8_kernel(const bf16_t* __restric
   ld8(dh + m * lddh + n, d);
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    dg[e] = d[e] * u[e] * gelu_tanh_grad(g[e]);
-    du[e] = d[e] * gelu_tanh(g[e]);
+    float gl_, gr_;
+    gelu_tanh_both(g[e], gl_, gr_);
+    dg[e] = d[e] * u[e] * gr_;
+    du[e] = d[e] * gl_;
   }
   st8(dgu + m * ldgu + n, dg);
   st8(dgu + m * ldgu + I + n, du);
@@ -258,8 +261,7 @@ __global__ void act_bwd_kernel(const bf16_t* __restrict__ dh, int64_t lddh, cons
   const float d = bf2f(dh[m * lddh + n]);
   float h, gr;
   if (act == PZ_EPI_GELU) {
-    h = gelu_tanh(x);
-    gr = gelu_tanh_grad(x);
+    gelu_tanh_both(x, h, gr);
   } else {
     h = silu(x);
     gr = silu_grad(x);

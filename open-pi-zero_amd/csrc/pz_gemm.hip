@@ -1031,7 +1031,7 @@ __device__ __forceinline__ void gemm8p_body(const GemmP& p) {
     nk = min(nk_all - kt0, p.tail_kt);
   }
   int tm, tn;
-  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn, p.group);
   const int64_t m0 = (int64_t)tm * BT;
   const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
   const int t = threadIdx.x, lane = t & 63;
@@ -1397,7 +1397,7 @@ __global__ void __launch_bounds__(NT2, 1) gemm8k_kernel(GemmP p) {
     nk = min(nk_all - kt0, p.tail_kt);
   }
   int tm, tn;
-  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  tile_coords(lid, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn, p.group);
   const int64_t m0 = (int64_t)tm * BT;
   const int64_t n0 = GEGLU ? (int64_t)tn * (BT / 2) : (int64_t)tn * BT;
   const int t = threadIdx.x, lane = t & 63;
@@ -1535,7 +1535,7 @@ template <bool GEGLU, int PB = 8>
 __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
   const int tile = blockIdx.x >> 4, rb = (blockIdx.x >> 1) & 7, h = blockIdx.x & 1;
   int tm, tn;
-  tile_coords(p.dp_tiles + tile, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn);
+  tile_coords(p.dp_tiles + tile, p.tiles_m * p.tiles_n, p.tiles_m, p.tiles_n, tm, tn, p.group);
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6, wr = wave >> 2, wc = wave & 3;
   const f32x4* W = reinterpret_cast<const f32x4*>(p.ws) + (int64_t)tile * p.tail_s * (32 * NT2);
   // GeGLU pairs gate cb = h with up cb = h + 2; plain outputs take cb = 2h, 2h + 1
@@ -2442,6 +2442,16 @@ extern "C" int pz_gemm(const pz_gemm_args* a, void* stream) {
   hipStream_t st = (hipStream_t)stream;
 
   const Plan pl = make_plan(a);
+  {
+    // 8-phase tile order (tile_coords): super-rows of 2 row tiles instead of 8 for the narrow long-K GEMMs (<= 8
+    // column tiles, K >= 16384: the Gemma gate|up dgrad, down forward, down / gate|up wgrads) and the DGEGLU dgrad --
+    // measured per shape at micro-batch 256 (profiles/r06/gemm_group_ab.txt: gate|up dgrad 125.8 -> 121.4 ms,
+    // DGEGLU 83.7 -> 81.5, down fwd 62.2 -> 61.2, wgrad 127.9 -> 127.0); the GeGLU forward keeps 8 (139.9 vs 142.2).
+    // PZ_GEMM_GROUP overrides (A/B; read per call).
+    const char* e = getenv("PZ_GEMM_GROUP");
+    if (e && atoi(e) >= 1 && atoi(e) <= 64) p.group = atoi(e);
+    else p.group = (a->K >= 16384 && pl.tiles_n <= 8) || a->epilogue == PZ_EPI_DGEGLU ? 2 : 8;
+  }
   if (pl.kind == PATH_GEMV) return pz_gemv_launch(a, st);
   if (a->norm_w)
     PZ_CHECK_ARG((pl.kind == PATH_SKINNY || pl.kind == PATH_SKINNY64) && PZ_ALIGNED(a->norm_w, 16),
@@ -2573,6 +2583,7 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
       (!a->norm_w || PZ_ALIGNED(a->norm_w, 16))) {
     GemmP p;
     memset(&p, 0, sizeof(p));
+    p.group = 8;
     p.A = (const bf16_t*)a->x;
     p.B = (const bf16_t*)a->W;
     p.C = a->q_out;
@@ -2593,6 +2604,7 @@ extern "C" int pz_gemm_qkv_rope(const pz_qkv_rope_args* a, void* stream) {
   if (a->norm_w || a->w_fp8 || !use_8phase() || pl.kind != PATH_256) return PZ_ERR_UNSUPPORTED;
   GemmP p;
   memset(&p, 0, sizeof(p));
+  p.group = 8;
   p.A = (const bf16_t*)a->x;
   p.B = (const bf16_t*)a->W;
   p.C = a->q_out;

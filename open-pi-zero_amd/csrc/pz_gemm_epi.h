@@ -51,16 +51,19 @@ struct GemmP {
   // ... and for the saved activations only (aux: GeGLU g|u, GELU / SiLU pre-activation -- read again only by the
   // backward, long after; PZ_GEMM_NT_AUX, read per call)
   int nt_aux;
+  // super-row height of the 8-phase kernels' tile order (tile_coords; PZ_GEMM_GROUP, read per call; default 8)
+  int group;
 };
 
 namespace {
 
 // bijective XCD-aware remap + grouped (super-row) tile order
-__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn,
+                                            int GROUP = 8) {
   const int xcd = bid & 7, local = bid >> 3;
   const int q = nwg >> 3, r = nwg & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
-  constexpr int GROUP = 8;
+  GROUP = GROUP >= 1 ? GROUP : 8;
   const int per_group = GROUP * tiles_n;
   const int g = wg / per_group;
   const int first_m = g * GROUP;

@@ -1083,3 +1083,43 @@ def test_siglip_mlp_row_pitch_bitwise(M):
     ops.linear_wgrad(g0, x, v0)
     ops.linear_wgrad(g1, x, v1)
     assert torch.equal(v1, v0)
+
+
+@pytest.mark.parametrize("case", ["long_k_narrow", "dgeglu", "geglu_fwd"])
+def test_gemm_tile_order_group_bitwise(case, monkeypatch):
+    """The 8-phase kernels' tile order (tile_coords super-row height: the planner takes 2 for narrow long-K GEMMs and
+    the DGEGLU dgrad, 8 otherwise; PZ_GEMM_GROUP overrides) changes which workgroup computes a tile, never its
+    arithmetic: every group height gives the same bits, also with a ragged last super-row (11 row tiles) and a split
+    tail; against torch fp32 too."""
+    from pizero_native import ops
+
+    torch.manual_seed(3)
+    outs = []
+    for grp in ("", "8", "3", "1", "16"):
+        monkeypatch.setenv("PZ_GEMM_GROUP", grp)
+        torch.manual_seed(3)
+        if case == "long_k_narrow":  # K >= 16384, <= 8 column tiles: group 2 by default
+            M, N, K = 2816, 1024, 16384
+            x, W = bf(M, K, scale=0.5), bf(N, K, scale=K ** -0.5)
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, out)
+            ref = x.float() @ W.float().t()
+        elif case == "dgeglu":  # down-proj dgrad with d(gate|up) in place over the saved g|u: group 2 by default
+            M, I, H = 2816, 2048, 512
+            dy, W = bf(M, H, scale=0.5), bf(H, I, scale=I ** -0.5)
+            out = bf(M, 2 * I)
+            ops.linear_dgrad(dy, W, out, epi=ops.PZ_EPI_DGEGLU, aux=out)
+            ref = None
+        else:  # GeGLU forward: group 8 by default
+            M, K, I = 2816, 512, 1024
+            x, W = bf(M, K), bf(2 * I, K, scale=K ** -0.5)
+            out = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+            ops.linear(x, W, out, epi=ops.PZ_EPI_GEGLU)
+            r = x.float() @ W.float().t()
+            ref = torch.nn.functional.gelu(r[:, :I], approximate="tanh") * r[:, I:]
+        torch.cuda.synchronize()
+        outs.append(out.clone())
+        if ref is not None and grp == "":
+            close(out, ref, atol=2e-2)
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])

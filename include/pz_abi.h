@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define PZ_ABI_VERSION 19
+#define PZ_ABI_VERSION 20
 
 enum {
   PZ_OK = 0,
@@ -350,6 +350,15 @@ int pz_flow_psi(const float* x0, const float* x1, const float* t, void* psi, int
 int pz_flow_loss(const void* v, int64_t ldv, int64_t v_bstride, const float* x0, const float* x1, float* loss,
                  void* dv, const float* grad_scale, int64_t B, int64_t H, int64_t A, float sig_min, void* stream);
 /* Euler step (pizero.py:479-481): a += dt*v ; t += dt.  v row (b,h) at v + b*v_bstride + h*ldv */
+/* ABI 20 -- one denoise step's glue in two launches instead of six (inference; bit-identical to the separate
+ * kernels): pz_action_in = bf16 cast of the fp32 action rows + the action encoder's first Linear (K = A) into
+ * cat[:, D:2D] + the time embedding (pz_time_embed_rows) into cat[:, :D]; pz_action_out = the action expert's final
+ * RMSNorm + the action decoder Linear (D -> A <= 8) + the Euler update action += dt v, t += dt (pz_euler_step).
+ * pizero.py:461-481 with vla/modules.py:15-53 (ActionEncoder, SinusoidalPosEmb) and pizero.py:100-103 */
+int pz_action_in(const float* action, int64_t A, const void* w1, const void* b1, const float* t, void* cat,
+                 int64_t ldc, int64_t B, int64_t H, int64_t D, float max_period, int32_t mode, void* stream);
+int pz_action_out(const void* x, int64_t ldx, const void* norm_w, float eps, const void* wd, const void* bd, int64_t D,
+                  int64_t A, float* action, float* t, int64_t B, int64_t H, float dt, void* stream);
 int pz_euler_step(float* action, const void* v, int64_t ldv, int64_t v_bstride, float* t, int64_t B, int64_t H,
                   int64_t A, float dt, void* stream);
 int pz_clamp(float* x, int64_t n, float lo, float hi, void* stream);

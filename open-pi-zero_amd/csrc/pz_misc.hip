@@ -100,15 +100,11 @@ __global__ void time_embed_kernel(const float* __restrict__ t, bf16_t* out, int6
 
 // time embedding written straight into the first D columns of the action encoder's concat input (inference:
 // every one of a sample's H rows gets its sample's embedding; time_embed_kernel's arithmetic)
-__global__ void time_embed_rows_kernel(const float* __restrict__ t, bf16_t* out, int64_t ldo, int64_t rows,
-                                       int64_t H, int D, float max_period, int mode) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= rows * D) return;
-  const int64_t r = idx / D;
-  const int j = (int)(idx % D), half = D / 2;
+// column j of the time embedding of time tb (time_embed_kernel's arithmetic, both modes)
+__device__ __forceinline__ bf16_t time_embed_col(float tb, int j, int D, float max_period, int mode) {
+  const int half = D / 2;
   const int i = j < half ? j : j - half;
   const float e = (float)(log((double)max_period) / (double)(half - 1));
-  const float tb = t[r / H];
   float a;
   if (mode == 0) {
     a = tb * expf((float)i * -e);
@@ -117,7 +113,126 @@ __global__ void time_embed_rows_kernel(const float* __restrict__ t, bf16_t* out,
     const float f = bf2f(f2bf(expf(bf2f(f2bf(ib * -e)))));
     a = bf2f(f2bf(bf2f(f2bf(tb)) * f));
   }
-  out[r * ldo + j] = f2bf(j < half ? sinf(a) : cosf(a));
+  return f2bf(j < half ? sinf(a) : cosf(a));
+}
+
+__global__ void time_embed_rows_kernel(const float* __restrict__ t, bf16_t* out, int64_t ldo, int64_t rows,
+                                       int64_t H, int D, float max_period, int mode) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * D) return;
+  const int64_t r = idx / D;
+  const int j = (int)(idx % D);
+  out[r * ldo + j] = time_embed_col(t[r / H], j, D, max_period, mode);
+}
+
+// Denoise-step input in one launch (inference): cat[r] = [time embedding of sample r / H | linear_1(bf16(action[r]))]
+// -- the bf16 cast, the 7 -> D action Linear (gemm_small_kernel's arithmetic: fp32 sum over k in order, bias, one
+// bf16 rounding) and time_embed_rows_kernel, bit for bit, in one launch instead of three
+__global__ void action_in_kernel(const float* __restrict__ action, int64_t A, const bf16_t* __restrict__ W1,
+                                 const bf16_t* __restrict__ b1, const float* __restrict__ t, bf16_t* cat, int64_t ldc,
+                                 int64_t rows, int64_t H, int D, float max_period, int mode) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= rows * 2 * D) return;
+  const int64_t r = idx / (2 * D);
+  const int j = (int)(idx % (2 * D));
+  if (j < D) {
+    cat[r * ldc + j] = time_embed_col(t[r / H], j, D, max_period, mode);
+    return;
+  }
+  const int n = j - D;
+  float s = 0.f;
+  for (int64_t k = 0; k < A; ++k) s += bf2f(f2bf(action[r * A + k])) * bf2f(W1[n * A + k]);
+  s *= 1.f;
+  if (b1) s += bf2f(b1[n]);
+  cat[r * ldc + j] = f2bf(s);
+}
+
+// Denoise-step output in one launch (inference), one wave per row: the action expert's final RMSNorm
+// (rmsnorm_fwd_kernel's arithmetic: 8-element chunks lane + 64 c, fp32 sum of squares, y = x r (1 + w) rounded to
+// bf16), the D -> A action decoder (gemm_small_rowwave_kernel's arithmetic on the same chunks, butterfly sum, bias,
+// bf16 v) and the Euler update action += dt v (euler_kernel), bit for bit -- one launch instead of three.  D <= 1024,
+// D % 8 == 0, A <= 8.
+__global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restrict__ x, int64_t ldx,
+                                                         const bf16_t* __restrict__ nw, float eps,
+                                                         const bf16_t* __restrict__ Wd, const bf16_t* __restrict__ bd,
+                                                         int D, int A, float* action, float* t, int64_t rows,
+                                                         int64_t H, float dt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nc = D / 8;
+  float v[2][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      const u32x4 q = *reinterpret_cast<const u32x4*>(x + row * ldx + ch * 8);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[c][2 * i] = __uint_as_float(q[i] << 16);
+        v[c][2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ss += v[c][i] * v[c][i];
+    }
+  }
+  ss = warp_sum(ss);
+  const float r = rsqrtf(ss / (float)D + eps);
+  u32x4 y[2] = {u32x4{0u, 0u, 0u, 0u}, u32x4{0u, 0u, 0u, 0u}};
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = lane + 64 * c;
+    if (ch < nc) {
+      const u32x4 q = *reinterpret_cast<const u32x4*>(nw + ch * 8);
+      float o[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        o[2 * i] = v[c][2 * i] * r * (1.f + __uint_as_float(q[i] << 16));
+        o[2 * i + 1] = v[c][2 * i + 1] * r * (1.f + __uint_as_float(q[i] & 0xffff0000u));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[c][i] = pack2bf(o[2 * i], o[2 * i + 1]);
+    }
+  }
+  constexpr int NMAX = 8;
+  float s[NMAX];
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) s[n] = 0.f;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int64_t k = 8 * lane + 512 * c;
+    if (k >= D) break;
+    const u32x4 xa = y[c];
+    float xf[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      xf[2 * e] = bf2f(xa[e] & 0xffff);
+      xf[2 * e + 1] = bf2f(xa[e] >> 16);
+    }
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n) {
+      if (n >= A) break;
+      const u32x4 wb = *reinterpret_cast<const u32x4*>(Wd + n * (int64_t)D + k);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s[n] += xf[2 * e] * bf2f(wb[e] & 0xffff) + xf[2 * e + 1] * bf2f(wb[e] >> 16);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < NMAX; ++n) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s[n] += __shfl_xor(s[n], off);
+  }
+  if (lane < A) {
+    float o = 0.f;
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n)
+      if (n == lane) o = s[n];
+    o *= 1.f;
+    if (bd) o += bf2f(bd[lane]);
+    action[row * A + lane] += dt * bf2f(f2bf(o));
+  }
+  if (t && lane == 0 && row % H == 0) t[row / H] += dt;
 }
 
 __global__ void concat_time_kernel(const bf16_t* __restrict__ temb, const bf16_t* __restrict__ e1, bf16_t* out,
@@ -403,6 +518,31 @@ extern "C" int pz_time_embed_rows(const float* t, void* out, int64_t ldo, int64_
                "time_embed_rows: bad args");
   hipLaunchKernelGGL(time_embed_rows_kernel, dim3(nblk(B * H * D)), dim3(256), 0, ST, t, (bf16_t*)out, ldo, B * H, H,
                      (int)D, max_period, (int)mode);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_action_in(const float* action, int64_t A, const void* w1, const void* b1, const float* t, void* cat,
+                            int64_t ldc, int64_t B, int64_t H, int64_t D, float max_period, int32_t mode, void* stream) {
+  PZ_CHECK_ARG(action && w1 && t && cat && A > 0 && B > 0 && H > 0 && D >= 4 && D % 2 == 0 && ldc >= 2 * D &&
+                   (mode == 0 || mode == 1),
+               "action_in: bad args");
+  hipLaunchKernelGGL(action_in_kernel, dim3(nblk(B * H * 2 * D)), dim3(256), 0, ST, action, A, (const bf16_t*)w1,
+                     (const bf16_t*)b1, t, (bf16_t*)cat, ldc, B * H, H, (int)D, max_period, (int)mode);
+  PZ_CHECK_LAUNCH();
+  return PZ_OK;
+}
+
+extern "C" int pz_action_out(const void* x, int64_t ldx, const void* norm_w, float eps, const void* wd, const void* bd,
+                             int64_t D, int64_t A, float* action, float* t, int64_t B, int64_t H, float dt,
+                             void* stream) {
+  PZ_CHECK_ARG(x && norm_w && wd && action && B > 0 && H > 0 && A >= 1 && A <= 8 && D >= 8 && D <= 1024 &&
+                   D % 8 == 0 && ldx % 8 == 0 && PZ_ALIGNED(x, 16) && PZ_ALIGNED(norm_w, 16) && PZ_ALIGNED(wd, 16),
+               "action_out: D <= 1024, D %% 8 == 0, A <= 8, 16-byte aligned rows");
+  const int64_t rows = B * H;
+  hipLaunchKernelGGL(action_out_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, ST, (const bf16_t*)x, ldx,
+                     (const bf16_t*)norm_w, eps, (const bf16_t*)wd, (const bf16_t*)bd, (int)D, (int)A, action, t, rows,
+                     H, dt);
   PZ_CHECK_LAUNCH();
   return PZ_OK;
 }

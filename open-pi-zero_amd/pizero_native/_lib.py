@@ -19,7 +19,7 @@ if os.environ.get("PZ_LIB_PATH"):
     print(f"[pizero_native] PZ_LIB_PATH override: loading {LIB_PATH} instead of the default libpizero_hip.so",
           file=_sys.stderr, flush=True)
 
-ABI_VERSION = 19  # include/pz_abi.h PZ_ABI_VERSION
+ABI_VERSION = 20  # include/pz_abi.h PZ_ABI_VERSION
 PZ_EPI_NONE, PZ_EPI_GELU, PZ_EPI_GEGLU, PZ_EPI_SILU = 0, 1, 2, 3
 PZ_EPI_DGELU, PZ_EPI_DSILU, PZ_EPI_DGEGLU = 4, 5, 6
 PZ_SUMSQ_PARTS = 2048  # include/pz_abi.h
@@ -164,6 +164,8 @@ SIGNATURES = {
     "pz_flow_psi": [vp, vp, vp, vp, i64, i64, f32, vp],
     "pz_flow_loss": [vp, i64, i64, vp, vp, vp, vp, vp, i64, i64, i64, f32, vp],
     "pz_euler_step": [vp, vp, i64, i64, vp, i64, i64, i64, f32, vp],
+    "pz_action_in": [vp, i64, vp, vp, vp, vp, i64, i64, i64, i64, f32, i32, vp],
+    "pz_action_out": [vp, i64, vp, f32, vp, vp, i64, i64, vp, vp, i64, i64, f32, vp],
     "pz_copy_rows": [vp, i64, i64, vp, i64, i64, i64, i64, i64, f32, i32, vp],
     "pz_time_embed_rows": [vp, vp, i64, i64, i64, i64, f32, i32, vp],
     "pz_clamp": [vp, i64, f32, f32, vp],

@@ -686,6 +686,16 @@ class Engine:
                         math.sqrt(d.gH), 1.0)
         return X
 
+    def _action_embed_tail(self, cat):
+        """the action encoder after its concat input (inference): Linear + SiLU, Linear"""
+        d = self.d
+        e2 = torch.empty(cat.shape[0], d.aH, device=cat.device, dtype=BF16)
+        ops.linear(cat, self.w("action_encoder.linear_2.weight"), e2, bias=self.w("action_encoder.linear_2.bias"),
+                   epi=PZ_EPI_SILU)
+        e3 = torch.empty_like(e2)
+        ops.linear(e2, self.w("action_encoder.linear_3.weight"), e3, bias=self.w("action_encoder.linear_3.bias"))
+        return e3
+
     def action_embed(self, psi_bf, t, save):
         """ActionEncoder (vla/modules.py:39-53) with time embedding (vla/modules.py:15-22).  Inference (save None):
         the first Linear and the time embedding write straight into the concat input (pz_time_embed_rows: no
@@ -1503,9 +1513,18 @@ class Engine:
         d = self.d
         dev = action.device
         nh, hd, Lp, L = d.nh, d.hd, d.Lp, d.L
-        psi = torch.empty(B * d.H, d.A, device=dev, dtype=BF16)
-        ops.cast_to_bf16(action, psi)
-        e3 = self.action_embed(psi, t, None)
+        # the step's glue in two launches (pz_action_in / pz_action_out, bit-identical to cast + Linear + time
+        # embedding and RMSNorm + decoder + Euler; PZ_FUSED_GLUE=0: the separate kernels)
+        glue = d.aH <= 1024 and d.aH % 8 == 0 and d.A <= 8 and os.environ.get("PZ_FUSED_GLUE", "1") != "0"
+        if glue:
+            cat = torch.empty(B * d.H, 2 * d.aH, device=dev, dtype=BF16)
+            ops.action_in(action, self.w("action_encoder.linear_1.weight"), self.w("action_encoder.linear_1.bias"), t,
+                          cat, B, d.H, d.aH, d.tmax, ref_bf16=d.time_bf16)
+            e3 = self._action_embed_tail(cat)
+        else:
+            psi = torch.empty(B * d.H, d.A, device=dev, dtype=BF16)
+            ops.cast_to_bf16(action, psi)
+            e3 = self.action_embed(psi, t, None)
         x = torch.empty_like(e3)
         ops.copy_rows(e3, d.aH, 0, x, d.aH, 0, 1, B * d.H, d.aH, scale=math.sqrt(d.aH))
         g = Group("action", "joint_model.mixtures.action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI, d.a_theta,
@@ -1552,6 +1571,11 @@ class Engine:
             ops.attn_softmax(S, Lp, Pm, Lp, B * d.H * nh, L, 1.0 / math.sqrt(hd), cap=50.0,
                              rows_per_batch=d.H * nh, heads=nh, qoff=d.P + d.C, **_mask_kw(d, cnt, "act"))
             x = self._post_attn(g, p, x, Pm, Vj, B, d.H, Lp, qrow0=0)
+        if glue:
+            ops.action_out(x, self.w("joint_model.mixtures.action.norm.weight"), d.rms_eps,
+                           self.w("action_decoder.weight"), self.w("action_decoder.bias"), action, t, B, d.H,
+                           1.0 / d.steps)
+            return
         y = torch.empty_like(x)
         ops.rmsnorm(x, self.w("joint_model.mixtures.action.norm.weight"), y, None, d.rms_eps)
         v = torch.empty(B * d.H, 8, device=dev, dtype=BF16)

@@ -621,6 +621,20 @@ def flow_loss(v, ldv, vbs, x0, x1, loss, dv, grad_scale, B, H, A, sig_min):
          float(sig_min), _st())
 
 
+def action_in(action, W1, b1, t, cat, B, H, D, max_period, ref_bf16=False):
+    """cat[:, :D] = time embedding, cat[:, D:2D] = bf16(action) @ W1^T + b1 (one launch; inference)"""
+    A = action.shape[-1]
+    call("pz_action_in", _p(action), A, _p(W1), _p(b1), _p(t), _p(cat), cat.stride(0), B, H, D, float(max_period),
+         int(bool(ref_bf16)), _st())
+
+
+def action_out(x, norm_w, eps, Wd, bd, action, t, B, H, dt):
+    """action += dt * (RMSNorm(x) @ Wd^T + bd) (bf16 v), t += dt: the denoise step's tail in one launch"""
+    D = x.shape[1]
+    call("pz_action_out", _p(x), x.stride(0), _p(norm_w), float(eps), _p(Wd), _p(bd), D, Wd.shape[0], _p(action),
+         _p(t), B, H, float(dt), _st())
+
+
 def euler_step(action, v, ldv, vbs, t, B, H, A, dt):
     call("pz_euler_step", _p(action), _p(v), ldv, vbs, _p(t), B, H, A, float(dt), _st())
 

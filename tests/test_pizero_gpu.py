@@ -170,6 +170,23 @@ def test_full_actions_b1_benched_config(full_model, sample):
     assert torch.equal(ag.float(), a.float()), float((ag.float() - a.float()).abs().max())
 
 
+def test_fused_denoise_glue_bitwise(full_model, monkeypatch):
+    """pz_action_in / pz_action_out (a denoise step's cast + action Linear + time embedding, and final RMSNorm +
+    action decoder + Euler update, two launches instead of six) give the same action chunk bit for bit as the
+    separate kernels (PZ_FUSED_GLUE=0), at the benched B=1 and at B=2 (the fused path is the default)."""
+    d = O.FULL_DIMS
+    g = load_golden("full")
+    m = full_model
+    for sel in ([0], None):
+        gi = gpu_inputs(m, d, int(g["bsz"]), select=sel)
+        outs = []
+        for fused in ("1", "0"):
+            monkeypatch.setenv("PZ_FUSED_GLUE", fused)
+            outs.append(run_infer(m, gi, clip=False).float().clone())
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
+
+
 def test_full_actions_fp8(full):
     """Config C5's fp8 inference (PiZero.use_fp8_inference: e4m3 weights with per-tensor scales; prefill
     GEMMs W8A8 on the fp8 MFMA with per-row activation scales, denoise rows W8A16) at bridge size

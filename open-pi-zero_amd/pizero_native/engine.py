@@ -1515,7 +1515,9 @@ class Engine:
         nh, hd, Lp, L = d.nh, d.hd, d.Lp, d.L
         # the step's glue in two launches (pz_action_in / pz_action_out, bit-identical to cast + Linear + time
         # embedding and RMSNorm + decoder + Euler; PZ_FUSED_GLUE=0: the separate kernels)
-        glue = d.aH <= 1024 and d.aH % 8 == 0 and d.A <= 8 and os.environ.get("PZ_FUSED_GLUE", "1") != "0"
+        glue = (d.aH <= 1024 and d.aH % 8 == 0 and d.A <= 8 and os.environ.get("PZ_FUSED_GLUE", "1") != "0" and
+                all(self.w(k).data_ptr() % 16 == 0 for k in ("joint_model.mixtures.action.norm.weight",
+                                                             "action_decoder.weight")))
         if glue:
             cat = torch.empty(B * d.H, 2 * d.aH, device=dev, dtype=BF16)
             ops.action_in(action, self.w("action_encoder.linear_1.weight"), self.w("action_encoder.linear_1.bias"), t,

@@ -686,15 +686,34 @@ class Engine:
                         math.sqrt(d.gH), 1.0)
         return X
 
-    def _action_embed_tail(self, cat):
-        """the action encoder after its concat input (inference): Linear + SiLU, Linear"""
+    def _action_embed_tail(self, cat, alpha=1.0):
+        """the action encoder after its concat input (inference): Linear + SiLU, Linear -- the last one times alpha
+        (a power of two: the bias is pre-scaled by it, exactly, and cached per weight version)"""
         d = self.d
         e2 = torch.empty(cat.shape[0], d.aH, device=cat.device, dtype=BF16)
         ops.linear(cat, self.w("action_encoder.linear_2.weight"), e2, bias=self.w("action_encoder.linear_2.bias"),
                    epi=PZ_EPI_SILU)
         e3 = torch.empty_like(e2)
-        ops.linear(e2, self.w("action_encoder.linear_3.weight"), e3, bias=self.w("action_encoder.linear_3.bias"))
+        b3 = self.w("action_encoder.linear_3.bias")
+        if alpha != 1.0:
+            if getattr(self, "_b3s_alpha", None) != alpha:
+                self._b3s = torch.empty_like(b3)
+                self._b3s_alpha, self._b3s_version = alpha, None
+            self.derived_refresh()
+            b3 = self._b3s
+        ops.linear(e2, self.w("action_encoder.linear_3.weight"), e3, bias=b3, alpha=alpha)
         return e3
+
+    def derived_refresh(self):
+        """Recompute the weight-derived bf16 tensors (the alpha-scaled action-encoder bias) IN PLACE when the
+        weights changed: a captured InferenceGraph holds their pointers, so InferenceGraph.replay calls this
+        before every replay.  Returns True if it recomputed."""
+        if getattr(self, "_b3s_alpha", None) is None or self._b3s_version == self.weights_version():
+            return False
+        b3 = self.w("action_encoder.linear_3.bias")
+        self._b3s.copy_(b3.float() * self._b3s_alpha)  # exact: alpha is a power of two
+        self._b3s_version = self.weights_version()
+        return True
 
     def action_embed(self, psi_bf, t, save):
         """ActionEncoder (vla/modules.py:39-53) with time embedding (vla/modules.py:15-22).  Inference (save None):
@@ -1522,13 +1541,22 @@ class Engine:
             cat = torch.empty(B * d.H, 2 * d.aH, device=dev, dtype=BF16)
             ops.action_in(action, self.w("action_encoder.linear_1.weight"), self.w("action_encoder.linear_1.bias"), t,
                           cat, B, d.H, d.aH, d.tmax, ref_bf16=d.time_bf16)
-            e3 = self._action_embed_tail(cat)
+            sq = math.sqrt(d.aH)
+            if sq.is_integer() and (int(sq) & (int(sq) - 1)) == 0 and os.environ.get("PZ_FOLD_SCALE", "1") != "0":
+                # the joint model's sqrt(hidden) input scaling is a power of two (32 at hidden 1024): folded into the
+                # last encoder Linear as alpha with a pre-scaled bias -- 2^k (acc + b) rounds exactly like rounding
+                # first and scaling the bf16 after (the copy_rows launch it replaces), so the bits are unchanged
+                x = self._action_embed_tail(cat, alpha=sq)
+            else:
+                e3 = self._action_embed_tail(cat)
+                x = torch.empty_like(e3)
+                ops.copy_rows(e3, d.aH, 0, x, d.aH, 0, 1, B * d.H, d.aH, scale=sq)
         else:
             psi = torch.empty(B * d.H, d.A, device=dev, dtype=BF16)
             ops.cast_to_bf16(action, psi)
             e3 = self.action_embed(psi, t, None)
-        x = torch.empty_like(e3)
-        ops.copy_rows(e3, d.aH, 0, x, d.aH, 0, 1, B * d.H, d.aH, scale=math.sqrt(d.aH))
+            x = torch.empty_like(e3)
+            ops.copy_rows(e3, d.aH, 0, x, d.aH, 0, 1, B * d.H, d.aH, scale=math.sqrt(d.aH))
         g = Group("action", "joint_model.mixtures.action.layers.", ["action"], d.H, d.P + d.C, d.aH, d.aI, d.a_theta,
                   False, "action")
         Q = torch.empty(B, d.H, nh * hd, device=dev, dtype=BF16)

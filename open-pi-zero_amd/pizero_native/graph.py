@@ -77,6 +77,7 @@ class InferenceGraph:
         # fp8 codes and their per-tensor scales are baked into the captured launches, so a weight change
         # since the capture re-quantises them (Engine.fp8_refresh) and re-captures the graph
         e = self.m._engine()
+        e.derived_refresh()  # in place: the captured launches keep their pointers
         if e.f8 is not self._f8 or e.fp8_refresh():
             self.capture()
         self.graph.replay()

@@ -173,7 +173,9 @@ def test_full_actions_b1_benched_config(full_model, sample):
 def test_fused_denoise_glue_bitwise(full_model, monkeypatch):
     """pz_action_in / pz_action_out (a denoise step's cast + action Linear + time embedding, and final RMSNorm +
     action decoder + Euler update, two launches instead of six) give the same action chunk bit for bit as the
-    separate kernels (PZ_FUSED_GLUE=0), at the benched B=1 and at B=2 (the fused path is the default)."""
+    separate kernels (PZ_FUSED_GLUE=0), at the benched B=1 and at B=2 (the fused path is the default).  The
+    fused path also folds the joint model's sqrt(hidden) = 32 input scale into the action encoder's last Linear
+    (alpha + a pre-scaled bias) where PZ_FUSED_GLUE=0 scales the rows in a separate launch."""
     d = O.FULL_DIMS
     g = load_golden("full")
     m = full_model
@@ -223,7 +225,8 @@ def test_fp8_codes_follow_weight_changes(full):
     """the fp8 weight copies are re-quantised when the weights change after use_fp8_inference
     (an in-place write through a parameter, e.g. load_state_dict; FusedAdamW.step bumps the same version
     counter after its raw-pointer kernel writes): eager and hipGraph inference then equal a fresh
-    prepare on the new weights, never the stale codes."""
+    prepare on the new weights, never the stale codes.  The action encoder's last bias also changes: the
+    graph reads an alpha-scaled copy of it (Engine.derived_refresh), refreshed in place before a replay."""
     from pizero_native.graph import InferenceGraph
     from pizero_native.optim import FusedAdamW
 
@@ -232,6 +235,8 @@ def test_fp8_codes_follow_weight_changes(full):
     name = "joint_model.mixtures.action.layers.0.mlp.down_proj.weight"
     p = m._param(name)  # (tied: named_parameters() may list it under the proprio alias)
     keep = p.detach().clone()
+    pb = m._param("action_encoder.linear_3.bias")
+    keep_b = pb.detach().clone()
     try:
         m.use_fp8_inference(True)
         a0 = run_infer(m, gi, clip=False)
@@ -242,6 +247,7 @@ def test_fp8_codes_follow_weight_changes(full):
         torch.cuda.synchronize()
         with torch.no_grad():
             p.mul_(-3.0)  # a large change of one fp8-served weight
+            pb.add_(0.25)  # and of a bf16 bias read through a derived (scaled) copy
         a1 = run_infer(m, gi, clip=False)
         ag = ig.replay().clone()
         torch.cuda.synchronize()
@@ -260,6 +266,7 @@ def test_fp8_codes_follow_weight_changes(full):
     finally:
         with torch.no_grad():
             p.copy_(keep)
+            pb.copy_(keep_b)
         m.use_fp8_inference(False)
         m.zero_grad(set_to_none=True)
 

@@ -7,6 +7,11 @@ import csv
 import sys
 
 
+def _step_start(r):
+    """first kernel of a denoise step: the time embedding (separate glue) or pz_action_in (fused glue, ABI 20)"""
+    return "time_embed" in r["Kernel_Name"] or "action_in_kernel" in r["Kernel_Name"]
+
+
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if r.get("Start_Timestamp") and r.get("End_Timestamp")]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -16,13 +21,13 @@ def main():
     ch = None
     for k in range(len(idx) - 2, -1, -1):
         seg = rows[idx[k]:idx[k + 1]]
-        if sum("time_embed" in r["Kernel_Name"] for r in seg) == 10:
+        if sum(_step_start(r) for r in seg) == 10:
             ch = seg
             break
     if ch is None:
         ch = rows[idx[-2]:idx[-1]]
     t0 = int(ch[0]["Start_Timestamp"])
-    te = [i for i, r in enumerate(ch) if "time_embed" in r["Kernel_Name"] or "denoise" in r["Kernel_Name"]]
+    te = [i for i, r in enumerate(ch) if _step_start(r) or "denoise" in r["Kernel_Name"]]
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
     print(f"chunk: {len(ch)} kernels, wall {(int(ch[-1]['End_Timestamp']) - t0) / 1e3:.1f} us, "
           f"busy {sum(map(dur, ch)):.1f} us; prefill {te[0]} kernels, "

@@ -141,9 +141,24 @@ __global__ void action_in_kernel(const float* __restrict__ action, int64_t A, co
   }
   const int n = j - D;
   float s = 0.f;
-  for (int64_t k = 0; k < A; ++k) s += bf2f(f2bf(action[r * A + k])) * bf2f(W1[n * A + k]);
-  s *= 1.f;
-  if (b1) s += bf2f(b1[n]);
+  if (A <= 8) {  // (the action dims of every Pi0 config) all loads in flight before the first product, same sum order
+    float xa[8], wa[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      xa[k] = k < A ? action[r * A + k] : 0.f;
+      wa[k] = k < A ? bf2f(W1[n * A + k]) : 0.f;
+    }
+    const float bias = b1 ? bf2f(b1[n]) : 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < A) s += bf2f(f2bf(xa[k])) * wa[k];
+    s *= 1.f;
+    if (b1) s += bias;
+  } else {
+    for (int64_t k = 0; k < A; ++k) s += bf2f(f2bf(action[r * A + k])) * bf2f(W1[n * A + k]);
+    s *= 1.f;
+    if (b1) s += bf2f(b1[n]);
+  }
   cat[r * ldc + j] = f2bf(s);
 }
 
@@ -161,13 +176,29 @@ __global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restric
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nc = D / 8;
+  constexpr int NMAX = 8;
+  // every global load up front (the row, the norm weights, the decoder rows, bias and action): one memory round trip
+  // instead of three dependent ones; the arithmetic below is unchanged
+  u32x4 xq[2], wq[2], wd[2][NMAX];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int ch = lane + 64 * c;
+    const bool ok = ch < nc;
+    xq[c] = ok ? *reinterpret_cast<const u32x4*>(x + row * ldx + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+    wq[c] = ok ? *reinterpret_cast<const u32x4*>(nw + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int n = 0; n < NMAX; ++n)
+      wd[c][n] = ok && n < A ? *reinterpret_cast<const u32x4*>(Wd + n * (int64_t)D + ch * 8) : u32x4{0u, 0u, 0u, 0u};
+  }
+  const float bias = lane < A && bd ? bf2f(bd[lane]) : 0.f;
+  const float act = lane < A ? action[row * A + lane] : 0.f;
   float v[2][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const int ch = lane + 64 * c;
     if (ch < nc) {
-      const u32x4 q = *reinterpret_cast<const u32x4*>(x + row * ldx + ch * 8);
+      const u32x4 q = xq[c];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[c][2 * i] = __uint_as_float(q[i] << 16);
@@ -184,7 +215,7 @@ __global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restric
   for (int c = 0; c < 2; ++c) {
     const int ch = lane + 64 * c;
     if (ch < nc) {
-      const u32x4 q = *reinterpret_cast<const u32x4*>(nw + ch * 8);
+      const u32x4 q = wq[c];
       float o[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -195,7 +226,6 @@ __global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restric
       for (int i = 0; i < 4; ++i) y[c][i] = pack2bf(o[2 * i], o[2 * i + 1]);
     }
   }
-  constexpr int NMAX = 8;
   float s[NMAX];
 #pragma unroll
   for (int n = 0; n < NMAX; ++n) s[n] = 0.f;
@@ -213,7 +243,7 @@ __global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restric
 #pragma unroll
     for (int n = 0; n < NMAX; ++n) {
       if (n >= A) break;
-      const u32x4 wb = *reinterpret_cast<const u32x4*>(Wd + n * (int64_t)D + k);
+      const u32x4 wb = wd[c][n];
 #pragma unroll
       for (int e = 0; e < 4; ++e) s[n] += xf[2 * e] * bf2f(wb[e] & 0xffff) + xf[2 * e + 1] * bf2f(wb[e] >> 16);
     }
@@ -229,8 +259,8 @@ __global__ void __launch_bounds__(256) action_out_kernel(const bf16_t* __restric
     for (int n = 0; n < NMAX; ++n)
       if (n == lane) o = s[n];
     o *= 1.f;
-    if (bd) o += bf2f(bd[lane]);
-    action[row * A + lane] += dt * bf2f(f2bf(o));
+    if (bd) o += bias;
+    action[row * A + lane] = act + dt * bf2f(f2bf(o));
   }
   if (t && lane == 0 && row % H == 0) t[row / H] += dt;
 }

@@ -43,6 +43,11 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const bf16_t* __restri
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const int nc = D / 8;
+  // the weight chunks loaded with the row, not after its reduction: one memory round trip
+  u32x4 wq[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    wq[c] = lane + 64 * c < nc ? *reinterpret_cast<const u32x4*>(w + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
   float v[MAXC][8];
   float ss = 0.f;
 #pragma unroll
@@ -62,7 +67,7 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const bf16_t* __restri
     const int ch = lane + 64 * c;
     if (ch < nc) {
       float wv[8], o[8];
-      load8(w + ch * 8, wv);
+      unpack8(wq[c], wv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = v[c][i] * r * (1.f + wv[i]);
       store8(y + row * ldy + ch * 8, o);
@@ -153,6 +158,14 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const bf16_t* __rest
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const int nc = D / 8;
+  // the weight and bias chunks loaded with the row, not after its reductions: one memory round trip
+  u32x4 wq[MAXC], bq[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const bool ok = lane + 64 * c < nc;
+    wq[c] = ok ? *reinterpret_cast<const u32x4*>(w + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
+    bq[c] = ok ? *reinterpret_cast<const u32x4*>(b + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
+  }
   float v[MAXC][8];
   float s = 0.f;
 #pragma unroll
@@ -186,8 +199,8 @@ __global__ void __launch_bounds__(256) layernorm_fwd_kernel(const bf16_t* __rest
     const int ch = lane + 64 * c;
     if (ch < nc) {
       float wv[8], bv[8], o[8];
-      load8(w + ch * 8, wv);
-      load8(b + ch * 8, bv);
+      unpack8(wq[c], wv);
+      unpack8(bq[c], bv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[i] = (v[c][i] - mu) * r * wv[i] + bv[i];
       store8(y + row * ldy + ch * 8, o);
@@ -645,6 +658,11 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const bf16_t* __restric
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const int nc = D / 8;
+  // the weight chunks loaded with the row, not after its reduction: one memory round trip
+  u32x4 wq[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+    wq[c] = lane + 64 * c < nc ? *reinterpret_cast<const u32x4*>(w + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
   float v[MAXC][8];
   float ss = 0.f;
 #pragma unroll
@@ -663,7 +681,7 @@ __global__ void __launch_bounds__(256) rmsnorm_q8_kernel(const bf16_t* __restric
     const int ch = lane + 64 * c;
     if (ch < nc) {
       float wv[8];
-      load8(w + ch * 8, wv);
+      unpack8(wq[c], wv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[c][i] = v[c][i] * r * (1.f + wv[i]);
     }
@@ -680,6 +698,14 @@ __global__ void __launch_bounds__(256) layernorm_q8_kernel(const bf16_t* __restr
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
   const int nc = D / 8;
+  // the weight and bias chunks loaded with the row, not after its reductions: one memory round trip
+  u32x4 wq[MAXC], bq[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const bool ok = lane + 64 * c < nc;
+    wq[c] = ok ? *reinterpret_cast<const u32x4*>(w + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
+    bq[c] = ok ? *reinterpret_cast<const u32x4*>(b + (lane + 64 * c) * 8) : u32x4{0u, 0u, 0u, 0u};
+  }
   float v[MAXC][8];
   float s = 0.f;
 #pragma unroll
@@ -709,8 +735,8 @@ __global__ void __launch_bounds__(256) layernorm_q8_kernel(const bf16_t* __restr
     const int ch = lane + 64 * c;
     if (ch < nc) {
       float wv[8], bv[8];
-      load8(w + ch * 8, wv);
-      load8(b + ch * 8, bv);
+      unpack8(wq[c], wv);
+      unpack8(bq[c], bv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[c][i] = (v[c][i] - mu) * r * wv[i] + bv[i];
     }

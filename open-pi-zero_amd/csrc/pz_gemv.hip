@@ -152,15 +152,21 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemvP p) {
       wok[CPG + c] = wok[c];
     }
   }
+  // epilogue: thread j < M*CPG of the group owns (row r, column c); its bias / residual are loaded before the weight
+  // stream, not after the reduction (one dependent memory round trip less)
+  const int r = j / CPG, c = j % CPG;
+  const int64_t n = col0 + c;
+  const bool own = j < p.M * CPG && n < p.N;
+  float e_bias = 0.f, e_res = 0.f;
+  if (!GEGLU && own) {
+    if (p.bias) e_bias = bf2f(p.bias[n]);
+    if (p.resid) e_res = bf2f(p.resid[r * p.ldr + n]);
+  }
   float acc[MR][CW], ss[MR];
   gemv_body<MR, CW, TPG>(p, wrow, wok, j, acc, ss);
   const bool nrm = p.nw != nullptr;
   gemv_reduce<MR, CW, TPG>(acc, ss, red, fin, nrm);
-  // epilogue: thread j < M*CPG of the group owns (row r, column c)
-  if (j >= p.M * CPG) return;
-  const int r = j / CPG, c = j % CPG;
-  const int64_t n = col0 + c;
-  if (n >= p.N) return;
+  if (!own) return;
   const float* gr = fin + g * NV;
   float scale = p.alpha;
   if (nrm) scale *= rsqrtf(gr[MR * CW + r] / (float)p.K + p.neps);
@@ -173,12 +179,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(GemvP p) {
     }
     x = gelu_tanh(x) * u;
   } else {
-    if (p.bias) x += bf2f(p.bias[n]);
+    if (p.bias) x += e_bias;
     if (p.epi == PZ_EPI_GELU || p.epi == PZ_EPI_SILU) {
       if (p.aux) p.aux[r * p.ldaux + n] = f2bf(x);
       x = p.epi == PZ_EPI_GELU ? gelu_tanh(x) : silu(x);
     }
-    if (p.resid) x += bf2f(p.resid[r * p.ldr + n]);
+    if (p.resid) x += e_res;
   }
   if (p.c_fp32) {
     float* C = reinterpret_cast<float*>(p.y) + r * p.ldy + n;
@@ -212,20 +218,30 @@ __global__ void __launch_bounds__(256) gemv_qkv_rope_kernel(GemvP p) {
     wrow[PPG + c] = h * p.hd + i + half;
     wok[c] = wok[PPG + c] = pr < npairs;
   }
-  float acc[MR][CW], ss[MR];
-  gemv_body<MR, CW, TPG>(p, wrow, wok, j, acc, ss);
-  const bool nrm = p.nw != nullptr;
-  gemv_reduce<MR, CW, TPG>(acc, ss, red, fin, nrm);
-  if (j >= p.M * PPG) return;
+  // the owner of (row r, pair c) reads its position before the weight stream and its (cos, sin) right after it, both
+  // off the epilogue's critical path (they were two dependent round trips after the reduction)
   const int r = j / PPG, c = j % PPG;
   const int64_t pr = pair0 + c;
-  if (pr >= npairs) return;
+  const bool own = j < p.M * PPG && pr < npairs;
+  const int64_t h = own ? pr / half : 0, i = own ? pr % half : 0;
+  const bool rot = own && h != p.nh + 1;
+  const int64_t ps = rot ? p.pos[r] : 0;
+  float acc[MR][CW], ss[MR];
+  gemv_body<MR, CW, TPG>(p, wrow, wok, j, acc, ss);
+  float co = 0.f, si = 0.f;
+  if (rot) {
+    const float* cs = p.cs + ps * p.hd;
+    co = cs[2 * i];
+    si = cs[2 * i + 1];
+  }
+  const bool nrm = p.nw != nullptr;
+  gemv_reduce<MR, CW, TPG>(acc, ss, red, fin, nrm);
+  if (!own) return;
   const float* gr = fin + g * NV;
   float scale = 1.f;
   if (nrm) scale = rsqrtf(gr[MR * CW + r] / (float)p.K + p.neps);
   // the unfused path rounds the projection to bf16 before rotating: do the same
   const float y1 = bf2f(f2bf(gr[r * CW + c] * scale)), y2 = bf2f(f2bf(gr[r * CW + PPG + c] * scale));
-  const int64_t h = pr / half, i = pr % half;
   const int64_t b = r / p.T, t = r % p.T;
   if (h == p.nh + 1) {  // value head: no rotation
     bf16_t* dv = p.v + (b * p.Lk + p.koff + t) * p.hd;
@@ -233,8 +249,6 @@ __global__ void __launch_bounds__(256) gemv_qkv_rope_kernel(GemvP p) {
     dv[i + half] = f2bf(y2);
     return;
   }
-  const float* cs = p.cs + p.pos[r] * p.hd;
-  const float co = cs[2 * i], si = cs[2 * i + 1];
   float o1, o2;
   rope_pair(y1, y2, co, si, o1, o2);
   bf16_t* d = h < p.nh ? p.q + (b * p.Lq + p.qoff + t) * (p.nh * p.hd) + h * p.hd

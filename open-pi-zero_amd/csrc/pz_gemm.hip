@@ -1543,28 +1543,41 @@ __global__ void __launch_bounds__(NT2) gemm8p_tail_epilogue(GemmP p) {
   // pieces loaded PB at a time (2 PB loads in flight per thread), summed in piece order (deterministic)
   const f32x4* W0 = W + (rb * 4 + c0) * NT2 + t;
   const f32x4* W1 = W + (rb * 4 + c1) * NT2 + t;
-  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-  for (int z = 0; z < p.tail_s; z += PB) {
-    f32x4 v0[PB], v1[PB];
+  auto sum_pieces = [&](f32x4& a0, f32x4& a1) {
+    a0 = a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int z = 0; z < p.tail_s; z += PB) {
+      f32x4 v0[PB], v1[PB];
 #pragma unroll
-    for (int u = 0; u < PB; ++u) {
-      const bool ok = z + u < p.tail_s;
-      v0[u] = ok ? W0[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
-      v1[u] = ok ? W1[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int u = 0; u < PB; ++u) {
+        const bool ok = z + u < p.tail_s;
+        v0[u] = ok ? W0[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
+        v1[u] = ok ? W1[(int64_t)(z + u) * (32 * NT2)] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
-    for (int u = 0; u < PB; ++u) {
-      a0 += v0[u];
-      a1 += v1[u];
+      for (int u = 0; u < PB; ++u) {
+        a0 += v0[u];
+        a1 += v1[u];
+      }
     }
-  }
+  };
   const int64_t m = (int64_t)tm * BT + wr * 128 + rb * 16 + (lane & 15);
+  f32x4 a0, a1;
   if (GEGLU) {
+    sum_pieces(a0, a1);
     store_geglu4(p, 0, m, (int64_t)tn * (BT / 2) + wc * 32 + h * 16 + 4 * (lane >> 4), a0, a1);
   } else {
     const int64_t n = (int64_t)tn * BT + wc * 64 + 4 * (lane >> 4);
-    store_out4(p, 0, 0, m, n + c0 * 16, a0);
-    store_out4(p, 0, 0, m, n + c1 * 16, a1);
+    // the epilogue's side inputs (residual, saved activation, bias) issued with the first pieces, not after the sum
+    epi_dispatch(p, [&](auto em) {
+      constexpr int EM = decltype(em)::value;
+      Side s0, s1;
+      epi_load4<EM>(p, 0, 0, m, n + c0 * 16, s0);
+      epi_load4<EM>(p, 0, 0, m, n + c1 * 16, s1);
+      const u32x2 b0 = epi_load_bias(p, n + c0 * 16), b1 = epi_load_bias(p, n + c1 * 16);
+      sum_pieces(a0, a1);
+      epi_store4<EM>(p, 0, 0, m, n + c0 * 16, a0, s0, b0);
+      epi_store4<EM>(p, 0, 0, m, n + c1 * 16, a1, s1, b1);
+    });
   }
 }
 

@@ -266,13 +266,21 @@ __global__ void __launch_bounds__(256) splitk_epilogue_kernel(GemmP p, int S) {
     }
     return acc;
   };
-  const f32x4 s = sum_slabs(W);
   if (geglu) {
+    const f32x4 s = sum_slabs(W);
     const f32x4 u = sum_slabs(W + p.geglu_I);
     store_geglu4(p, 0, m, n, s, u);
-  } else {
-    store_out4(p, 0, 0, m, n, s);
+    return;
   }
+  // the epilogue's side inputs (residual, saved activation, bias) issued with the first slabs, not after their sum
+  epi_dispatch(p, [&](auto em) {
+    constexpr int EM = decltype(em)::value;
+    Side sd;
+    epi_load4<EM>(p, 0, 0, m, n, sd);
+    const u32x2 bias = epi_load_bias(p, n);
+    const f32x4 s = sum_slabs(W);
+    epi_store4<EM>(p, 0, 0, m, n, s, sd, bias);
+  });
 }
 
 // -------------------------------------------------------------------------
